@@ -1,0 +1,330 @@
+#!/usr/bin/env python3
+"""AES-GCM seal+open throughput of the MI355X record engine (BASELINE.json metric), device-resident.
+
+    python bench.py [--gpus N --steps K --warmup W] [--workload tls16k] [--extra quic1200] [--no-cpu-baseline]
+
+One step = seal the whole batch, then open the sealed batch again (one launch each), inputs already in HBM.
+value = (sum L sealed + sum L opened) over all ranks / max-over-ranks wall time of the K timed steps, in GiB/s
+(2^30 bytes). Multi-GPU (torchrun, one process per GPU): every rank seals/opens its own full batch (weak scaling,
+independent record shards, no collective on the data path; a barrier + max-reduce of the timings only).
+
+Also reported:
+  roofline      dominant kernel (seal), algorithmic bytes per launch / average launch time (HIP events on the
+                launch stream) against the 8 TB/s HBM peak of MI355X; traffic (PMC) from profiles/ when committed
+  cpu_baseline  picotls' own lib/fusion.c (oracle/_ref, compiled from the reference) sealing+opening a bounded sample
+                of the same workload on this host's cores (rank 0, N=1 only)
+  extra         the 1200-byte QUIC configuration (configs[2]) at full size
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md (8.0 TB/s spec)
+METRIC = "AES-GCM seal+open GiB/s (device-resident), 16KiB & 1200B record batches"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--workload", default="tls16k")
+    p.add_argument("--extra", default="quic1200", help="comma list of extra workloads to report ('' for none)")
+    p.add_argument("--records", type=int, default=0, help="override record count (smaller runs)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget of the cpu_baseline leg")
+    p.add_argument("--e2e", action="store_true", help="also time pinned-host -> H2D -> seal -> D2H (DESIGN.md)")
+    p.add_argument("--verify", type=int, default=1, help="verify round trip + fusion spot checks after timing")
+    return p.parse_args()
+
+
+class Rank:
+    def __init__(self, gpus: int):
+        import torch
+
+        self.torch = torch
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != gpus:
+            if self.world == 1 and gpus > 1:
+                raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
+        torch.cuda.set_device(self.local)
+        self.dev = torch.device("cuda", self.local)
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.init_process_group("nccl", device_id=self.dev)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if self.dist is None:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x: float) -> float:
+        if self.dist is None:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+
+def run_workload(R: Rank, wl, steps: int, warmup: int, verify: int, shard_global: bool):
+    import torch
+    import picotls_amd as pa
+    from picotls_amd.records import algorithmic_bytes
+    from picotls_amd.workloads import payload_torch
+
+    if shard_global:  # strong scaling: the global batch is split across ranks
+        per = wl.nrecs // R.world
+        begin = R.rank * per
+        end = wl.nrecs if R.rank == R.world - 1 else begin + per
+    else:  # weak scaling: every rank processes a full batch (its own records)
+        begin, end = 0, wl.nrecs
+    b = wl.descriptors(begin, end)
+    keys, ivs = wl.keys()
+    ks = pa.Keyset(keys, ivs, wl.key_size)
+    dev = R.dev
+    d_seal = torch.from_numpy(b.seal.view(np.uint8).copy()).to(dev)
+    d_open = torch.from_numpy(b.open.view(np.uint8).copy()).to(dev)
+    d_aad = torch.from_numpy(wl.aad_arena(b, begin)).to(dev)
+    d_pt = payload_torch(wl.seed + 7919 * (R.rank if not shard_global else 0), b.pt_bytes, dev)
+    d_sealed = torch.empty(b.sealed_bytes, dtype=torch.uint8, device=dev)
+    d_back = torch.empty(b.pt_bytes, dtype=torch.uint8, device=dev)
+    d_ok = torch.zeros(b.n, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    def seal():
+        pa.seal_batch(ks, d_seal.data_ptr(), b.n, d_pt.data_ptr(), d_aad.data_ptr(), d_sealed.data_ptr(), sp)
+
+    def open_():
+        pa.open_batch(ks, d_open.data_ptr(), b.n, d_sealed.data_ptr(), d_aad.data_ptr(), d_back.data_ptr(),
+                      d_ok.data_ptr(), sp)
+
+    for _ in range(warmup):
+        seal()
+        open_()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    torch.cuda.synchronize(dev)
+    R.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for e0, e1, e2 in ev:
+        e0.record(stream)
+        seal()
+        e1.record(stream)
+        open_()
+        e2.record(stream)
+    torch.cuda.synchronize(dev)
+    R.barrier()
+    t1 = time.perf_counter()
+    wall = t1 - t0
+    seal_ms = float(np.mean([a.elapsed_time(bb) for a, bb, _ in ev]))
+    open_ms = float(np.mean([bb.elapsed_time(c) for _, bb, c in ev]))
+
+    res = {"records": b.n, "payload_bytes": b.payload_bytes, "wall_s": wall, "seal_ms": seal_ms, "open_ms": open_ms}
+    lens = b.seal["len"]
+    res["seal_alg_bytes"] = algorithmic_bytes(lens, b.seal["aad_len"], True)
+    res["open_alg_bytes"] = algorithmic_bytes(lens, b.seal["aad_len"], False)
+
+    if verify:
+        ok_all = bool(d_ok.min().item() == 1) if b.n else True
+        same = bool(torch.equal(d_back, d_pt))
+        res["verified_roundtrip"] = ok_all and same
+        res["fusion_spot_check"] = spot_check(wl, b, keys, ivs, d_pt, d_aad, d_sealed, begin) if R.rank == 0 else None
+    del d_pt, d_sealed, d_back, d_ok, d_seal, d_open, d_aad
+    ks.free()
+    torch.cuda.empty_cache()
+    return res
+
+
+def spot_check(wl, b, keys, ivs, d_pt, d_aad, d_sealed, begin, nsample: int = 64):
+    """Compares nsample records sealed on the GPU with lib/fusion.c on the same inputs (bit-exact)."""
+    try:
+        from oracle import FusionRef
+
+        ref = FusionRef()
+    except Exception as e:  # the checker is optional for the timing, never for the tests
+        return f"skipped: {e}"
+    rng = np.random.default_rng(99)
+    idx = np.unique(np.concatenate([[0, b.n - 1], rng.integers(0, b.n, nsample)]))
+    sub = b.seal[idx].copy()
+    pt_parts, aad_parts, new_in, new_aad = [], [], [], []
+    off = aoff = 0
+    for r in sub:
+        ln, al = int(r["len"]), int(r["aad_len"])
+        pt_parts.append(d_pt[int(r["in_off"]):int(r["in_off"]) + ln].cpu().numpy())
+        aad_parts.append(d_aad[int(r["aad_off"]):int(r["aad_off"]) + al].cpu().numpy())
+        new_in.append(off)
+        new_aad.append(aoff)
+        off += ln + 16
+        aoff += al
+    recs = sub.copy()
+    recs["in_off"] = new_in
+    recs["out_off"] = new_in
+    recs["aad_off"] = new_aad
+    pt = np.concatenate(pt_parts + [np.zeros(16 * len(sub) + 1, np.uint8)])
+    aad = np.concatenate(aad_parts + [np.zeros(1, np.uint8)])
+    out = np.zeros(len(pt), np.uint8)
+    ref.run_batch(True, keys, ivs, wl.key_size, recs, pt, aad, out, nthreads=1)
+    for r, o in zip(sub, new_in):
+        ln = int(r["len"])
+        gpu = d_sealed[int(r["out_off"]):int(r["out_off"]) + ln + 16].cpu().numpy()
+        if not np.array_equal(gpu, out[o:o + ln + 16]):
+            return False
+    return True
+
+
+def cpu_baseline(wl, seconds: float):
+    """lib/fusion.c (the reference, compiled from /root/reference into oracle/_ref) on this host's cores."""
+    try:
+        from oracle import FusionRef
+
+        ref = FusionRef()
+    except Exception as e:
+        return {"value": None, "unit": "GiB/s", "cores": 0, "kind": "reference", "sample": f"unavailable: {e}"}
+    cpus = sorted(os.sched_getaffinity(0))
+    nthreads = len(cpus)
+    n = min(wl.nrecs, max(1, (256 << 20) // (wl.rec_len or 8192)))  # ~256 MiB sample of the same workload
+    b = wl.descriptors(0, n)
+    keys, ivs = wl.keys()
+    from picotls_amd.workloads import payload_np
+
+    pt = payload_np(wl.seed, 0, b.pt_bytes).copy()
+    aad = wl.aad_arena(b, 0)
+    sealed = np.zeros(b.sealed_bytes, np.uint8)
+    back = np.zeros(b.pt_bytes, np.uint8)
+    ok = np.zeros(b.n, np.uint8)
+    t_seal = t_open = 0.0
+    reps = 0
+    start = time.perf_counter()
+    while True:
+        ts, _ = ref.run_batch(True, keys, ivs, wl.key_size, b.seal, pt, aad, sealed, nthreads=nthreads, cpus=cpus)
+        to, fails = ref.run_batch(False, keys, ivs, wl.key_size, b.open, sealed, aad, back, ok=ok, nthreads=nthreads, cpus=cpus)
+        assert fails == 0
+        t_seal += ts
+        t_open += to
+        reps += 1
+        if time.perf_counter() - start > seconds or reps >= 50:
+            break
+    gib = 2 * b.payload_bytes * reps / 2**30
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(gib / (t_seal + t_open), 3), "unit": "GiB/s", "cores": nthreads, "kind": "reference",
+            "sample": f"{b.n} x {wl.rec_len or 'mixed'} B records of '{wl.name}' ({b.payload_bytes / 2**20:.0f} MiB), "
+                      f"seal+open x{reps}, ptls_fusion_aes{8 * wl.key_size}gcm via ptls_aead_encrypt/decrypt, "
+                      f"{nthreads} pinned threads, CLOCK_MONOTONIC; CPU: {model}",
+            "seal_GiBps": round(b.payload_bytes * reps / 2**30 / t_seal, 3),
+            "open_GiBps": round(b.payload_bytes * reps / 2**30 / t_open, 3)}
+
+
+def traffic_from_profiles(workload: str):
+    """Corrected HBM bytes per seal launch from the committed rocprofv3 PMC summary (profiles/*pmc*.json)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        return json.load(open(path)).get("seal_hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    from picotls_amd.workloads import WORKLOADS
+
+    R = Rank(args.gpus)
+    wl = WORKLOADS[args.workload]
+    if args.records:
+        wl = wl.scaled(args.records)
+    shard_global = args.workload == "shard1200"
+    res = run_workload(R, wl, args.steps, args.warmup, args.verify, shard_global)
+
+    wall = R.max(res["wall_s"])
+    total_payload = R.sum(float(res["payload_bytes"]))
+    value = 2 * total_payload * args.steps / wall / 2**30
+    seal_s, open_s = res["seal_ms"] / 1e3, res["open_ms"] / 1e3
+    achieved = res["seal_alg_bytes"] / seal_s / 1e9
+    out = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": R.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong" if shard_global else "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: splitmix64 payload (seed 0x5eed) generated on device; random-key AES-GCM",
+        "config": {"workload": wl.name, "desc": wl.desc, "records_per_gpu": res["records"],
+                   "record_len": wl.rec_len or "U[64,16384]", "aad_len": wl.aad_len,
+                   "aead": f"AES-{8 * wl.key_size}-GCM", "keys": wl.nkeys,
+                   "parallelism": f"{R.world} independent per-GPU record shards, no data-path collective"},
+        "seal_GiBps": round(res["payload_bytes"] / seal_s / 2**30, 3),
+        "open_GiBps": round(res["payload_bytes"] / open_s / 2**30, 3),
+        "roofline": {"bound": "hbm", "kernel": "gcm_batch_kernel<10,seal>" if wl.key_size == 16 else "gcm_batch_kernel<14,seal>",
+                     "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic_from_profiles(wl.name),
+                     "alg_bytes_per_launch": res["seal_alg_bytes"], "avg_launch_ms": round(res["seal_ms"], 4),
+                     "open_achieved": round(res["open_alg_bytes"] / open_s / 1e9, 2)},
+        "verified": {"roundtrip": res.get("verified_roundtrip"), "fusion_spot_check": res.get("fusion_spot_check")},
+    }
+    extra = {}
+    for name in [x for x in args.extra.split(",") if x]:
+        if name == args.workload:
+            continue
+        w2 = WORKLOADS[name]
+        if args.records:
+            w2 = w2.scaled(max(1, args.records * (wl.rec_len or 8192) // (w2.rec_len or 8192)))
+        r2 = run_workload(R, w2, args.steps, args.warmup, args.verify, name == "shard1200")
+        wall2 = R.max(r2["wall_s"])
+        tot2 = R.sum(float(r2["payload_bytes"]))
+        extra[name] = {"value": round(2 * tot2 * args.steps / wall2 / 2**30, 3), "unit": "GiB/s",
+                       "records_per_gpu": r2["records"], "record_len": w2.rec_len,
+                       "seal_GiBps": round(r2["payload_bytes"] / (r2["seal_ms"] / 1e3) / 2**30, 3),
+                       "open_GiBps": round(r2["payload_bytes"] / (r2["open_ms"] / 1e3) / 2**30, 3),
+                       "seal_achieved_GBps": round(r2["seal_alg_bytes"] / (r2["seal_ms"] / 1e3) / 1e9, 2),
+                       "seal_hbm_frac": round(r2["seal_alg_bytes"] / (r2["seal_ms"] / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                       "verified": {"roundtrip": r2.get("verified_roundtrip"),
+                                    "fusion_spot_check": r2.get("fusion_spot_check")}}
+    if extra:
+        out["extra"] = extra
+    if R.rank == 0 and R.world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds)
+    elif R.rank == 0:
+        out["cpu_baseline"] = None
+    if R.rank == 0:
+        print(json.dumps(out), flush=True)
+    if R.dist is not None:
+        R.dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

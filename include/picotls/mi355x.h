@@ -1,0 +1,137 @@
+/*
+ * picotls/mi355x.h -- MI355X (gfx950) AES-GCM record engine for picotls: the C-ABI drop-in boundary.
+ *
+ * Two layers, both plain C ABI (no HIP or torch types; device buffers are passed as void *, streams as void *
+ * holding a hipStream_t, NULL = the device's default stream):
+ *
+ * 1. The batch engine (libptls_mi355x.so). picotls has only per-record synchronous AEAD calls, so a GPU backend
+ *    adds one entry point that seals or opens N independent records in one launch. Each record of a batch gives
+ *    exactly what one picotls call gets, so batch results equal N independent calls:
+ *        ptls_mi355x_seal_batch(...)  record i  ==  ptls_aead_encrypt(ctx[key_idx], out+out_off, in+in_off, len, seq,
+ *                                                                    aad+aad_off, aad_len)
+ *                                     include/picotls.h:2102-2107 -> do_encrypt (fusion: lib/fusion.c:1136-1146 ->
+ *                                     ptls_fusion_aesgcm_encrypt :401)
+ *        ptls_mi355x_open_batch(...)  record i  ==  ptls_aead_decrypt(ctx[key_idx], out+out_off, in+in_off, len+16, seq,
+ *                                                                    aad+aad_off, aad_len) != SIZE_MAX
+ *                                     include/picotls.h:2160-2164 -> do_decrypt (fusion: lib/fusion.c:1154-1171 ->
+ *                                     ptls_fusion_aesgcm_decrypt :661)
+ *    A keyset replaces N ptls_aead_new_direct(algo, is_enc, key, iv) calls (lib/picotls.c:6553-6568; fusion's
+ *    aesgcm_setup lib/fusion.c:1189-1211 / new_aesgcm :985-1011): AES key schedule, H = E_K(0^128) and the H-power
+ *    tables are derived on the GPU. The static IV / do_set_iv semantics (lib/fusion.c:1173-1187,
+ *    ptls_aead_xor_iv lib/picotls.c:6576-6585) are ptls_mi355x_keyset_set_iv / _get_iv.
+ *
+ * 2. The picotls algorithm objects (libptls_mi355x_picotls.so, built where picotls.h is available):
+ *        extern ptls_aead_algorithm_t ptls_mi355x_aes128gcm, ptls_mi355x_aes256gcm;
+ *    the exact counterparts of ptls_fusion_aes128gcm / ptls_fusion_aes256gcm (lib/fusion.c:1236-1261), each call a
+ *    batch of one. They are declared in picotls/mi355x_picotls.h so that this header does not need picotls.h.
+ *
+ * Error behaviour follows the reference: sealing has no error path in picotls (fusion asserts on OOM,
+ * lib/fusion.c:1143); here invalid arguments / launch failures return a negative value. Opening reports a per-record
+ * ok byte (1 = tag verified) and, like fusion (lib/fusion.c:783-828), writes the plaintext even when the tag fails.
+ */
+#ifndef picotls_mi355x_h
+#define picotls_mi355x_h
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/**
+ * One record of a batch (40 bytes, little endian, 8-byte aligned array). Offsets are byte offsets into the arenas
+ * passed to the batch call.
+ *   seal: reads  in[in_off .. in_off+len)            plaintext
+ *         writes out[out_off .. out_off+len+16)      ciphertext || tag   (out may alias in)
+ *   open: reads  in[in_off .. in_off+len+16)         ciphertext || tag
+ *         writes out[out_off .. out_off+len)         plaintext            (out may alias in)
+ *   aad:  aad[aad_off .. aad_off+aad_len)
+ *   nonce = static_iv(key_idx) ^ (0^32 || seq big-endian)        (lib/picotls.c:6587-6601, lib/fusion.c:1127-1134)
+ */
+typedef struct st_ptls_mi355x_record_t {
+    uint64_t in_off;
+    uint64_t out_off;
+    uint64_t seq;
+    uint32_t aad_off;
+    uint32_t len;
+    uint32_t key_idx;
+    uint16_t aad_len;
+    uint16_t flags; /* reserved, must be 0 */
+} ptls_mi355x_record_t;
+
+#define PTLS_MI355X_RECORD_SIZE 40
+#define PTLS_MI355X_MAX_RECORD_LEN (1u << 24) /* 16 MiB; TLS caps records at 2^14 + 256 */
+
+typedef struct st_ptls_mi355x_keyset_t ptls_mi355x_keyset_t;
+
+/**
+ * Returns 1 when a gfx950 device is usable and the engine's code object loads, 0 otherwise.
+ */
+int ptls_mi355x_is_supported(void);
+
+/**
+ * Creates a keyset of nkeys AES-GCM traffic keys on the current HIP device.
+ * keys: nkeys * key_size bytes (host memory), ivs: nkeys * 12 bytes (host memory), key_size: 16 or 32.
+ * Returns NULL on invalid arguments or device failure.
+ */
+ptls_mi355x_keyset_t *ptls_mi355x_keyset_new(const void *keys, const void *ivs, size_t nkeys, size_t key_size);
+/**
+ * Destroys a keyset; device key material is cleared first (ptls_clear_memory, lib/fusion.c:1045).
+ */
+void ptls_mi355x_keyset_free(ptls_mi355x_keyset_t *ks);
+size_t ptls_mi355x_keyset_size(const ptls_mi355x_keyset_t *ks);
+size_t ptls_mi355x_keyset_key_size(const ptls_mi355x_keyset_t *ks);
+/**
+ * Static IV accessors (do_get_iv / do_set_iv, include/picotls.h:475-481). Return 0 on success.
+ */
+int ptls_mi355x_keyset_get_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, void *iv);
+int ptls_mi355x_keyset_set_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, const void *iv);
+
+/**
+ * Seals nrecs records in one launch. recs, in, aad, out are DEVICE pointers. Asynchronous on `stream`.
+ * Returns 0 on success, a negative value on invalid arguments or launch failure.
+ */
+int ptls_mi355x_seal_batch(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
+                           const void *aad, void *out, void *stream);
+/**
+ * Opens nrecs records in one launch; ok[i] = 1 when record i authenticated, 0 otherwise. DEVICE pointers.
+ */
+int ptls_mi355x_open_batch(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
+                           const void *aad, void *out, uint8_t *ok, void *stream);
+
+/**
+ * AES-ECB of nblocks 16-byte blocks, block i under key key_idx[i] (key_idx may be NULL: key 0). DEVICE pointers.
+ * The single-block cipher of fusion (ptls_fusion_aesecb_encrypt, lib/fusion.c:924) batched; QUIC header-protection
+ * masks are AES-ECB of the ciphertext sample (lib/fusion.c:1051-1101).
+ */
+int ptls_mi355x_ecb_batch(ptls_mi355x_keyset_t *ks, const uint32_t *key_idx, const void *in, void *out, size_t nblocks,
+                          void *stream);
+
+/**
+ * Synchronous single-record helpers on HOST buffers (a batch of one, with H2D/D2H copies). These back the picotls
+ * vtable (do_encrypt / do_decrypt) and mirror ptls_aead_encrypt / ptls_aead_decrypt: encrypt writes len+16 bytes;
+ * decrypt takes inlen = len+16 and returns the plaintext length or SIZE_MAX (tag mismatch or inlen < 16).
+ */
+int ptls_mi355x_encrypt(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const void *input, size_t inlen, uint64_t seq,
+                        const void *aad, size_t aadlen);
+size_t ptls_mi355x_decrypt(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const void *input, size_t inlen,
+                           uint64_t seq, const void *aad, size_t aadlen);
+
+/**
+ * One AES-ECB block on HOST buffers under key key_idx (ptls_fusion_aesecb_encrypt, lib/fusion.c:924). Backs the
+ * 16-byte AES-CTR cipher objects (ptls_fusion_aes128ctr equivalents, lib/fusion.c:1051-1101) used for QUIC header
+ * protection by the per-record vtable.
+ */
+int ptls_mi355x_encrypt_block(ptls_mi355x_keyset_t *ks, size_t key_idx, void *out, const void *in);
+
+/**
+ * Returns a static string describing the last error on this thread (or "" if none).
+ */
+const char *ptls_mi355x_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

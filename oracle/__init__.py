@@ -1,0 +1,183 @@
+"""TEST INFRASTRUCTURE ONLY -- the checkers for the MI355X AES-GCM record engine.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg import this package, and
+only to *check* or *time the reference*; the product (``picotls_amd``) never routes through it.
+
+Two checkers:
+
+* :class:`GcmOracle` -- ``oracle/gcm_ref.c``, a plain-C restatement of SP 800-38D AES-GCM with picotls' TLS 1.3
+  nonce rule (see the file header for the reference file:line each function follows).
+* :class:`FusionRef` -- picotls' own ``lib/fusion.c`` compiled unmodified from ``/root/reference`` by
+  ``oracle/Makefile`` into ``oracle/_ref/libfusion_ref.so`` (driven through ``ptls_aead_new_direct`` /
+  ``ptls_aead_encrypt`` / ``ptls_aead_decrypt``, ``t/ptlsbench.c:88-185``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF_DIR = os.path.join(HERE, "_ref")
+
+# numpy view of the 40-byte record descriptor (include/picotls/mi355x.h, ptls_mi355x_record_t)
+RECORD_DTYPE = np.dtype(
+    [
+        ("in_off", "<u8"),
+        ("out_off", "<u8"),
+        ("seq", "<u8"),
+        ("aad_off", "<u4"),
+        ("len", "<u4"),
+        ("key_idx", "<u4"),
+        ("aad_len", "<u2"),
+        ("flags", "<u2"),
+    ]
+)
+assert RECORD_DTYPE.itemsize == 40
+
+
+def build(force: bool = False) -> None:
+    """Builds oracle/_ref (the restatement always; lib/fusion.c only where /root/reference exists)."""
+    target = os.path.join(REF_DIR, "libgcm_oracle.so")
+    if force or not os.path.exists(target) or (
+        os.path.exists("/root/reference/lib/fusion.c") and not os.path.exists(os.path.join(REF_DIR, "libfusion_ref.so"))
+    ):
+        subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, (bytes, bytearray)):
+        a = np.frombuffer(a, dtype=np.uint8)
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class GcmOracle:
+    """ctypes front-end of oracle/gcm_ref.c."""
+
+    def __init__(self):
+        path = os.path.join(REF_DIR, "libgcm_oracle.so")
+        if not os.path.exists(path):
+            build()
+        lib = ctypes.CDLL(path)
+        vp, sz, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64
+        lib.oracle_aes_encrypt.argtypes = [vp, sz, vp, vp]
+        lib.oracle_gf128_mul.argtypes = [vp, vp, vp]
+        lib.oracle_ghash.argtypes = [vp, vp, vp, sz]
+        lib.oracle_gcm_seal.argtypes = [vp, sz, vp, u64, vp, sz, vp, sz, vp]
+        lib.oracle_gcm_open.argtypes = [vp, sz, vp, u64, vp, sz, vp, sz, vp]
+        lib.oracle_gcm_open.restype = sz
+        lib.oracle_seal_batch.argtypes = [vp, vp, sz, vp, sz, vp, vp, vp]
+        lib.oracle_open_batch.argtypes = [vp, vp, sz, vp, sz, vp, vp, vp, vp]
+        self.lib = lib
+
+    def aes_encrypt(self, key: bytes, block: bytes) -> bytes:
+        out = bytearray(16)
+        self.lib.oracle_aes_encrypt(_ptr(key), len(key), _ptr(out), _ptr(block))
+        return bytes(out)
+
+    def gf128_mul(self, x: bytes, y: bytes) -> bytes:
+        out = bytearray(16)
+        self.lib.oracle_gf128_mul(_ptr(out), _ptr(x), _ptr(y))
+        return bytes(out)
+
+    def ghash(self, h: bytes, data: bytes) -> bytes:
+        assert len(data) % 16 == 0
+        out = bytearray(16)
+        self.lib.oracle_ghash(_ptr(out), _ptr(h), _ptr(data) if data else None, len(data) // 16)
+        return bytes(out)
+
+    def seal(self, key: bytes, iv: bytes, seq: int, aad: bytes, pt: bytes) -> bytes:
+        out = bytearray(len(pt) + 16)
+        self.lib.oracle_gcm_seal(_ptr(key), len(key), _ptr(iv), seq, _ptr(aad) if aad else None, len(aad),
+                                 _ptr(pt) if pt else None, len(pt), _ptr(out))
+        return bytes(out)
+
+    def open(self, key: bytes, iv: bytes, seq: int, aad: bytes, ct_tag: bytes):
+        """Returns the plaintext, or None when the tag does not verify (ptls_aead_decrypt -> SIZE_MAX)."""
+        out = bytearray(max(len(ct_tag) - 16, 0) + 1)
+        r = self.lib.oracle_gcm_open(_ptr(key), len(key), _ptr(iv), seq, _ptr(aad) if aad else None, len(aad),
+                                     _ptr(ct_tag) if ct_tag else None, len(ct_tag), _ptr(out))
+        if r == ctypes.c_size_t(-1).value:
+            return None
+        return bytes(out[:r])
+
+    def seal_batch(self, keys, ivs, key_size, recs, in_arena, aad_arena, out_arena):
+        self.lib.oracle_seal_batch(_ptr(keys), _ptr(ivs), key_size, _ptr(recs), len(recs), _ptr(in_arena),
+                                   _ptr(aad_arena), _ptr(out_arena))
+
+    def open_batch(self, keys, ivs, key_size, recs, in_arena, aad_arena, out_arena, ok):
+        self.lib.oracle_open_batch(_ptr(keys), _ptr(ivs), key_size, _ptr(recs), len(recs), _ptr(in_arena),
+                                   _ptr(aad_arena), _ptr(out_arena), _ptr(ok))
+
+
+class FusionRef:
+    """ctypes front-end of picotls' lib/fusion.c (oracle/_ref/libfusion_ref.so, built from /root/reference)."""
+
+    def __init__(self):
+        path = os.path.join(REF_DIR, "libfusion_ref.so")
+        if not os.path.exists(path):
+            build()
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: build it with `make -C oracle` where /root/reference exists")
+        lib = ctypes.CDLL(path)
+        vp, sz, u64, ci = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int
+        lib.ref_cpu_supported.restype = ci
+        lib.ref_run_batch.argtypes = [ci, ci, vp, vp, sz, vp, sz, vp, vp, vp, vp, ci, vp, ctypes.POINTER(sz)]
+        lib.ref_run_batch.restype = ctypes.c_double
+        lib.ref_seal.argtypes = [vp, sz, vp, u64, vp, sz, vp, sz, vp]
+        lib.ref_open.argtypes = [vp, sz, vp, u64, vp, sz, vp, sz, vp]
+        lib.ref_open.restype = sz
+        lib.ref_fusion_raw_seal.argtypes = [vp, sz, vp, sz, vp, sz, vp]
+        lib.ref_seal_with_hp.argtypes = [vp, sz, vp, u64, vp, sz, vp, sz, vp, vp, sz, vp]
+        lib.ref_aesecb.argtypes = [vp, sz, vp, vp]
+        self.lib = lib
+        if not lib.ref_cpu_supported():
+            raise RuntimeError("host CPU lacks AES-NI/PCLMUL/AVX2: lib/fusion.c cannot run here")
+
+    def seal(self, key, iv, seq, aad, pt):
+        out = bytearray(len(pt) + 16)
+        self.lib.ref_seal(_ptr(key), len(key), _ptr(iv), seq, _ptr(aad) if aad else None, len(aad),
+                          _ptr(pt) if pt else None, len(pt), _ptr(out))
+        return bytes(out)
+
+    def open(self, key, iv, seq, aad, ct_tag):
+        out = bytearray(max(len(ct_tag) - 16, 0) + 1)
+        r = self.lib.ref_open(_ptr(key), len(key), _ptr(iv), seq, _ptr(aad) if aad else None, len(aad),
+                              _ptr(ct_tag) if ct_tag else None, len(ct_tag), _ptr(out))
+        if r == ctypes.c_size_t(-1).value:
+            return None
+        return bytes(out[:r])
+
+    def raw_seal_zero_ctr(self, key, pt, aad):
+        out = bytearray(len(pt) + 16)
+        self.lib.ref_fusion_raw_seal(_ptr(key), len(key), _ptr(pt) if pt else None, len(pt), _ptr(aad) if aad else None,
+                                     len(aad), _ptr(out))
+        return bytes(out)
+
+    def seal_with_hp(self, key, iv, seq, aad, pt, hp_key, sample_off):
+        out = bytearray(len(pt) + 16)
+        mask = bytearray(16)
+        self.lib.ref_seal_with_hp(_ptr(key), len(key), _ptr(iv), seq, _ptr(aad) if aad else None, len(aad),
+                                  _ptr(pt) if pt else None, len(pt), _ptr(out), _ptr(hp_key), sample_off, _ptr(mask))
+        return bytes(out), bytes(mask)
+
+    def aesecb(self, key, block):
+        out = bytearray(16)
+        self.lib.ref_aesecb(_ptr(key), len(key), _ptr(out), _ptr(block))
+        return bytes(out)
+
+    def run_batch(self, is_seal, keys, ivs, key_size, recs, in_arena, aad_arena, out_arena, ok=None, nthreads=1,
+                  cpus=None, nontemporal=False):
+        """Seal/open a whole batch with `nthreads` pinned threads; returns (seconds, failures)."""
+        fails = ctypes.c_size_t(0)
+        cpu_arr = None
+        if cpus is not None:
+            cpu_arr = np.asarray(cpus, dtype=np.int32)
+        t = self.lib.ref_run_batch(1 if is_seal else 0, 1 if nontemporal else 0, _ptr(keys), _ptr(ivs), key_size,
+                                   _ptr(recs), len(recs), _ptr(in_arena), _ptr(aad_arena), _ptr(out_arena), _ptr(ok),
+                                   nthreads, _ptr(cpu_arr), ctypes.byref(fails))
+        return t, fails.value

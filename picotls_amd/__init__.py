@@ -1,0 +1,258 @@
+"""picotls_amd -- MI355X-native AES-GCM record engine for picotls (Python host mirror of the C ABI).
+
+The product is the C ABI in ``include/picotls/mi355x.h`` (``libptls_mi355x.so``: hand-written gfx950 HIP kernels) and
+the picotls plugin objects in ``include/picotls/mi355x_picotls.h``. This module binds the same entry points with
+ctypes so that Python tests and ``bench.py`` drive exactly the code a C caller would, and mirrors picotls' AEAD
+operator interface (``include/picotls.h:519-580, 2082-2164``; ``lib/picotls.c:6547-6601``):
+
+* :data:`aes128gcm` / :data:`aes256gcm` -- algorithm descriptors (``ptls_mi355x_aes{128,256}gcm``)
+* :func:`aead_new_direct` -> :class:`AeadContext` with ``encrypt`` / ``encrypt_s`` / ``decrypt`` / ``get_iv`` /
+  ``set_iv`` / ``xor_iv`` (``decrypt`` returns ``None`` where picotls returns ``SIZE_MAX``)
+* :class:`Keyset`, :func:`seal_batch`, :func:`open_batch`, :func:`ecb_batch` -- the batch extension.
+
+There is no CPU fallback: when the shared object or a gfx950 device is missing every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from .records import RECORD_DTYPE, RecordBatch, shard_ranges  # noqa: F401
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "_lib", "libptls_mi355x.so")
+PICOTLS_LIB_PATH = os.path.join(_PKG, "_lib", "libptls_mi355x_picotls.so")
+
+# every function of include/picotls/mi355x.h (tests check the .so exports exactly these)
+ABI_FUNCTIONS = (
+    "ptls_mi355x_is_supported",
+    "ptls_mi355x_keyset_new",
+    "ptls_mi355x_keyset_free",
+    "ptls_mi355x_keyset_size",
+    "ptls_mi355x_keyset_key_size",
+    "ptls_mi355x_keyset_get_iv",
+    "ptls_mi355x_keyset_set_iv",
+    "ptls_mi355x_seal_batch",
+    "ptls_mi355x_open_batch",
+    "ptls_mi355x_ecb_batch",
+    "ptls_mi355x_encrypt",
+    "ptls_mi355x_decrypt",
+    "ptls_mi355x_encrypt_block",
+    "ptls_mi355x_last_error",
+)
+
+SIZE_MAX = ctypes.c_size_t(-1).value
+_lib = None
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Loads libptls_mi355x.so (no device calls). Raises if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise EngineError(f"{path} is missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                          "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    lib = ctypes.CDLL(path)
+    vp, sz, u64, ci = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int
+    lib.ptls_mi355x_is_supported.restype = ci
+    lib.ptls_mi355x_keyset_new.argtypes = [vp, vp, sz, sz]
+    lib.ptls_mi355x_keyset_new.restype = vp
+    lib.ptls_mi355x_keyset_free.argtypes = [vp]
+    lib.ptls_mi355x_keyset_size.argtypes = [vp]
+    lib.ptls_mi355x_keyset_size.restype = sz
+    lib.ptls_mi355x_keyset_key_size.argtypes = [vp]
+    lib.ptls_mi355x_keyset_key_size.restype = sz
+    lib.ptls_mi355x_keyset_get_iv.argtypes = [vp, sz, vp]
+    lib.ptls_mi355x_keyset_set_iv.argtypes = [vp, sz, vp]
+    lib.ptls_mi355x_seal_batch.argtypes = [vp, vp, sz, vp, vp, vp, vp]
+    lib.ptls_mi355x_open_batch.argtypes = [vp, vp, sz, vp, vp, vp, vp, vp]
+    lib.ptls_mi355x_ecb_batch.argtypes = [vp, vp, vp, vp, sz, vp]
+    lib.ptls_mi355x_encrypt.argtypes = [vp, sz, vp, vp, sz, u64, vp, sz]
+    lib.ptls_mi355x_decrypt.argtypes = [vp, sz, vp, vp, sz, u64, vp, sz]
+    lib.ptls_mi355x_decrypt.restype = sz
+    lib.ptls_mi355x_encrypt_block.argtypes = [vp, sz, vp, vp]
+    lib.ptls_mi355x_last_error.restype = ctypes.c_char_p
+    _lib = lib
+    return lib
+
+
+def _err(what: str) -> EngineError:
+    msg = load_library().ptls_mi355x_last_error()
+    return EngineError(f"{what}: {msg.decode() if msg else 'unknown error'}")
+
+
+def is_supported() -> bool:
+    return bool(load_library().ptls_mi355x_is_supported())
+
+
+def _buf(b) -> ctypes.c_void_p | None:
+    if b is None or len(b) == 0:
+        return None
+    if isinstance(b, bytes):
+        return ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p)
+    if isinstance(b, bytearray):
+        return ctypes.c_void_p(ctypes.addressof((ctypes.c_char * len(b)).from_buffer(b)))
+    if isinstance(b, np.ndarray):
+        return ctypes.c_void_p(b.ctypes.data)
+    raise TypeError(type(b))
+
+
+# ------------------------------------------------------------------------------------------------ keysets / batches
+
+
+class Keyset:
+    """N AES-GCM traffic keys resident on the current device (ptls_mi355x_keyset_new)."""
+
+    def __init__(self, keys: bytes | np.ndarray, ivs: bytes | np.ndarray, key_size: int):
+        lib = load_library()
+        keys = np.frombuffer(bytes(keys), dtype=np.uint8) if not isinstance(keys, np.ndarray) else np.ascontiguousarray(keys, np.uint8)
+        ivs = np.frombuffer(bytes(ivs), dtype=np.uint8) if not isinstance(ivs, np.ndarray) else np.ascontiguousarray(ivs, np.uint8)
+        if key_size not in (16, 32) or keys.size % key_size or ivs.size != keys.size // key_size * 12:
+            raise ValueError("keys must be n*key_size bytes and ivs n*12 bytes")
+        self.n = keys.size // key_size
+        self.key_size = key_size
+        h = lib.ptls_mi355x_keyset_new(_buf(keys), _buf(ivs), self.n, key_size)
+        if not h:
+            raise _err("ptls_mi355x_keyset_new")
+        self.handle = ctypes.c_void_p(h)
+
+    def free(self):
+        if getattr(self, "handle", None):
+            load_library().ptls_mi355x_keyset_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def get_iv(self, idx: int = 0) -> bytes:
+        out = bytearray(12)
+        if load_library().ptls_mi355x_keyset_get_iv(self.handle, idx, _buf(out)) != 0:
+            raise _err("get_iv")
+        return bytes(out)
+
+    def set_iv(self, iv: bytes, idx: int = 0) -> None:
+        if load_library().ptls_mi355x_keyset_set_iv(self.handle, idx, _buf(bytes(iv))) != 0:
+            raise _err("set_iv")
+
+
+def seal_batch(ks: Keyset, recs_ptr: int, nrecs: int, in_ptr: int, aad_ptr: int, out_ptr: int, stream: int = 0) -> None:
+    """Device pointers (ints, e.g. torch ``tensor.data_ptr()``); asynchronous on ``stream`` (a hipStream_t)."""
+    if load_library().ptls_mi355x_seal_batch(ks.handle, recs_ptr, nrecs, in_ptr, aad_ptr or None, out_ptr, stream or None) != 0:
+        raise _err("ptls_mi355x_seal_batch")
+
+
+def open_batch(ks: Keyset, recs_ptr: int, nrecs: int, in_ptr: int, aad_ptr: int, out_ptr: int, ok_ptr: int,
+               stream: int = 0) -> None:
+    if load_library().ptls_mi355x_open_batch(ks.handle, recs_ptr, nrecs, in_ptr, aad_ptr or None, out_ptr, ok_ptr,
+                                             stream or None) != 0:
+        raise _err("ptls_mi355x_open_batch")
+
+
+def ecb_batch(ks: Keyset, key_idx_ptr: int, in_ptr: int, out_ptr: int, nblocks: int, stream: int = 0) -> None:
+    if load_library().ptls_mi355x_ecb_batch(ks.handle, key_idx_ptr or None, in_ptr, out_ptr, nblocks, stream or None) != 0:
+        raise _err("ptls_mi355x_ecb_batch")
+
+
+# ------------------------------------------------------------------------------------------------ picotls mirror
+
+
+@dataclass(frozen=True)
+class AeadAlgorithm:
+    """Mirror of ptls_aead_algorithm_t (include/picotls.h:519-580) for ptls_mi355x_aes{128,256}gcm."""
+
+    name: str
+    key_size: int
+    iv_size: int = 12
+    tag_size: int = 16
+    confidentiality_limit: int = 0x2000000  # PTLS_AESGCM_CONFIDENTIALITY_LIMIT, include/picotls.h:89
+    integrity_limit: int = 0x40000000000000  # PTLS_AESGCM_INTEGRITY_LIMIT, include/picotls.h:90
+    tls12_fixed_iv_size: int = 0
+    tls12_record_iv_size: int = 0
+    non_temporal: int = 0
+    align_bits: int = 0
+
+
+aes128gcm = AeadAlgorithm("AES128-GCM", 16)
+aes256gcm = AeadAlgorithm("AES256-GCM", 32)
+
+
+class AeadContext:
+    """Mirror of ptls_aead_context_t created by ptls_aead_new_direct (lib/picotls.c:6553-6568)."""
+
+    def __init__(self, algo: AeadAlgorithm, is_enc: bool, key: bytes, iv: bytes):
+        if len(key) != algo.key_size or len(iv) != algo.iv_size:
+            raise ValueError("key / iv size mismatch")
+        self.algo = algo
+        self.is_enc = is_enc
+        self._iv = bytes(iv)
+        self.ks = Keyset(key, iv, algo.key_size)
+
+    def free(self):
+        self.ks.free()
+
+    # do_get_iv / do_set_iv / ptls_aead_xor_iv (lib/picotls.c:6576-6585)
+    def get_iv(self) -> bytes:
+        return self._iv
+
+    def set_iv(self, iv: bytes) -> None:
+        self._iv = bytes(iv)
+        self.ks.set_iv(self._iv)
+
+    def xor_iv(self, data: bytes) -> None:
+        iv = bytearray(self._iv)
+        for i, b in enumerate(data):
+            iv[i] ^= b
+        self.set_iv(bytes(iv))
+
+    # ptls_aead_encrypt (include/picotls.h:2102-2107): returns ciphertext || tag
+    def encrypt(self, pt: bytes, seq: int, aad: bytes = b"") -> bytes:
+        out = bytearray(len(pt) + self.algo.tag_size)
+        if load_library().ptls_mi355x_encrypt(self.ks.handle, 0, _buf(out), _buf(bytes(pt)), len(pt), seq,
+                                             _buf(bytes(aad)), len(aad)) != 0:
+            raise _err("ptls_mi355x_encrypt")
+        return bytes(out)
+
+    # ptls_aead_encrypt_s with a header-protection cipher (include/picotls.h:2109-2113, lib/fusion.c:425-430,636-651)
+    def encrypt_s(self, pt: bytes, seq: int, aad: bytes, hp: "CtrCipher", sample_off: int) -> tuple[bytes, bytes]:
+        sealed = self.encrypt(pt, seq, aad)
+        sample = sealed[sample_off:sample_off + 16]
+        return sealed, hp.mask(sample)
+
+    # ptls_aead_decrypt (include/picotls.h:2160-2164): plaintext, or None for SIZE_MAX
+    def decrypt(self, ct_tag: bytes, seq: int, aad: bytes = b"") -> bytes | None:
+        if len(ct_tag) < 16:
+            return None
+        out = bytearray(len(ct_tag) - 16 + 1)
+        r = load_library().ptls_mi355x_decrypt(self.ks.handle, 0, _buf(out), _buf(bytes(ct_tag)), len(ct_tag), seq,
+                                               _buf(bytes(aad)), len(aad))
+        if r == SIZE_MAX:
+            return None
+        return bytes(out[:r])
+
+
+class CtrCipher:
+    """Mirror of ptls_mi355x_aes{128,256}ctr (fusion's 16-byte AES-CTR, lib/fusion.c:1051-1101)."""
+
+    def __init__(self, key: bytes):
+        self.ks = Keyset(key, bytes(12), len(key))
+
+    def mask(self, iv16: bytes) -> bytes:
+        out = bytearray(16)
+        if load_library().ptls_mi355x_encrypt_block(self.ks.handle, 0, _buf(out), _buf(bytes(iv16))) != 0:
+            raise _err("ptls_mi355x_encrypt_block")
+        return bytes(out)
+
+
+def aead_new_direct(algo: AeadAlgorithm, is_enc: bool, key: bytes, iv: bytes) -> AeadContext:
+    return AeadContext(algo, is_enc, key, iv)

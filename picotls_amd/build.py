@@ -1,0 +1,67 @@
+"""Builds the engine's shared objects in-tree (they travel to the GPU box with the repo snapshot).
+
+  picotls_amd/_lib/libptls_mi355x.so          HIP kernels + C ABI (include/picotls/mi355x.h), hipcc --offload-arch=gfx950
+  picotls_amd/_lib/libptls_mi355x_picotls.so  the ptls_aead_algorithm_t objects (C, gcc), only where picotls.h exists
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+LIB_DIR = os.path.join(PKG, "_lib")
+ENGINE_SO = os.path.join(LIB_DIR, "libptls_mi355x.so")
+PICOTLS_SO = os.path.join(LIB_DIR, "libptls_mi355x_picotls.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+PICOTLS_INCLUDE = os.environ.get("PICOTLS_INCLUDE", "/root/reference/include")
+
+ENGINE_SRCS = [os.path.join(PKG, "csrc", "aesgcm_engine.hip")]
+PICOTLS_SRCS = [os.path.join(PKG, "csrc", "ptls_mi355x.c")]
+HEADERS = [os.path.join(ROOT, "include", "picotls", "mi355x.h"), os.path.join(ROOT, "include", "picotls", "mi355x_picotls.h")]
+
+
+def _stale(target: str, deps: list[str]) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
+
+
+def build_engine(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(LIB_DIR, exist_ok=True)
+    if force or _stale(ENGINE_SO, ENGINE_SRCS + HEADERS):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
+               "-Wno-unused-value", "-I", os.path.join(ROOT, "include"), *ENGINE_SRCS, "-o", ENGINE_SO + ".tmp"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        os.replace(ENGINE_SO + ".tmp", ENGINE_SO)
+    return ENGINE_SO
+
+
+def build_picotls_backend(force: bool = False, verbose: bool = False) -> str | None:
+    """The picotls vtable adapter needs picotls.h at build time (a picotls installation; here the reference tree)."""
+    if not os.path.exists(os.path.join(PICOTLS_INCLUDE, "picotls.h")):
+        return PICOTLS_SO if os.path.exists(PICOTLS_SO) else None
+    if force or _stale(PICOTLS_SO, PICOTLS_SRCS + HEADERS + [ENGINE_SO]):
+        cc = shutil.which("gcc") or "cc"
+        cmd = [cc, "-std=gnu99", "-O2", "-fPIC", "-shared", "-Wall", "-I", os.path.join(ROOT, "include"), "-I",
+               PICOTLS_INCLUDE, *PICOTLS_SRCS, "-L", LIB_DIR, "-lptls_mi355x", "-Wl,-rpath,$ORIGIN",
+               "-o", PICOTLS_SO + ".tmp"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        os.replace(PICOTLS_SO + ".tmp", PICOTLS_SO)
+    return PICOTLS_SO
+
+
+def build(force: bool = False, verbose: bool = False) -> None:
+    build_engine(force, verbose)
+    build_picotls_backend(force, verbose)
+
+
+if __name__ == "__main__":
+    build(force=True, verbose=True)

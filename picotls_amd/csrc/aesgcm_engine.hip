@@ -1,0 +1,831 @@
+// picotls_amd/csrc/aesgcm_engine.hip -- MI355X (gfx950 / CDNA4) AES-GCM record engine: HIP kernels + the C ABI
+// declared in include/picotls/mi355x.h.
+//
+// What it replaces: picotls' fusion AES-GCM engine (lib/fusion.c:401-845 seal/open, :847-929 AES core and key
+// schedule, :114-321 + :934-1011 GHASH and H-power tables), re-designed for a GPU: one launch seals or opens a
+// whole batch of independent records.
+//
+// Design (DESIGN.md has the numbers):
+//   * one persistent 1024-thread workgroup per CU; G = 8 lanes of a wavefront work on one record, so a wave holds 8
+//     records and lane j of a record handles GHASH stream positions j, j+G, j+2G, ... (the stream is
+//     [zero padding | AAD blocks | ciphertext blocks | length block], front-padded to a multiple of G, which leaves
+//     GHASH unchanged). A record's ciphertext block b sits at one stream position, so the lane that runs AES-CTR
+//     on counter 2+b is the lane that folds that block into its GHASH accumulator: no data exchange.
+//   * AES: T-table rounds from LDS. Te0 and Te2 (= rotl16 Te0) are replicated into all 32 banks
+//     (entry n at n*256 + bank*4, Te2 at +128): lane l always reads bank l%32, so every ds_read_b32 is
+//     conflict-free; Te1/Te3 are one v_alignbit away. The byte -> LDS address step is a single v_perm_b32.
+//   * GHASH: 4-bit-window tables in LDS. For each H power one table = 32 windows x 16 entries x 16 B (8 KiB);
+//     the 16 entries of a window fill exactly one 256-byte LDS bank row, so a ds_read_b128 of 16 lanes never
+//     conflicts (equal entries broadcast). A product X*H^k is the XOR of 32 table entries; the reduction is baked
+//     into the tables. Horner with stride H^G on every step except the last, where lane j multiplies by H^(G-j)
+//     instead; an XOR over the G lanes then gives GHASH. Tables for H^1..H^G (64 KiB) are built on chip from the
+//     keyset's H powers at kernel start.
+//   * Data path: 16-byte unaligned-capable global loads/stores (unaligned access mode is on for gfx950), G lanes
+//     of a record touch G*16 contiguous bytes per step. Partial first/last blocks use byte accesses so nothing
+//     outside [in_off, in_off+len) / [out_off, out_off+len+16) is touched.
+//
+// All word-level state is kept in "LE column" form: a 16-byte block is 4 little-endian u32 words, word c = bytes
+// 4c..4c+3 = AES state column c. GHASH elements use the same byte order (byte 0 holds x^0..x^7, MSB first).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <stdio.h>
+
+#include "picotls/mi355x.h"
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef u32x4 __attribute__((aligned(1))) u32x4_u;
+
+static_assert(sizeof(ptls_mi355x_record_t) == PTLS_MI355X_RECORD_SIZE, "record descriptor must be 40 bytes");
+
+// ------------------------------------------------------------------------------------------------ constants
+
+namespace {
+
+struct SboxTable {
+    uint8_t v[256];
+};
+
+constexpr uint8_t xtime_c(uint8_t a) { return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0)); }
+
+// FIPS-197 S-box derived at compile time: multiplicative inverse via exp/log tables of generator 3, then the
+// affine transform.
+constexpr SboxTable make_sbox()
+{
+    uint8_t exp_t[256] = {}, log_t[256] = {};
+    uint8_t x = 1;
+    for (int i = 0; i < 255; ++i) {
+        exp_t[i] = x;
+        log_t[x] = (uint8_t)i;
+        x = (uint8_t)(x ^ xtime_c(x));  // x * 3
+    }
+    SboxTable t = {};
+    for (int v = 0; v < 256; ++v) {
+        uint8_t inv = v == 0 ? 0 : exp_t[(255 - log_t[v]) % 255];
+        uint8_t s = inv;
+        for (int k = 1; k <= 4; ++k)
+            s ^= (uint8_t)((inv << k) | (inv >> (8 - k)));
+        t.v[v] = (uint8_t)(s ^ 0x63);
+    }
+    return t;
+}
+
+}  // namespace
+
+__constant__ SboxTable c_sbox = make_sbox();
+
+// one keyset entry in HBM (512 bytes, 16-byte aligned)
+struct KeyEntry {
+    u32 rk[15][4];  // round keys, LE column words
+    u32 iv[4];      // static IV as LE words (word 3 = 0)
+    u32 h[16][4];   // H^1 .. H^16 as GHASH elements (LE words)
+};
+static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
+
+#define ENGINE_G 8                 // lanes per record
+#define ENGINE_WG 1024             // threads per workgroup
+#define LDS_AES_BYTES 65536        // Te0/Te2, 32-bank replicated
+#define GHASH_TABLE_BYTES 8192     // 32 windows x 16 entries x 16 B
+#define LDS_BYTES (LDS_AES_BYTES + ENGINE_G * GHASH_TABLE_BYTES)
+#define LDS_ALLOC (LDS_BYTES + 16)  // + scratch word for the key-run scan
+
+// ------------------------------------------------------------------------------------------------ small helpers
+
+__device__ __forceinline__ u32 bswap32(u32 x) { return __builtin_bswap32(x); }
+__device__ __forceinline__ u32 rotl8(u32 x) { return __builtin_amdgcn_alignbit(x, x, 24); }
+__device__ __forceinline__ u32 xor3(u32 a, u32 b, u32 c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+
+// GF(2^128) * x on a GHASH element held as big-endian words (b0 most significant; bit 127 of the integer is x^0)
+__device__ __forceinline__ void gf_mulx_be(u32 &b0, u32 &b1, u32 &b2, u32 &b3)
+{
+    u32 lsb = b3 & 1;
+    b3 = (b3 >> 1) | (b2 << 31);
+    b2 = (b2 >> 1) | (b1 << 31);
+    b1 = (b1 >> 1) | (b0 << 31);
+    b0 = (b0 >> 1) ^ (lsb ? 0xe1000000u : 0u);
+}
+
+// ------------------------------------------------------------------------------------------------ keyset setup
+
+__device__ __forceinline__ u32 sub_word(u32 w)
+{
+    return (u32)c_sbox.v[w & 0xff] | (u32)c_sbox.v[(w >> 8) & 0xff] << 8 | (u32)c_sbox.v[(w >> 16) & 0xff] << 16 |
+           (u32)c_sbox.v[w >> 24] << 24;
+}
+
+__device__ __forceinline__ u32 xtime_w(u32 w) { return ((w & 0x7f7f7f7fu) << 1) ^ (((w >> 7) & 0x01010101u) * 0x1bu); }
+
+// plain word-level AES (setup only: H = E_K(0^128))
+__device__ void aes_plain(const u32 (*rk)[4], int nr, u32 s[4])
+{
+    for (int c = 0; c < 4; ++c)
+        s[c] ^= rk[0][c];
+    for (int r = 1; r <= nr; ++r) {
+        u32 t[4];
+        for (int c = 0; c < 4; ++c)
+            t[c] = sub_word(s[c]);
+        for (int c = 0; c < 4; ++c)
+            s[c] = (t[c] & 0xff) | (t[(c + 1) & 3] & 0xff00) | (t[(c + 2) & 3] & 0xff0000) | (t[(c + 3) & 3] & 0xff000000);
+        if (r != nr) {
+            for (int c = 0; c < 4; ++c) {
+                u32 w = s[c], r1 = (w >> 8) | (w << 24), r2 = (w >> 16) | (w << 16), r3 = (w >> 24) | (w << 8);
+                s[c] = xtime_w(w ^ r1) ^ r1 ^ r2 ^ r3;
+            }
+        }
+        for (int c = 0; c < 4; ++c)
+            s[c] ^= rk[r][c];
+    }
+}
+
+// one thread per key: FIPS-197 key expansion, H = E_K(0), H^1..H^16, static IV
+__global__ void keyset_setup_kernel(const uint8_t *__restrict__ keys, const uint8_t *__restrict__ ivs, KeyEntry *__restrict__ out,
+                                    u32 nkeys, u32 key_size)
+{
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nkeys)
+        return;
+    const int nk = (int)key_size / 4, nr = nk + 6;
+    u32 w[60];
+    const uint8_t *k = keys + (size_t)i * key_size;
+    for (int j = 0; j < nk; ++j)
+        w[j] = (u32)k[4 * j] | (u32)k[4 * j + 1] << 8 | (u32)k[4 * j + 2] << 16 | (u32)k[4 * j + 3] << 24;
+    u32 rcon = 1;
+    for (int j = nk; j < 4 * (nr + 1); ++j) {
+        u32 t = w[j - 1];
+        if (j % nk == 0) {
+            t = sub_word((t >> 8) | (t << 24)) ^ rcon;
+            rcon = (rcon << 1) ^ ((rcon & 0x80) ? 0x1b : 0);
+        } else if (nk > 6 && j % nk == 4) {
+            t = sub_word(t);
+        }
+        w[j] = w[j - nk] ^ t;
+    }
+    KeyEntry *e = out + i;
+    u32 rk[15][4];
+    for (int r = 0; r < 15; ++r)
+        for (int c = 0; c < 4; ++c)
+            rk[r][c] = r <= nr ? w[4 * r + c] : 0;
+    for (int r = 0; r < 15; ++r)
+        for (int c = 0; c < 4; ++c)
+            e->rk[r][c] = rk[r][c];
+    const uint8_t *v = ivs + (size_t)i * 12;
+    for (int c = 0; c < 3; ++c)
+        e->iv[c] = (u32)v[4 * c] | (u32)v[4 * c + 1] << 8 | (u32)v[4 * c + 2] << 16 | (u32)v[4 * c + 3] << 24;
+    e->iv[3] = 0;
+
+    u32 s[4] = {0, 0, 0, 0};
+    aes_plain(rk, nr, s);
+    // H as big-endian words for the bitwise multiply (SP 800-38D Algorithm 1)
+    const u32 h0 = bswap32(s[0]), h1 = bswap32(s[1]), h2 = bswap32(s[2]), h3 = bswap32(s[3]);
+    u32 p0 = h0, p1 = h1, p2 = h2, p3 = h3;  // current power
+    for (int n = 0; n < 16; ++n) {
+        e->h[n][0] = bswap32(p0), e->h[n][1] = bswap32(p1), e->h[n][2] = bswap32(p2), e->h[n][3] = bswap32(p3);
+        // p = p * H
+        u32 z0 = 0, z1 = 0, z2 = 0, z3 = 0, v0 = h0, v1 = h1, v2 = h2, v3 = h3;
+        u32 x[4] = {p0, p1, p2, p3};
+        for (int b = 0; b < 128; ++b) {
+            if ((x[b >> 5] >> (31 - (b & 31))) & 1)
+                z0 ^= v0, z1 ^= v1, z2 ^= v2, z3 ^= v3;
+            gf_mulx_be(v0, v1, v2, v3);
+        }
+        p0 = z0, p1 = z1, p2 = z2, p3 = z3;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ LDS tables
+
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) u32 lds_u32;
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+
+// AES T-table: Te0 replicated into banks 0..31 (bytes 0..127 of row n), Te2 = rotl16(Te0) into bytes 128..255
+__device__ void build_aes_tables(lds_u8 *lds)
+{
+    lds_u32 *t = (lds_u32 *)lds;
+    for (u32 idx = threadIdx.x; idx < 256 * 64; idx += blockDim.x) {
+        u32 n = idx >> 6, slot = idx & 63;
+        u32 s = c_sbox.v[n];
+        u32 s2 = ((s << 1) ^ ((s & 0x80) ? 0x1b : 0)) & 0xff;
+        u32 te0 = s2 | s << 8 | s << 16 | (s2 ^ s) << 24;
+        t[idx] = slot < 32 ? te0 : ((te0 << 16) | (te0 >> 16));
+    }
+}
+
+// GHASH tables for H^1..H^G of one key: table t (H^(t+1)), window p (x^(4p)..x^(4p+3)), entry n (4-bit value, MSB
+// = coefficient of x^(4p)) = sum over set bits of n of x^(4p+q) * H^(t+1). Thread (t, p, q) computes
+// V_q = x^(4p+q) * H^(t+1) and, via shuffles with its 3 window neighbours, entries n = 4q .. 4q+3.
+__device__ void build_ghash_tables(lds_u8 *lds, const KeyEntry *__restrict__ key)
+{
+    for (u32 idx = threadIdx.x; idx < ENGINE_G * 128; idx += blockDim.x) {
+        u32 t = idx >> 7, i = idx & 127, p = i >> 2, q = i & 3;
+        u32 b0 = bswap32(key->h[t][0]), b1 = bswap32(key->h[t][1]), b2 = bswap32(key->h[t][2]), b3 = bswap32(key->h[t][3]);
+        for (u32 k = 0; k < i; ++k)
+            gf_mulx_be(b0, b1, b2, b3);
+        u32 v[4][4];
+        const int base = (threadIdx.x & 63) & ~3;
+        for (int m = 0; m < 4; ++m) {
+            v[m][0] = __shfl(b0, base + m, 64);
+            v[m][1] = __shfl(b1, base + m, 64);
+            v[m][2] = __shfl(b2, base + m, 64);
+            v[m][3] = __shfl(b3, base + m, 64);
+        }
+        lds_u32x4 *row = (lds_u32x4 *)(lds + LDS_AES_BYTES + t * GHASH_TABLE_BYTES + p * 256);
+        for (u32 n = 4 * q; n < 4 * q + 4; ++n) {
+            u32 e0 = 0, e1 = 0, e2 = 0, e3 = 0;
+            for (int m = 0; m < 4; ++m) {
+                if ((n >> (3 - m)) & 1) {
+                    e0 ^= v[m][0], e1 ^= v[m][1], e2 ^= v[m][2], e3 ^= v[m][3];
+                }
+            }
+            u32x4 ent = {bswap32(e0), bswap32(e1), bswap32(e2), bswap32(e3)};
+            row[n] = ent;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ AES (T-table)
+
+// LDS byte address of Te0[byte r of w] in this lane's bank: byte0 = bank*4 (from laneoff), byte1 = byte r of w.
+#define TE_ADDR(w, r, laneoff) __builtin_amdgcn_perm((w), (laneoff), 0x0c0c0000u | ((4u + (r)) << 8))
+
+__device__ __forceinline__ u32 te0(const lds_u8 *lds, u32 w, int r, u32 laneoff)
+{
+    return *(const lds_u32 *)(lds + TE_ADDR(w, r, laneoff));
+}
+__device__ __forceinline__ u32 te2(const lds_u8 *lds, u32 w, int r, u32 laneoff)
+{
+    return *(const lds_u32 *)(lds + TE_ADDR(w, r, laneoff) + 128);
+}
+
+template <int NR>
+__device__ __forceinline__ void aes_encrypt_tt(const lds_u8 *lds, u32 laneoff, const u32 (*rk)[4], u32 &s0, u32 &s1, u32 &s2,
+                                               u32 &s3)
+{
+#pragma unroll
+    for (int r = 1; r < NR; ++r) {
+        u32 t0 = xor3(te0(lds, s0, 0, laneoff), te2(lds, s2, 2, laneoff), rk[r][0]) ^
+                 rotl8(te0(lds, s1, 1, laneoff) ^ te2(lds, s3, 3, laneoff));
+        u32 t1 = xor3(te0(lds, s1, 0, laneoff), te2(lds, s3, 2, laneoff), rk[r][1]) ^
+                 rotl8(te0(lds, s2, 1, laneoff) ^ te2(lds, s0, 3, laneoff));
+        u32 t2 = xor3(te0(lds, s2, 0, laneoff), te2(lds, s0, 2, laneoff), rk[r][2]) ^
+                 rotl8(te0(lds, s3, 1, laneoff) ^ te2(lds, s1, 3, laneoff));
+        u32 t3 = xor3(te0(lds, s3, 0, laneoff), te2(lds, s1, 2, laneoff), rk[r][3]) ^
+                 rotl8(te0(lds, s0, 1, laneoff) ^ te2(lds, s2, 3, laneoff));
+        s0 = t0, s1 = t1, s2 = t2, s3 = t3;
+    }
+    // last round: SubBytes + ShiftRows + AddRoundKey; S(x) is byte 1/2 of Te0[x] and byte 0/3 of Te2[x]
+    u32 a, b, c, d, x, y, o[4];
+    const u32 st[4] = {s0, s1, s2, s3};
+#pragma unroll
+    for (int col = 0; col < 4; ++col) {
+        a = te2(lds, st[col], 0, laneoff);
+        b = te0(lds, st[(col + 1) & 3], 1, laneoff);
+        c = te0(lds, st[(col + 2) & 3], 2, laneoff);
+        d = te2(lds, st[(col + 3) & 3], 3, laneoff);
+        x = __builtin_amdgcn_perm(b, a, 0x0c0c0500u);
+        y = __builtin_amdgcn_perm(d, c, 0x07020c0cu);
+        o[col] = __builtin_amdgcn_bitop3_b32(x, y, rk[NR][col], 0x56);  // (x | y) ^ rk
+    }
+    s0 = o[0], s1 = o[1], s2 = o[2], s3 = o[3];
+}
+
+// ------------------------------------------------------------------------------------------------ GHASH (tables)
+
+// returns a * H^(t+1), where tsel = 0x10000 | (t * 8192): table base for the lane
+__device__ __forceinline__ u32x4 gmul_tab(const lds_u8 *lds, u32x4 a, u32 tsel)
+{
+    u32 r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const u32 w = a[q];
+        const u32 hi = w & 0xf0f0f0f0u, lo = (w << 4) & 0xf0f0f0f0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const u32 sel = 0x0c020100u | (4u + k);
+            const u32 ahi = __builtin_amdgcn_perm(hi, tsel, sel);
+            const u32 alo = __builtin_amdgcn_perm(lo, tsel, sel);
+            const u32x4 e0 = *(const lds_u32x4 *)(lds + ahi + (8 * q + 2 * k) * 256);
+            const u32x4 e1 = *(const lds_u32x4 *)(lds + alo + (8 * q + 2 * k + 1) * 256);
+            r0 = xor3(r0, e0[0], e1[0]);
+            r1 = xor3(r1, e0[1], e1[1]);
+            r2 = xor3(r2, e0[2], e1[2]);
+            r3 = xor3(r3, e0[3], e1[3]);
+        }
+    }
+    u32x4 r = {r0, r1, r2, r3};
+    return r;
+}
+
+// ------------------------------------------------------------------------------------------------ byte-exact I/O
+
+// loads n (< 16) bytes, zero padded
+__device__ __forceinline__ u32x4 load_partial(const uint8_t *p, u32 n)
+{
+    u32 w[4] = {0, 0, 0, 0};
+    for (u32 i = 0; i < n; ++i)
+        w[i >> 2] |= (u32)p[i] << (8 * (i & 3));
+    u32x4 v = {w[0], w[1], w[2], w[3]};
+    return v;
+}
+
+__device__ __forceinline__ void store_partial(uint8_t *p, u32x4 v, u32 n)
+{
+    for (u32 i = 0; i < n; ++i)
+        p[i] = (uint8_t)(v[i >> 2] >> (8 * (i & 3)));
+}
+
+// zero bytes n..15
+__device__ __forceinline__ u32x4 mask_tail(u32x4 v, u32 n)
+{
+    u32x4 r;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        int nb = (int)n - 4 * c;
+        u32 m = nb >= 4 ? 0xffffffffu : nb <= 0 ? 0u : (0xffffffffu >> (32 - 8 * nb));
+        r[c] = v[c] & m;
+    }
+    return r;
+}
+
+// ------------------------------------------------------------------------------------------------ main kernel
+
+struct BatchArgs {
+    const KeyEntry *keys;
+    const ptls_mi355x_record_t *recs;
+    u64 nrecs;
+    const uint8_t *in;
+    const uint8_t *aad;
+    uint8_t *out;
+    uint8_t *ok;
+    u32 multi_key;  // 0: every record uses key 0 (no key-run scan)
+    u32 nkeys;      // records whose key_idx >= nkeys are skipped (open: ok = 0)
+};
+
+#define RUN_SCAN_CAP 256  // records examined per key-run scan (multi-key batches)
+
+// Seals / opens the records [rec0 + slot] of one record group; all G lanes of a record cooperate (see file header).
+template <int NR, bool OPEN>
+__device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u8 *lds, const u32 (&rk)[NR + 1][4], u32 iv0,
+                                              u32 iv1, u32 iv2, u64 rec, bool valid, u32 j, u32 laneoff, u32 tsel_horner,
+                                              u32 tsel_last)
+{
+    constexpr int G = ENGINE_G;
+    ptls_mi355x_record_t r = {};
+    if (valid)
+        r = args.recs[rec];
+    const u32 L = r.len, A = r.aad_len;
+    const u32 na = (A + 15) >> 4, nb = (L + 15) >> 4;
+    const u32 total = na + nb + 1;
+    const u32 K = valid ? (total + G - 1) / G : 0;
+    const int P = (int)(K * G) - (int)total;
+
+    u32 Kmax = K;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+        Kmax = max(Kmax, (u32)__shfl_xor((int)Kmax, off, 64));
+
+    const u32 n0 = iv0 ^ rk[0][0];
+    const u32 n1 = iv1 ^ bswap32((u32)(r.seq >> 32)) ^ rk[0][1];
+    const u32 n2 = iv2 ^ bswap32((u32)r.seq) ^ rk[0][2];
+    const uint8_t *src = args.in + r.in_off;
+    uint8_t *dst = args.out + r.out_off;
+    const uint8_t *aadp = args.aad + r.aad_off;
+
+    u32x4 acc = {0, 0, 0, 0};
+    u32x4 ek0 = {0, 0, 0, 0};
+
+    for (u32 k = 0; k < Kmax; ++k) {
+        const bool act = k < K;
+        const int logical = (int)(j + G * k) - P;
+        const int b = logical - (int)na;
+        const bool is_data = act && logical >= (int)na && b < (int)nb;
+        const bool is_aad = act && logical >= 0 && logical < (int)na;
+        const bool is_len = act && logical == (int)(na + nb);
+
+        // AES-CTR: data lanes encrypt counter 2+b; every other lane encrypts J0 (only the length lane keeps it)
+        u32 s0 = n0, s1 = n1, s2 = n2;
+        u32 s3 = bswap32(is_data ? (u32)(b + 2) : 1u) ^ rk[0][3];
+        aes_encrypt_tt<NR>(lds, laneoff, rk, s0, s1, s2, s3);
+        const u32x4 ks = {s0, s1, s2, s3};
+
+        u32x4 X = {0, 0, 0, 0};
+        if (is_data) {
+            const u32 rem = L - 16u * (u32)b;
+            const uint8_t *ip = src + 16u * (u32)b;
+            uint8_t *op = dst + 16u * (u32)b;
+            if (rem >= 16) {
+                const u32x4 v = *(const u32x4_u *)ip;
+                const u32x4 o = v ^ ks;
+                *(u32x4_u *)op = o;
+                X = OPEN ? v : o;
+            } else {
+                const u32x4 v = load_partial(ip, rem);
+                const u32x4 o = mask_tail(v ^ ks, rem);
+                store_partial(op, o, rem);
+                X = OPEN ? v : o;
+            }
+        } else if (is_aad) {
+            const u32 rem = A - 16u * (u32)logical;
+            const uint8_t *ap = aadp + 16u * (u32)logical;
+            X = rem >= 16 ? *(const u32x4_u *)ap : load_partial(ap, rem);
+        } else if (is_len) {
+            const u64 abits = (u64)A * 8, cbits = (u64)L * 8;
+            X[0] = bswap32((u32)(abits >> 32));
+            X[1] = bswap32((u32)abits);
+            X[2] = bswap32((u32)(cbits >> 32));
+            X[3] = bswap32((u32)cbits);
+            ek0 = ks;
+        }
+        acc ^= X;
+        const u32x4 prod = gmul_tab(lds, acc, k + 1 == K ? tsel_last : tsel_horner);
+        if (act)
+            acc = prod;
+    }
+
+    // XOR over the G lanes of the record
+#pragma unroll
+    for (int off = 1; off < G; off <<= 1) {
+        acc[0] ^= (u32)__shfl_xor((int)acc[0], off, 64);
+        acc[1] ^= (u32)__shfl_xor((int)acc[1], off, 64);
+        acc[2] ^= (u32)__shfl_xor((int)acc[2], off, 64);
+        acc[3] ^= (u32)__shfl_xor((int)acc[3], off, 64);
+    }
+    if (valid && j == G - 1) {
+        const u32x4 tag = acc ^ ek0;
+        if (OPEN) {
+            const u32x4 rt = *(const u32x4_u *)(src + L);
+            const u32x4 d = rt ^ tag;
+            args.ok[rec] = (d[0] | d[1] | d[2] | d[3]) == 0;
+        } else {
+            *(u32x4_u *)(dst + L) = tag;
+        }
+    }
+}
+
+// Persistent kernel: workgroup w owns the contiguous record range [n*w/grid, n*(w+1)/grid) and walks it in key runs
+// (maximal stretches of equal key_idx, at most RUN_SCAN_CAP records); the GHASH tables in LDS are rebuilt only when
+// the key changes, so a single-key batch builds them once and a key-sorted many-connection batch once per key.
+template <int NR, bool OPEN>
+__global__ __launch_bounds__(ENGINE_WG) void gcm_batch_kernel(BatchArgs args)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    lds_u8 *lds = (lds_u8 *)smem;
+    lds_u32 *s_run = (lds_u32 *)(lds + LDS_BYTES);  // scratch word after the tables
+    constexpr int G = ENGINE_G;
+    constexpr int RPW = 64 / G;  // records per wave-iteration
+
+    build_aes_tables(lds);
+
+    const u32 lane = threadIdx.x & 63;
+    const u32 j = lane % G;
+    const u32 slot = lane / G;
+    const u32 laneoff = (lane & 31) * 4;
+    const u32 wave = threadIdx.x >> 6;
+    const u32 waves_per_wg = blockDim.x >> 6;
+    const u32 tsel_horner = 0x10000u | (u32)(G - 1) * GHASH_TABLE_BYTES;
+    const u32 tsel_last = 0x10000u | (u32)(G - 1 - j) * GHASH_TABLE_BYTES;
+
+    const u64 n = args.nrecs;
+    const u64 beg = n * blockIdx.x / gridDim.x, end = n * (blockIdx.x + 1) / gridDim.x;
+    u32 loaded_key = 0xffffffffu;
+
+    for (u64 pos = beg; pos < end;) {
+        const u32 key_idx = args.multi_key ? args.recs[pos].key_idx : 0u;
+        u64 run_end = end;
+        if (args.multi_key) {
+            const u64 lim = min(end, pos + RUN_SCAN_CAP);
+            if (threadIdx.x == 0)
+                *s_run = (u32)(lim - pos);
+            __syncthreads();
+            for (u64 t = pos + threadIdx.x; t < lim; t += blockDim.x)
+                if (args.recs[t].key_idx != key_idx)
+                    atomicMin((u32 *)s_run, (u32)(t - pos));
+            __syncthreads();
+            run_end = pos + *s_run;
+            __syncthreads();
+        }
+        if (key_idx >= args.nkeys) {  // invalid key: nothing is written except a failed ok byte
+            if (OPEN)
+                for (u64 t = pos + threadIdx.x; t < run_end; t += blockDim.x)
+                    args.ok[t] = 0;
+            pos = run_end;
+            continue;
+        }
+        if (key_idx != loaded_key) {
+            __syncthreads();  // no wave still reads the previous key's tables
+            build_ghash_tables(lds, args.keys + key_idx);
+            __syncthreads();
+            loaded_key = key_idx;
+        }
+        const KeyEntry *key = args.keys + key_idx;
+        // round keys and IV are workgroup-uniform: pin them in SGPRs
+        u32 rk[NR + 1][4];
+#pragma unroll
+        for (int r = 0; r <= NR; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                rk[r][c] = __builtin_amdgcn_readfirstlane(key->rk[r][c]);
+        const u32 iv0 = __builtin_amdgcn_readfirstlane(key->iv[0]), iv1 = __builtin_amdgcn_readfirstlane(key->iv[1]),
+                  iv2 = __builtin_amdgcn_readfirstlane(key->iv[2]);
+
+        const u64 ngroups = (run_end - pos + RPW - 1) / RPW;
+        for (u64 grp = wave; grp < ngroups; grp += waves_per_wg) {
+            const u64 rec = pos + grp * RPW + slot;
+            process_group<NR, OPEN>(args, lds, rk, iv0, iv1, iv2, rec, rec < run_end, j, laneoff, tsel_horner, tsel_last);
+        }
+        pos = run_end;
+    }
+}
+
+// AES-ECB of independent blocks (one block per thread, keys from the keyset)
+template <int NR>
+__global__ __launch_bounds__(256) void ecb_kernel(const KeyEntry *keys, const u32 *key_idx, const uint8_t *in, uint8_t *out,
+                                                  u64 nblocks)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    lds_u8 *lds = (lds_u8 *)smem;
+    build_aes_tables(lds);
+    __syncthreads();
+    const u32 laneoff = (threadIdx.x & 31) * 4;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nblocks; i += (u64)gridDim.x * blockDim.x) {
+        const KeyEntry *k = keys + (key_idx != nullptr ? key_idx[i] : 0);
+        u32 rk[NR + 1][4];
+        for (int r = 0; r <= NR; ++r)
+            for (int c = 0; c < 4; ++c)
+                rk[r][c] = k->rk[r][c];
+        const u32x4 v = *(const u32x4_u *)(in + 16 * i);
+        u32 s0 = v[0] ^ rk[0][0], s1 = v[1] ^ rk[0][1], s2 = v[2] ^ rk[0][2], s3 = v[3] ^ rk[0][3];
+        aes_encrypt_tt<NR>(lds, laneoff, rk, s0, s1, s2, s3);
+        const u32x4 o = {s0, s1, s2, s3};
+        *(u32x4_u *)(out + 16 * i) = o;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ host side
+
+static thread_local char g_err[256];
+
+static int fail(const char *fmt, const char *detail)
+{
+    snprintf(g_err, sizeof(g_err), fmt, detail);
+    return -1;
+}
+
+#define HIP_TRY(expr)                                                                                                         \
+    do {                                                                                                                      \
+        hipError_t e_ = (expr);                                                                                               \
+        if (e_ != hipSuccess)                                                                                                 \
+            return fail(#expr ": %s", hipGetErrorString(e_));                                                                 \
+    } while (0)
+
+struct st_ptls_mi355x_keyset_t {
+    int device;
+    size_t nkeys, key_size;
+    int nr;
+    KeyEntry *d_keys;
+    int ncu;
+};
+
+static int engine_init_attrs(void)
+{
+    static int done = 0;
+    if (done)
+        return 0;
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<10, false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<10, true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<14, false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<14, true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
+    HIP_TRY(hipFuncSetAttribute((const void *)ecb_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
+    HIP_TRY(hipFuncSetAttribute((const void *)ecb_kernel<14>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
+    done = 1;
+    return 0;
+}
+
+extern "C" {
+
+const char *ptls_mi355x_last_error(void) { return g_err; }
+
+int ptls_mi355x_is_supported(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+        return 0;
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess)
+        return 0;
+    return strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+}
+
+ptls_mi355x_keyset_t *ptls_mi355x_keyset_new(const void *keys, const void *ivs, size_t nkeys, size_t key_size)
+{
+    if (keys == NULL || ivs == NULL || nkeys == 0 || (key_size != 16 && key_size != 32) || nkeys > (1u << 30)) {
+        fail("%s", "ptls_mi355x_keyset_new: invalid arguments");
+        return NULL;
+    }
+    if (engine_init_attrs() != 0)
+        return NULL;
+    ptls_mi355x_keyset_t *ks = (ptls_mi355x_keyset_t *)calloc(1, sizeof(*ks));
+    uint8_t *d_raw = NULL;
+    if (ks == NULL)
+        return NULL;
+    ks->nkeys = nkeys, ks->key_size = key_size, ks->nr = key_size == 16 ? 10 : 14;
+    if (hipGetDevice(&ks->device) != hipSuccess || hipDeviceGetAttribute(&ks->ncu, hipDeviceAttributeMultiprocessorCount, ks->device) != hipSuccess)
+        goto Fail;
+    if (hipMalloc((void **)&ks->d_keys, nkeys * sizeof(KeyEntry)) != hipSuccess)
+        goto Fail;
+    if (hipMalloc((void **)&d_raw, nkeys * (key_size + 12)) != hipSuccess)
+        goto Fail;
+    if (hipMemcpy(d_raw, keys, nkeys * key_size, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_raw + nkeys * key_size, ivs, nkeys * 12, hipMemcpyHostToDevice) != hipSuccess)
+        goto Fail;
+    keyset_setup_kernel<<<(unsigned)((nkeys + 127) / 128), 128>>>(d_raw, d_raw + nkeys * key_size, ks->d_keys, (u32)nkeys, (u32)key_size);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+        goto Fail;
+    hipMemset(d_raw, 0, nkeys * (key_size + 12));
+    hipFree(d_raw);
+    return ks;
+Fail:
+    fail("%s", "ptls_mi355x_keyset_new: device setup failed");
+    if (d_raw != NULL)
+        hipFree(d_raw);
+    if (ks->d_keys != NULL)
+        hipFree(ks->d_keys);
+    free(ks);
+    return NULL;
+}
+
+void ptls_mi355x_keyset_free(ptls_mi355x_keyset_t *ks)
+{
+    if (ks == NULL)
+        return;
+    hipMemset(ks->d_keys, 0, ks->nkeys * sizeof(KeyEntry));
+    hipDeviceSynchronize();
+    hipFree(ks->d_keys);
+    free(ks);
+}
+
+size_t ptls_mi355x_keyset_size(const ptls_mi355x_keyset_t *ks) { return ks->nkeys; }
+size_t ptls_mi355x_keyset_key_size(const ptls_mi355x_keyset_t *ks) { return ks->key_size; }
+
+int ptls_mi355x_keyset_get_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, void *iv)
+{
+    if (ks == NULL || key_idx >= ks->nkeys)
+        return fail("%s", "get_iv: bad key index");
+    u32 w[3];
+    HIP_TRY(hipMemcpy(w, ks->d_keys[key_idx].iv, 12, hipMemcpyDeviceToHost));
+    memcpy(iv, w, 12);
+    return 0;
+}
+
+int ptls_mi355x_keyset_set_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, const void *iv)
+{
+    if (ks == NULL || key_idx >= ks->nkeys)
+        return fail("%s", "set_iv: bad key index");
+    u32 w[3];
+    memcpy(w, iv, 12);
+    HIP_TRY(hipMemcpy(ks->d_keys[key_idx].iv, w, 12, hipMemcpyHostToDevice));
+    return 0;
+}
+
+static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
+                        const void *aad, void *out, uint8_t *ok, void *stream)
+{
+    if (ks == NULL || (nrecs != 0 && (recs == NULL || in == NULL || out == NULL || (open && ok == NULL))))
+        return fail("%s", "batch: invalid arguments");
+    if (nrecs == 0)
+        return 0;
+    BatchArgs a = {ks->d_keys, recs, (u64)nrecs, (const uint8_t *)in, (const uint8_t *)aad, (uint8_t *)out, ok,
+                   ks->nkeys > 1 ? 1u : 0u, (u32)ks->nkeys};
+    if (a.aad == NULL)
+        a.aad = a.in;
+    const u64 groups = (nrecs + (64 / ENGINE_G) - 1) / (64 / ENGINE_G);
+    // one persistent workgroup per CU; small batches use fewer workgroups so each still gets >= 4 record groups
+    u64 grid = (u64)ks->ncu;
+    if (grid > (groups + 3) / 4)
+        grid = (groups + 3) / 4;
+    if (grid < 1)
+        grid = 1;
+    hipStream_t s = (hipStream_t)stream;
+    if (ks->nr == 10) {
+        if (open)
+            gcm_batch_kernel<10, true><<<(unsigned)grid, ENGINE_WG, LDS_ALLOC, s>>>(a);
+        else
+            gcm_batch_kernel<10, false><<<(unsigned)grid, ENGINE_WG, LDS_ALLOC, s>>>(a);
+    } else {
+        if (open)
+            gcm_batch_kernel<14, true><<<(unsigned)grid, ENGINE_WG, LDS_ALLOC, s>>>(a);
+        else
+            gcm_batch_kernel<14, false><<<(unsigned)grid, ENGINE_WG, LDS_ALLOC, s>>>(a);
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int ptls_mi355x_seal_batch(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
+                           const void *aad, void *out, void *stream)
+{
+    return launch_batch(ks, false, recs, nrecs, in, aad, out, NULL, stream);
+}
+
+int ptls_mi355x_open_batch(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
+                           const void *aad, void *out, uint8_t *ok, void *stream)
+{
+    return launch_batch(ks, true, recs, nrecs, in, aad, out, ok, stream);
+}
+
+int ptls_mi355x_ecb_batch(ptls_mi355x_keyset_t *ks, const uint32_t *key_idx, const void *in, void *out, size_t nblocks,
+                          void *stream)
+{
+    if (ks == NULL || (nblocks != 0 && (in == NULL || out == NULL)))
+        return fail("%s", "ecb: invalid arguments");
+    if (nblocks == 0)
+        return 0;
+    u64 grid = (nblocks + 255) / 256;
+    if (grid > (u64)ks->ncu * 4)
+        grid = (u64)ks->ncu * 4;
+    hipStream_t s = (hipStream_t)stream;
+    if (ks->nr == 10)
+        ecb_kernel<10><<<(unsigned)grid, 256, LDS_AES_BYTES, s>>>(ks->d_keys, key_idx, (const uint8_t *)in, (uint8_t *)out, nblocks);
+    else
+        ecb_kernel<14><<<(unsigned)grid, 256, LDS_AES_BYTES, s>>>(ks->d_keys, key_idx, (const uint8_t *)in, (uint8_t *)out, nblocks);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int ptls_mi355x_encrypt_block(ptls_mi355x_keyset_t *ks, size_t key_idx, void *out, const void *in)
+{
+    if (ks == NULL || key_idx >= ks->nkeys || out == NULL || in == NULL)
+        return fail("%s", "encrypt_block: invalid arguments");
+    uint8_t *d = NULL;
+    HIP_TRY(hipMalloc((void **)&d, 48));
+    u32 idx = (u32)key_idx;
+    int ret = -1;
+    if (hipMemcpy(d, in, 16, hipMemcpyHostToDevice) == hipSuccess && hipMemcpy(d + 32, &idx, 4, hipMemcpyHostToDevice) == hipSuccess &&
+        ptls_mi355x_ecb_batch(ks, (const uint32_t *)(d + 32), d, d + 16, 1, NULL) == 0 &&
+        hipMemcpy(out, d + 16, 16, hipMemcpyDeviceToHost) == hipSuccess)
+        ret = 0;
+    hipFree(d);
+    return ret;
+}
+
+// single record on host buffers: a batch of one
+static int single(ptls_mi355x_keyset_t *ks, size_t key_idx, bool open, void *output, const void *input, size_t len, uint64_t seq,
+                  const void *aad, size_t aadlen, int *verified)
+{
+    if (ks == NULL || key_idx >= ks->nkeys || aadlen > 0xffff || len > PTLS_MI355X_MAX_RECORD_LEN)
+        return fail("%s", "single: invalid arguments");
+    const size_t inbytes = len + (open ? 16 : 0), outbytes = len + (open ? 0 : 16);
+    uint8_t *d = NULL;
+    const size_t off_in = 0, off_out = (inbytes + 15) & ~(size_t)15, off_aad = off_out + ((outbytes + 15) & ~(size_t)15),
+                 off_rec = off_aad + ((aadlen + 15) & ~(size_t)15), off_ok = off_rec + 64, total = off_ok + 16;
+    HIP_TRY(hipMalloc((void **)&d, total));
+    ptls_mi355x_record_t r = {off_in, off_out, seq, (u32)off_aad, (u32)len, 0, (uint16_t)aadlen, 0};
+    int ret = -1;
+    ptls_mi355x_keyset_t view = *ks;
+    view.d_keys = ks->d_keys + key_idx;
+    view.nkeys = 1;
+    if (hipMemcpy(d + off_in, input, inbytes, hipMemcpyHostToDevice) != hipSuccess ||
+        (aadlen != 0 && hipMemcpy(d + off_aad, aad, aadlen, hipMemcpyHostToDevice) != hipSuccess) ||
+        hipMemcpy(d + off_rec, &r, sizeof(r), hipMemcpyHostToDevice) != hipSuccess)
+        goto Exit;
+    if (launch_batch(&view, open, (const ptls_mi355x_record_t *)(d + off_rec), 1, d + off_in, d + off_aad, d + off_out,
+                     d + off_ok, NULL) != 0)
+        goto Exit;
+    if (hipMemcpy(output, d + off_out, outbytes, hipMemcpyDeviceToHost) != hipSuccess)
+        goto Exit;
+    if (open) {
+        uint8_t okb = 0;
+        if (hipMemcpy(&okb, d + off_ok, 1, hipMemcpyDeviceToHost) != hipSuccess)
+            goto Exit;
+        *verified = okb;
+    }
+    ret = 0;
+Exit:
+    if (ret != 0 && g_err[0] == '\0')
+        fail("%s", "single: device copy failed");
+    hipFree(d);
+    return ret;
+}
+
+int ptls_mi355x_encrypt(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const void *input, size_t inlen, uint64_t seq,
+                        const void *aad, size_t aadlen)
+{
+    return single(ks, key_idx, false, output, input, inlen, seq, aad, aadlen, NULL);
+}
+
+size_t ptls_mi355x_decrypt(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const void *input, size_t inlen, uint64_t seq,
+                           const void *aad, size_t aadlen)
+{
+    if (inlen < 16)
+        return SIZE_MAX;
+    int verified = 0;
+    if (single(ks, key_idx, true, output, input, inlen - 16, seq, aad, aadlen, &verified) != 0)
+        return SIZE_MAX;
+    return verified ? inlen - 16 : SIZE_MAX;
+}
+
+}  // extern "C"

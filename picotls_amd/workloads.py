@@ -1,0 +1,146 @@
+"""The benchmark / parity workloads of BASELINE.json (synthetic record batches) and their deterministic generators.
+
+configs (BASELINE.json):
+  tls16k     1M x 16384 B TLS records, AES-128-GCM, one traffic key, AAD = TLS header {23,3,3,len}   (configs[1])
+  quic1200   4M x 1200 B QUIC-sized records, AES-128-GCM, one key, 13-byte AAD                      (configs[2])
+  mixed      4M records, L ~ U[64, 16384], AES-256-GCM, 64K keys (many-connection case)             (configs[3])
+  shard1200  32M x 1200 B sharded evenly across GPUs, AES-128-GCM                                   (configs[4])
+
+Payload and key bytes come from a seekable splitmix64 stream (seed 0x5eed), identical on host (numpy) and device
+(torch), so every shard of a batch is a slice of one global batch.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, replace
+
+import numpy as np
+
+from .records import RecordBatch
+
+GOLDEN = 0x9E3779B97F4A7C15
+C1 = 0xBF58476D1CE4E5B9
+C2 = 0x94D049BB133111EB
+M64 = (1 << 64) - 1
+
+
+def _to_i64(x: int) -> int:
+    x &= M64
+    return x - (1 << 64) if x >= 1 << 63 else x
+
+
+def splitmix_words_np(seed: int, word_off: int, nwords: int) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        i = np.arange(word_off + 1, word_off + nwords + 1, dtype=np.uint64)
+        z = np.uint64(seed & M64) + i * np.uint64(GOLDEN)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(C1)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(C2)
+        return z ^ (z >> np.uint64(31))
+
+
+def payload_np(seed: int, byte_off: int, nbytes: int) -> np.ndarray:
+    w0 = byte_off // 8
+    w1 = (byte_off + nbytes + 7) // 8
+    words = splitmix_words_np(seed, w0, w1 - w0)
+    b = words.astype("<u8").view(np.uint8)
+    s = byte_off - 8 * w0
+    return b[s:s + nbytes]
+
+
+def payload_torch(seed: int, nbytes: int, device, out=None, chunk_words: int = 1 << 25):
+    """Device-side splitmix64 byte stream (bytes [0, nbytes) of the stream), written into `out` (uint8) if given."""
+    import torch
+
+    if out is None:
+        out = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    nwords = (nbytes + 7) // 8
+    m30, m27, m31 = (1 << 34) - 1, (1 << 37) - 1, (1 << 33) - 1  # logical right shifts on int64
+    g, c1, c2, sd = _to_i64(GOLDEN), _to_i64(C1), _to_i64(C2), _to_i64(seed)
+    for w0 in range(0, nwords, chunk_words):
+        n = min(chunk_words, nwords - w0)
+        z = torch.arange(w0 + 1, w0 + n + 1, dtype=torch.int64, device=device)
+        z.mul_(g).add_(sd)
+        z = (z ^ ((z >> 30) & m30)) * c1
+        z = (z ^ ((z >> 27) & m27)) * c2
+        z = z ^ ((z >> 31) & m31)
+        bytes_ = z.view(torch.uint8)
+        lo, hi = 8 * w0, min(8 * (w0 + n), nbytes)
+        out[lo:hi] = bytes_[: hi - lo]
+        del z, bytes_
+    return out
+
+
+def tls_aad(length: int) -> bytes:
+    """TLS 1.3 record header used as AAD (lib/picotls.c:719-726): type 23, legacy version 0x0303, length incl. tag."""
+    n = length + 16
+    return bytes([23, 3, 3, (n >> 8) & 0xFF, n & 0xFF])
+
+
+@dataclass(frozen=True)
+class Workload:
+    name: str
+    nrecs: int
+    rec_len: int | None  # None: mixed lengths
+    aad_len: int
+    key_size: int
+    nkeys: int = 1
+    min_len: int = 64
+    max_len: int = 16384
+    tls_header_aad: bool = False
+    seed: int = 0x5EED
+    desc: str = ""
+
+    def scaled(self, nrecs: int) -> "Workload":
+        return replace(self, nrecs=nrecs)
+
+    # -- per-record attributes of the GLOBAL batch, sliced [begin, end)
+    def lens(self, begin: int, end: int) -> np.ndarray:
+        if self.rec_len is not None:
+            return np.full(end - begin, self.rec_len, dtype=np.uint64)
+        w = splitmix_words_np(self.seed ^ 0x4C454E, begin, end - begin)
+        return (np.uint64(self.min_len) + w % np.uint64(self.max_len - self.min_len + 1)).astype(np.uint64)
+
+    def key_and_seq(self, begin: int, end: int) -> tuple[np.ndarray, np.ndarray]:
+        """Single key: seq = record index. Many keys: records are grouped by connection (a server batches per
+        connection), i.e. key_idx = floor(i * nkeys / nrecs) and seq counts per key."""
+        i = np.arange(begin, end, dtype=np.uint64)
+        if self.nkeys == 1:
+            return np.zeros(end - begin, np.uint32), i
+        key = (i * np.uint64(self.nkeys) // np.uint64(self.nrecs)).astype(np.uint32)
+        first = (key.astype(np.uint64) * np.uint64(self.nrecs) + np.uint64(self.nkeys) - np.uint64(1)) // np.uint64(self.nkeys)
+        return key, i - first
+
+    def descriptors(self, begin: int, end: int) -> RecordBatch:
+        key, seq = self.key_and_seq(begin, end)
+        return RecordBatch.build(self.lens(begin, end), self.aad_len, seqs=seq, key_idx=key)
+
+    def keys(self) -> tuple[np.ndarray, np.ndarray]:
+        kb = payload_np(self.seed ^ 0x4B4559, 0, self.nkeys * self.key_size).copy()
+        ivb = payload_np(self.seed ^ 0x4956, 0, self.nkeys * 12).copy()
+        return kb, ivb
+
+    def aad_arena(self, batch: RecordBatch, begin: int) -> np.ndarray:
+        if batch.aad_bytes == 0:
+            return np.zeros(1, np.uint8)
+        if self.tls_header_aad:
+            arena = np.zeros(batch.aad_bytes, np.uint8)
+            lens = batch.seal["len"].astype(np.int64) + 16
+            offs = batch.seal["aad_off"].astype(np.int64)
+            arena[offs + 0] = 23
+            arena[offs + 1] = 3
+            arena[offs + 2] = 3
+            arena[offs + 3] = (lens >> 8) & 0xFF
+            arena[offs + 4] = lens & 0xFF
+            return arena
+        slot = batch.aad_bytes // max(batch.n, 1)
+        return payload_np(self.seed ^ 0x414144, begin * slot, batch.aad_bytes).copy()
+
+
+WORKLOADS = {
+    "tls16k": Workload("tls16k", 1 << 20, 16384, 5, 16, tls_header_aad=True,
+                       desc="1M x 16384 B TLS records, AES-128-GCM, single traffic key"),
+    "quic1200": Workload("quic1200", 4 << 20, 1200, 13, 16, desc="4M x 1200 B QUIC-sized records, AES-128-GCM, single key"),
+    "mixed": Workload("mixed", 4 << 20, None, 13, 32, nkeys=65536,
+                      desc="4M mixed-length records 64 B-16 KiB, AES-256-GCM, 64K traffic keys"),
+    "shard1200": Workload("shard1200", 32 << 20, 1200, 13, 16,
+                          desc="32M x 1200 B records sharded evenly across GPUs, AES-128-GCM"),
+}

@@ -1,0 +1,178 @@
+/*
+ * tests/c/test_vtable.c -- the MI355X picotls plugin (ptls_mi355x_aes{128,256}gcm / _ctr) against lib/fusion.c,
+ * through picotls' own plugin surface, in the reference's cross-backend style (t/picotls.c:224-370 test_ciphersuite:
+ * ctx and ctx_peer on different backends; t/fusion.c:385-466 test_generated; t/fusion.c:346-380 gcm_iv96).
+ * TAP-like output; exit status 0 iff every check passed.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "picotls.h"
+#include "picotls/fusion.h"
+#include "picotls/mi355x_picotls.h"
+
+static int nfail, ntest;
+#define OK(cond, ...)                                                                                                       \
+    do {                                                                                                                    \
+        ++ntest;                                                                                                            \
+        if (!(cond)) {                                                                                                      \
+            ++nfail;                                                                                                        \
+            printf("not ok %d - ", ntest);                                                                                  \
+            printf(__VA_ARGS__);                                                                                            \
+            printf(" (%s:%d)\n", __FILE__, __LINE__);                                                                       \
+        }                                                                                                                   \
+    } while (0)
+
+static uint64_t rs = 0x1234567;
+static uint8_t rnd8(void)
+{
+    rs ^= rs << 13, rs ^= rs >> 7, rs ^= rs << 17;
+    return (uint8_t)(rs >> 24);
+}
+static void rnd(void *p, size_t n)
+{
+    for (size_t i = 0; i < n; ++i)
+        ((uint8_t *)p)[i] = rnd8();
+}
+
+static void pair_test(ptls_aead_algorithm_t *a, ptls_aead_algorithm_t *b, const char *what, int iters)
+{
+    static uint8_t text[4096], aad[256], enc_a[4096 + 16], enc_b[4096 + 16], dec[4096];
+    for (int i = 0; i < iters; ++i) {
+        uint8_t key[32], iv[12];
+        uint64_t seq;
+        rnd(key, sizeof(key)), rnd(iv, sizeof(iv)), rnd(&seq, sizeof(seq));
+        size_t textlen = (i * 37 + rnd8()) % 2048, aadlen = rnd8() % 64;
+        rnd(text, textlen), rnd(aad, aadlen);
+        ptls_aead_context_t *ea = ptls_aead_new_direct(a, 1, key, iv), *db = ptls_aead_new_direct(b, 0, key, iv);
+        ptls_aead_context_t *eb = ptls_aead_new_direct(b, 1, key, iv), *da = ptls_aead_new_direct(a, 0, key, iv);
+        OK(ea && db && eb && da, "%s: ptls_aead_new_direct", what);
+        if (!(ea && db && eb && da))
+            return;
+        ptls_aead_encrypt(ea, enc_a, text, textlen, seq, aad, aadlen);
+        ptls_aead_encrypt(eb, enc_b, text, textlen, seq, aad, aadlen);
+        OK(memcmp(enc_a, enc_b, textlen + 16) == 0, "%s: ciphertext||tag equal (len=%zu aad=%zu)", what, textlen, aadlen);
+        OK(ptls_aead_decrypt(db, dec, enc_a, textlen + 16, seq, aad, aadlen) == textlen && memcmp(dec, text, textlen) == 0,
+           "%s: peer decrypts", what);
+        OK(ptls_aead_decrypt(da, dec, enc_b, textlen + 16, seq, aad, aadlen) == textlen && memcmp(dec, text, textlen) == 0,
+           "%s: peer decrypts (reverse)", what);
+        /* bit flip (t/picotls.c:252-254), wrong AAD (:329-330), wrong seq */
+        enc_b[rnd8() % (textlen + 16)] ^= 1 << (rnd8() % 8);
+        OK(ptls_aead_decrypt(db, dec, enc_b, textlen + 16, seq, aad, aadlen) == SIZE_MAX, "%s: tamper rejected", what);
+        if (aadlen != 0) {
+            aad[0] ^= 1;
+            OK(ptls_aead_decrypt(db, dec, enc_a, textlen + 16, seq, aad, aadlen) == SIZE_MAX, "%s: wrong aad rejected", what);
+            aad[0] ^= 1;
+        }
+        OK(ptls_aead_decrypt(db, dec, enc_a, textlen + 16, seq + 1, aad, aadlen) == SIZE_MAX, "%s: wrong seq rejected", what);
+        OK(ptls_aead_decrypt(db, dec, enc_a, 15, seq, aad, aadlen) == SIZE_MAX, "%s: inlen < 16", what);
+        ptls_aead_free(ea), ptls_aead_free(db), ptls_aead_free(eb), ptls_aead_free(da);
+    }
+}
+
+static void iv96_test(ptls_aead_algorithm_t *algo)
+{
+    /* t/fusion.c:346-380 */
+    static const uint8_t key[16] = {0x00, 0x11, 0x22, 0x33, 0x44, 0x55, 0x66, 0x77, 0x88, 0x99, 0xaa, 0xbb, 0xcc, 0xdd, 0xee, 0xff},
+                         iv[] = {20, 20, 20, 20, 24, 25, 26, 27, 28, 29, 30, 31}, seq32[4] = {0, 1, 2, 3},
+                         bad[4] = {0x89, 0xab, 0xcd, 0xef};
+    uint8_t aad[20], text[85], enc[85 + 16], dec[85];
+    for (int i = 0; i < 20; ++i)
+        aad[i] = i;
+    for (int i = 0; i < 85; ++i)
+        text[i] = "hello world\n"[i % 12];
+    text[84] = 0;
+    ptls_aead_context_t *ctx = ptls_aead_new_direct(algo, 0, key, iv), *ref = ptls_aead_new_direct(&ptls_fusion_aes128gcm, 0, key, iv);
+    uint8_t enc_ref[85 + 16];
+    ptls_aead_xor_iv(ctx, seq32, 4);
+    ptls_aead_xor_iv(ref, seq32, 4);
+    ptls_aead_encrypt(ctx, enc, text, 85, 0, aad, 20);
+    ptls_aead_encrypt(ref, enc_ref, text, 85, 0, aad, 20);
+    OK(memcmp(enc, enc_ref, sizeof(enc)) == 0, "iv96: ciphertext equals fusion");
+    OK(ptls_aead_decrypt(ctx, dec, enc, sizeof(enc), 0, aad, 20) == 85, "iv96: decrypt");
+    ptls_aead_xor_iv(ctx, seq32, 4);
+    ptls_aead_xor_iv(ctx, bad, 4);
+    OK(ptls_aead_decrypt(ctx, dec, enc, sizeof(enc), 0, aad, 20) == SIZE_MAX, "iv96: wrong iv rejected");
+    ptls_aead_xor_iv(ctx, bad, 4);
+    ptls_aead_xor_iv(ctx, seq32, 4);
+    OK(ptls_aead_decrypt(ctx, dec, enc, sizeof(enc), 0, aad, 20) == 85 && memcmp(dec, text, 85) == 0, "iv96: restored iv");
+    uint8_t got[12], exp[12];
+    ptls_aead_get_iv(ctx, got);
+    ptls_aead_get_iv(ref, exp);
+    OK(memcmp(got, exp, 12) == 0, "iv96: get_iv");
+    ptls_aead_free(ctx), ptls_aead_free(ref);
+}
+
+static void encrypt_v_test(ptls_aead_algorithm_t *algo, ptls_aead_algorithm_t *refalgo)
+{
+    uint8_t key[32], iv[12], text[300], aad[5] = {23, 3, 3, 1, 44}, out[316], exp[316];
+    rnd(key, 32), rnd(iv, 12), rnd(text, sizeof(text));
+    ptls_aead_context_t *ctx = ptls_aead_new_direct(algo, 1, key, iv), *ref = ptls_aead_new_direct(refalgo, 1, key, iv);
+    ptls_iovec_t vec[3] = {{text, 100}, {text + 100, 0}, {text + 100, 200}};
+    ptls_aead_encrypt_v(ctx, out, vec, 3, 42, aad, 5);
+    ptls_aead_encrypt(ref, exp, text, 300, 42, aad, 5);
+    OK(memcmp(out, exp, sizeof(out)) == 0, "encrypt_v (TLS record iovecs) equals fusion");
+    ptls_aead_free(ctx), ptls_aead_free(ref);
+}
+
+static void supp_test(ptls_aead_algorithm_t *algo, ptls_cipher_algorithm_t *ctr, ptls_aead_algorithm_t *refalgo,
+                      ptls_cipher_algorithm_t *refctr)
+{
+    /* QUIC header protection fused into the seal (include/picotls.h:441-456, lib/fusion.c:425-430,636-651) */
+    uint8_t key[32], hpkey[32], iv[12], text[200], aad[13], out[216], exp[216];
+    rnd(key, 32), rnd(hpkey, 32), rnd(iv, 12), rnd(text, 200), rnd(aad, 13);
+    for (size_t len = 1; len < 200; len += 17) {
+        ptls_aead_context_t *ctx = ptls_aead_new_direct(algo, 1, key, iv), *ref = ptls_aead_new_direct(refalgo, 1, key, iv);
+        ptls_aead_supplementary_encryption_t s1 = {ptls_cipher_new(ctr, 1, hpkey), out + 2}, s2 = {ptls_cipher_new(refctr, 1, hpkey), exp + 2};
+        ptls_aead_encrypt_s(ctx, out, text, len, 7, aad, 13, &s1);
+        ptls_aead_encrypt_s(ref, exp, text, len, 7, aad, 13, &s2);
+        OK(memcmp(out, exp, len + 16) == 0, "encrypt_s: sealed equal (len=%zu)", len);
+        OK(memcmp(s1.output, s2.output, 16) == 0, "encrypt_s: header-protection mask equal (len=%zu)", len);
+        ptls_cipher_free(s1.ctx), ptls_cipher_free(s2.ctx);
+        ptls_aead_free(ctx), ptls_aead_free(ref);
+    }
+}
+
+static void ecb_kat(void)
+{
+    /* t/picotls.c:372-413 (FIPS-197 C.1 / C.3) through the AES-CTR objects: CTR keystream block 0 = ECB(iv) */
+    static const uint8_t key[32] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31},
+                         pt[16] = {0x00, 0x11, 0x22, 0x33, 0x44, 0x55, 0x66, 0x77, 0x88, 0x99, 0xaa, 0xbb, 0xcc, 0xdd, 0xee, 0xff},
+                         e128[16] = {0x69, 0xC4, 0xE0, 0xD8, 0x6A, 0x7B, 0x04, 0x30, 0xD8, 0xCD, 0xB7, 0x80, 0x70, 0xB4, 0xC5, 0x5A},
+                         e256[16] = {0x8E, 0xA2, 0xB7, 0xCA, 0x51, 0x67, 0x45, 0xBF, 0xEA, 0xFC, 0x49, 0x90, 0x4B, 0x49, 0x60, 0x89};
+    uint8_t zero[16] = {0}, out[16];
+    ptls_cipher_context_t *c = ptls_cipher_new(&ptls_mi355x_aes128ctr, 1, key);
+    ptls_cipher_init(c, pt);
+    ptls_cipher_encrypt(c, out, zero, 16);
+    OK(memcmp(out, e128, 16) == 0, "aes128 ctr block 0 == FIPS-197 C.1");
+    ptls_cipher_free(c);
+    c = ptls_cipher_new(&ptls_mi355x_aes256ctr, 1, key);
+    ptls_cipher_init(c, pt);
+    ptls_cipher_encrypt(c, out, zero, 16);
+    OK(memcmp(out, e256, 16) == 0, "aes256 ctr block 0 == FIPS-197 C.3");
+    ptls_cipher_free(c);
+}
+
+int main(void)
+{
+    if (!ptls_fusion_is_supported_by_cpu()) {
+        printf("1..0 # SKIP fusion not supported by this CPU\n");
+        return 0;
+    }
+    OK(strcmp(ptls_mi355x_aes128gcm.name, ptls_fusion_aes128gcm.name) == 0 && ptls_mi355x_aes128gcm.key_size == 16 &&
+           ptls_mi355x_aes128gcm.iv_size == 12 && ptls_mi355x_aes128gcm.tag_size == 16 &&
+           ptls_mi355x_aes128gcm.confidentiality_limit == ptls_fusion_aes128gcm.confidentiality_limit &&
+           ptls_mi355x_aes128gcm.integrity_limit == ptls_fusion_aes128gcm.integrity_limit,
+       "aes128gcm algorithm fields match fusion");
+    OK(strcmp(ptls_mi355x_aes256gcm.name, "AES256-GCM") == 0 && ptls_mi355x_aes256gcm.key_size == 32, "aes256gcm fields");
+    ecb_kat();
+    pair_test(&ptls_fusion_aes128gcm, &ptls_mi355x_aes128gcm, "aes128gcm fusion<->mi355x", 60);
+    pair_test(&ptls_fusion_aes256gcm, &ptls_mi355x_aes256gcm, "aes256gcm fusion<->mi355x", 60);
+    iv96_test(&ptls_mi355x_aes128gcm);
+    encrypt_v_test(&ptls_mi355x_aes128gcm, &ptls_fusion_aes128gcm);
+    encrypt_v_test(&ptls_mi355x_aes256gcm, &ptls_fusion_aes256gcm);
+    supp_test(&ptls_mi355x_aes128gcm, &ptls_mi355x_aes128ctr, &ptls_fusion_aes128gcm, &ptls_fusion_aes128ctr);
+    supp_test(&ptls_mi355x_aes256gcm, &ptls_mi355x_aes256ctr, &ptls_fusion_aes256gcm, &ptls_fusion_aes256ctr);
+    printf("1..%d\n# %d failed\n", ntest, nfail);
+    return nfail == 0 ? 0 : 1;
+}

@@ -1,0 +1,73 @@
+"""CPU-side checks of the drop-in boundary: the shared objects load and export exactly what include/ declares.
+
+No compute calls (no GPU in this container)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import picotls_amd as pa
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared(header: str) -> set:
+    text = open(os.path.join(ROOT, "include", "picotls", header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return set(re.findall(r"\b(ptls_mi355x_\w+)\s*\(", text))
+
+
+def exported(so: str) -> set:
+    out = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_engine_library_loads_and_exports_header():
+    lib = pa.load_library()
+    assert isinstance(lib, ctypes.CDLL)
+    decl = declared("mi355x.h")
+    assert decl == set(pa.ABI_FUNCTIONS)
+    missing = decl - exported(pa.LIB_PATH)
+    assert not missing, missing
+
+
+def test_picotls_backend_exports_algorithms():
+    if not os.path.exists(pa.PICOTLS_LIB_PATH):
+        pytest.skip("picotls headers were not available at build time")
+    syms = exported(pa.PICOTLS_LIB_PATH)
+    for s in ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr", "ptls_mi355x_aes256ctr"):
+        assert s in syms
+    assert declared("mi355x_picotls.h") <= syms
+
+
+def test_kernels_are_gfx950_code_objects():
+    # the fat binary embeds a gfx950 code object (target id hipv4-amdgcn-amd-amdhsa--gfx950) and nothing else
+    data = open(pa.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+    for other in (b"--gfx942", b"--gfx90a", b"--gfx1100"):
+        assert other not in data
+
+
+def test_record_descriptor_layout_matches_header():
+    text = open(os.path.join(ROOT, "include", "picotls", "mi355x.h")).read()
+    assert "#define PTLS_MI355X_RECORD_SIZE 40" in text
+    assert pa.RECORD_DTYPE.itemsize == 40
+    names = list(pa.RECORD_DTYPE.names)
+    assert names == ["in_off", "out_off", "seq", "aad_off", "len", "key_idx", "aad_len", "flags"]
+    # the oracle's ctypes view must agree with the engine's
+    import oracle
+
+    assert oracle.RECORD_DTYPE == pa.RECORD_DTYPE
+
+
+def test_no_cpu_fallback_when_library_missing(tmp_path):
+    # the product path fails loudly instead of falling back to any CPU implementation
+    saved = pa._lib
+    try:
+        pa._lib = None
+        with pytest.raises(pa.EngineError):
+            pa.load_library(str(tmp_path / "missing.so"))
+    finally:
+        pa._lib = saved

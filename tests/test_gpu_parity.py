@@ -1,0 +1,295 @@
+"""Parity of the HIP engine (through its C ABI) with picotls' lib/fusion.c and the CPU oracle. Bit-exact.
+
+Run on the MI355X box: python -m pytest tests -m gpu
+"""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import picotls_amd as pa  # noqa: E402
+from oracle import FusionRef, GcmOracle  # noqa: E402
+from picotls_amd.records import RecordBatch  # noqa: E402
+from vecs import check_sealed, materialise  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+HAVE_REF = os.path.exists(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
+                                       "libfusion_ref.so"))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def engine():
+    assert torch.cuda.is_available(), "no GPU visible"
+    pa.load_library()
+    assert pa.is_supported(), "engine reports no gfx950 device"
+    torch.cuda.init()
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    return GcmOracle()
+
+
+@pytest.fixture(scope="module")
+def ref():
+    if not HAVE_REF:
+        pytest.skip("oracle/_ref/libfusion_ref.so not shipped")
+    return FusionRef()
+
+
+from gpu_util import dev, empty, gpu_open, gpu_seal  # noqa: E402
+
+
+def u8(b: bytes) -> np.ndarray:
+    return np.frombuffer(bytes(b), dtype=np.uint8)
+
+
+# ------------------------------------------------------------------------------------------------ known answers
+
+
+def test_ecb_kat(kat):
+    # t/fusion.c:72-86, t/picotls.c:397-413,429-437 through ptls_mi355x_ecb_batch
+    for v in kat["ecb"]:
+        key = bytes.fromhex(v["key"])
+        if v["src"].startswith("t/picotls.c:374-376,397"):
+            key = key[:16]
+        ks = pa.Keyset(key, bytes(12), len(key))
+        d_in, d_out = dev(u8(bytes.fromhex(v["pt"]) * 3)), empty(48)
+        pa.ecb_batch(ks, 0, d_in.data_ptr(), d_out.data_ptr(), 3)
+        torch.cuda.synchronize()
+        assert bytes(d_out.cpu().numpy()).hex() == v["ct"] * 3, v["src"]
+
+
+def test_gcm_zero_counter_kat(kat):
+    # t/fusion.c:236-256,277-288
+    for v in kat["gcm_zero_ctr"]:
+        key, aad, pt = (bytes.fromhex(v[k]) for k in ("key", "aad", "pt"))
+        ctx = pa.aead_new_direct(pa.aes128gcm, True, key, bytes(12))
+        sealed = ctx.encrypt(pt, 0, aad)
+        assert sealed.hex() == v["sealed"], v["src"]
+        assert ctx.decrypt(sealed, 0, aad) == pt
+
+
+def test_gcm_tag_vectors_and_hp_mask(kat):
+    # t/fusion.c:290-344: 19 tags, then the same with the supplementary (header-protection) block
+    t = kat["gcm_zero_ctr_tags"]
+    ctx = pa.aead_new_direct(pa.aes128gcm, True, bytes(16), bytes(12))
+    hp = pa.CtrCipher(bytes.fromhex(t["hp_key"]))
+    for aadlen, ptlen, tag, mask in t["cases"]:
+        sealed, m = ctx.encrypt_s(bytes(ptlen), 0, bytes(aadlen), hp, t["hp_sample_off"])
+        assert sealed[ptlen:].hex() == tag, (aadlen, ptlen)
+        assert m.hex() == mask
+        assert ctx.decrypt(sealed, 0, bytes(aadlen)) == bytes(ptlen)
+
+
+def test_gcm_seq_iv96_kat(kat):
+    # t/fusion.c:258-274, :346-380 (ptls_aead_xor_iv; decrypt with the wrong IV fails, then succeeds again)
+    for v in kat["gcm_seq"]:
+        key, aad, pt, iv = (bytes.fromhex(v[k]) for k in ("key", "aad", "pt", "iv"))
+        ctx = pa.aead_new_direct(pa.aes128gcm, False, key, iv)
+        if "xor_iv" in v:
+            ctx.xor_iv(bytes.fromhex(v["xor_iv"]))
+        sealed = ctx.encrypt(pt, v["seq"], aad)
+        assert sealed.hex() == v["sealed"]
+        assert ctx.decrypt(sealed, v["seq"], aad) == pt
+        if "bad_xor_iv" in v:
+            ctx.xor_iv(bytes.fromhex(v["xor_iv"]))
+            ctx.xor_iv(bytes.fromhex(v["bad_xor_iv"]))
+            assert ctx.decrypt(sealed, v["seq"], aad) is None
+            ctx.xor_iv(bytes.fromhex(v["bad_xor_iv"]))
+            ctx.xor_iv(bytes.fromhex(v["xor_iv"]))
+            assert ctx.decrypt(sealed, v["seq"], aad) == pt
+
+
+def test_nist_vectors(kat):
+    for v in kat["nist"]:
+        key, iv, aad, pt = (bytes.fromhex(v[k]) for k in ("key", "iv", "aad", "pt"))
+        ctx = pa.aead_new_direct(pa.aes128gcm, True, key, iv)
+        sealed = ctx.encrypt(pt, 0, aad)
+        assert sealed.hex() == v["ct"] + v["tag"], v["src"]
+        bad = bytearray(sealed)
+        bad[-1] ^= 0xFF
+        assert ctx.decrypt(bytes(bad), 0, aad) is None
+        assert ctx.decrypt(sealed[:15], 0, aad) is None  # inlen < 16 -> SIZE_MAX
+
+
+def test_fusion_vectors_one_multikey_batch(fusion_vectors):
+    # every vector of lib/fusion.c's golden set in ONE launch per key size (one key per record: multi-key path)
+    for key_size in (16, 32):
+        vs = [v for v in fusion_vectors["vectors"] if v["key_size"] == key_size]
+        mats = [materialise(v) for v in vs]
+        b = RecordBatch.build([len(m[4]) for m in mats], [len(m[3]) for m in mats], seqs=[m[2] for m in mats],
+                              key_idx=np.arange(len(vs)))
+        keys = b"".join(m[0] for m in mats)
+        ivs = b"".join(m[1] for m in mats)
+        ks = pa.Keyset(keys, ivs, key_size)
+        pt = np.zeros(b.pt_bytes, np.uint8)
+        aad = np.zeros(max(b.aad_bytes, 1), np.uint8)
+        for i, m in enumerate(mats):
+            o = int(b.seal["in_off"][i])
+            pt[o:o + len(m[4])] = u8(m[4])
+            a = int(b.seal["aad_off"][i])
+            aad[a:a + len(m[3])] = u8(m[3])
+        sealed = gpu_seal(ks, b.seal, pt, aad, b.sealed_bytes)
+        for i, v in enumerate(vs):
+            o = int(b.seal["out_off"][i])
+            assert check_sealed(v, bytes(sealed[o:o + v["len"] + 16])), (key_size, v["seed"])
+        back, ok = gpu_open(ks, b.open, sealed, aad, b.pt_bytes)
+        assert ok.all()
+        for i, m in enumerate(mats):
+            o = int(b.open["out_off"][i])
+            assert bytes(back[o:o + len(m[4])]) == m[4]
+
+
+# ------------------------------------------------------------------------------------------------ randomized
+
+
+def _random_batch(rng, n, max_len, max_aad, key_size, nkeys=1, sort_keys=True):
+    lens = rng.integers(0, max_len + 1, n)
+    aads = rng.integers(0, max_aad + 1, n)
+    key_idx = rng.integers(0, nkeys, n)
+    if sort_keys:
+        key_idx = np.sort(key_idx)
+    b = RecordBatch.build(lens, aads, seqs=rng.integers(0, 2**63, n, dtype=np.uint64), key_idx=key_idx)
+    keys = np.frombuffer(rng.bytes(nkeys * key_size), np.uint8)
+    ivs = np.frombuffer(rng.bytes(nkeys * 12), np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(max(b.aad_bytes, 1)), np.uint8)
+    return b, keys, ivs, pt, aad
+
+
+@pytest.mark.parametrize("key_size,nkeys,sort_keys", [(16, 1, True), (32, 1, True), (16, 7, True), (32, 50, False)])
+def test_random_batch_vs_fusion(ref, key_size, nkeys, sort_keys):
+    rng = np.random.default_rng(key_size * 1000 + nkeys)
+    b, keys, ivs, pt, aad = _random_batch(rng, 3000, 3000, 64, key_size, nkeys, sort_keys)
+    ks = pa.Keyset(keys, ivs, key_size)
+    sealed = gpu_seal(ks, b.seal, pt, aad, b.sealed_bytes)
+    expect = np.zeros(b.sealed_bytes, np.uint8)
+    ref.run_batch(True, keys, ivs, key_size, b.seal, pt, aad, expect, nthreads=8)
+    assert np.array_equal(sealed, expect)
+    back, ok = gpu_open(ks, b.open, sealed, aad, b.pt_bytes)
+    assert ok.all()
+    assert np.array_equal(back, pt)
+
+
+def test_every_length_0_to_300_vs_oracle(oracle):
+    # all stream layouts around the G-lane boundaries (partial blocks, AAD-only, empty records)
+    rng = np.random.default_rng(7)
+    lens = np.arange(0, 301)
+    b = RecordBatch.build(lens, (lens * 7) % 41, seqs=lens * 1000003)
+    keys, ivs = np.frombuffer(rng.bytes(16), np.uint8), np.frombuffer(rng.bytes(12), np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(b.aad_bytes), np.uint8)
+    ks = pa.Keyset(keys, ivs, 16)
+    sealed = gpu_seal(ks, b.seal, pt, aad, b.sealed_bytes)
+    expect = np.zeros(b.sealed_bytes, np.uint8)
+    oracle.seal_batch(keys, ivs, 16, b.seal, pt, aad, expect)
+    assert np.array_equal(sealed, expect)
+
+
+def test_tamper_rejected_per_record(ref):
+    rng = np.random.default_rng(11)
+    b, keys, ivs, pt, aad = _random_batch(rng, 512, 2000, 40, 16)
+    ks = pa.Keyset(keys, ivs, 16)
+    sealed = gpu_seal(ks, b.seal, pt, aad, b.sealed_bytes)
+    bad = sealed.copy()
+    badaad = aad.copy()
+    victims = rng.choice(b.n, 64, replace=False)
+    for i, r in enumerate(victims):
+        ln = int(b.seal["len"][r])
+        kind = i % 3
+        if kind == 0 or (kind == 2 and int(b.seal["aad_len"][r]) == 0):  # flip a bit of ciphertext or tag
+            off = int(b.open["in_off"][r]) + int(rng.integers(0, ln + 16))
+            bad[off] ^= 1 << int(rng.integers(0, 8))
+        elif kind == 1:  # flip a tag bit
+            bad[int(b.open["in_off"][r]) + ln + int(rng.integers(0, 16))] ^= 0x80
+        else:  # flip an AAD bit
+            badaad[int(b.seal["aad_off"][r]) + int(rng.integers(0, int(b.seal["aad_len"][r])))] ^= 4
+    back, ok = gpu_open(ks, b.open, bad, badaad, b.pt_bytes)
+    expect_ok = np.ones(b.n, np.uint8)
+    expect_ok[victims] = 0
+    assert np.array_equal(ok, expect_ok)
+    # like lib/fusion.c (:783-828) the plaintext is written even when the tag fails: compare with fusion's output
+    ref_back = np.zeros(b.pt_bytes, np.uint8)
+    ref_ok = np.zeros(b.n, np.uint8)
+    ref.run_batch(False, keys, ivs, 16, b.open, bad, badaad, ref_back, ok=ref_ok, nthreads=4)
+    assert np.array_equal(ref_ok, expect_ok)
+    assert np.array_equal(back, ref_back)
+
+
+def test_unaligned_offsets_and_in_place(oracle):
+    rng = np.random.default_rng(13)
+    n = 200
+    lens = rng.integers(0, 700, n)
+    aads = rng.integers(0, 30, n)
+    recs = np.zeros(n, dtype=pa.RECORD_DTYPE)
+    off = 3
+    aoff = 1
+    for i in range(n):
+        recs[i]["in_off"] = off
+        recs[i]["out_off"] = off  # in place: ciphertext over plaintext, tag right after it
+        recs[i]["len"] = lens[i]
+        recs[i]["aad_off"] = aoff
+        recs[i]["aad_len"] = aads[i]
+        recs[i]["seq"] = i * 977
+        off += int(lens[i]) + 16 + int(rng.integers(0, 16))
+        aoff += int(aads[i]) + int(rng.integers(0, 5))
+    keys, ivs = np.frombuffer(rng.bytes(32), np.uint8), np.frombuffer(rng.bytes(12), np.uint8)
+    arena = np.frombuffer(rng.bytes(off + 16), np.uint8).copy()
+    aad = np.frombuffer(rng.bytes(aoff + 1), np.uint8)
+    expect = arena.copy()
+    oracle.seal_batch(keys, ivs, 32, recs, arena, aad, expect)
+    ks = pa.Keyset(keys, ivs, 32)
+    d_arena = dev(arena)
+    d_recs, d_aad = dev(recs), dev(aad)
+    pa.seal_batch(ks, d_recs.data_ptr(), n, d_arena.data_ptr(), d_aad.data_ptr(), d_arena.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(d_arena.cpu().numpy(), expect)
+    d_ok = empty(n, 0x55)
+    pa.open_batch(ks, d_recs.data_ptr(), n, d_arena.data_ptr(), d_aad.data_ptr(), d_arena.data_ptr(), d_ok.data_ptr())
+    torch.cuda.synchronize()
+    got = d_arena.cpu().numpy()
+    assert d_ok.cpu().numpy().all()
+    for i in range(n):
+        o, ln = int(recs[i]["in_off"]), int(lens[i])
+        assert np.array_equal(got[o:o + ln], arena[o:o + ln])
+
+
+def test_empty_batch_and_bad_args():
+    ks = pa.Keyset(bytes(16), bytes(12), 16)
+    pa.seal_batch(ks, 0, 0, 0, 0, 0)  # nrecs = 0 is a no-op
+    with pytest.raises(pa.EngineError):
+        pa.seal_batch(ks, 0, 5, 0, 0, 0)
+    with pytest.raises(ValueError):
+        pa.Keyset(bytes(24), bytes(12), 24)
+
+
+def test_max_tls_record_and_large_records(ref):
+    # PTLS_MAX_PLAINTEXT_RECORD_SIZE (lib/picotls.c:52) + the 256-byte TLS 1.3 expansion allowance, and beyond
+    rng = np.random.default_rng(17)
+    lens = [16384, 16384 + 256, 65536, 1 << 20, 16383, 16385]
+    b = RecordBatch.build(lens, [5, 5, 13, 13, 0, 32])
+    keys, ivs = np.frombuffer(rng.bytes(16), np.uint8), np.frombuffer(rng.bytes(12), np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(b.aad_bytes), np.uint8)
+    ks = pa.Keyset(keys, ivs, 16)
+    sealed = gpu_seal(ks, b.seal, pt, aad, b.sealed_bytes)
+    expect = np.zeros(b.sealed_bytes, np.uint8)
+    ref.run_batch(True, keys, ivs, 16, b.seal, pt, aad, expect, nthreads=4)
+    assert np.array_equal(sealed, expect)
+
+
+def test_picotls_vtable_pairs():
+    # cross-backend pairs in the reference's style (t/picotls.c:224-370): seal with fusion / open with MI355X and back,
+    # through ptls_aead_new_direct + the ptls_aead_algorithm_t objects (tests/c/test_vtable.c)
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "_bin", "test_vtable")
+    if not os.path.exists(exe):
+        pytest.skip("tests/c/_bin/test_vtable not built (needs picotls headers at build time)")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    assert "not ok" not in r.stdout

@@ -1,0 +1,146 @@
+"""Pins the CPU oracle (oracle/gcm_ref.c) to the reference's own known answers and to lib/fusion.c.
+
+CPU only. The oracle is test infrastructure; the HIP engine is checked against it in test_gpu_parity.py.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import FusionRef, GcmOracle
+from vecs import check_sealed, h_from_fusion_internal, materialise
+
+HAVE_REF = os.path.exists(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
+                                       "libfusion_ref.so"))
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    return GcmOracle()
+
+
+def test_ecb_kat(oracle, kat):
+    # t/fusion.c:72-86, t/picotls.c:397-413,429-437
+    for v in kat["ecb"]:
+        key = bytes.fromhex(v["key"])
+        if v["src"].startswith("t/picotls.c:374-376,397"):
+            key = key[:16]
+        assert oracle.aes_encrypt(key, bytes.fromhex(v["pt"])).hex() == v["ct"], v["src"]
+
+
+def test_ghash_kat(oracle, kat):
+    # t/fusion.c:88-234, H and results held in fusion's internal form
+    h = h_from_fusion_internal(bytes.fromhex(kat["ghash"]["h_fusion_internal"]))
+    for c in kat["ghash"]["cases"]:
+        data = bytes.fromhex(c["data"])[:16 * c["nblocks"]]
+        assert oracle.ghash(h, data) == bytes.fromhex(c["out_fusion_internal"])[::-1], c["nblocks"]
+
+
+def test_gcm_zero_counter_kat(oracle, kat):
+    # t/fusion.c:236-256,277-288: raw API with counter 0 == IV 0^96, seq 0
+    for v in kat["gcm_zero_ctr"]:
+        key, aad, pt = (bytes.fromhex(v[k]) for k in ("key", "aad", "pt"))
+        sealed = oracle.seal(key, bytes(12), 0, aad, pt)
+        assert sealed.hex() == v["sealed"], v["src"]
+        assert oracle.open(key, bytes(12), 0, aad, sealed) == pt
+
+
+def test_gcm_tag_vectors(oracle, kat):
+    # t/fusion.c:290-344 (19 tags over zero inputs) and the supp mask (AES-ECB(01*16, sealed[2:18]))
+    t = kat["gcm_zero_ctr_tags"]
+    hp_key = bytes.fromhex(t["hp_key"])
+    for aadlen, ptlen, tag, mask in t["cases"]:
+        sealed = oracle.seal(bytes(16), bytes(12), 0, bytes(aadlen), bytes(ptlen))
+        assert sealed[ptlen:].hex() == tag, (aadlen, ptlen)
+        off = t["hp_sample_off"]
+        assert oracle.aes_encrypt(hp_key, sealed[off:off + 16]).hex() == mask
+        assert oracle.open(bytes(16), bytes(12), 0, bytes(aadlen), sealed) == bytes(ptlen)
+
+
+def test_gcm_seq_and_iv96(oracle, kat):
+    # t/fusion.c:258-274 and gcm_iv96 :346-380 (ptls_aead_xor_iv, wrong IV rejected)
+    for v in kat["gcm_seq"]:
+        key, aad, pt, iv = (bytes.fromhex(v[k]) for k in ("key", "aad", "pt", "iv"))
+        if "xor_iv" in v:
+            iv = bytes(a ^ b for a, b in zip(iv, bytes.fromhex(v["xor_iv"]) + bytes(8)))
+        sealed = oracle.seal(key, iv, v["seq"], aad, pt)
+        assert sealed.hex() == v["sealed"]
+        assert oracle.open(key, iv, v["seq"], aad, sealed) == pt
+        if "bad_xor_iv" in v:
+            bad = bytes(a ^ b for a, b in zip(iv, bytes.fromhex(v["bad_xor_iv"]) + bytes(8)))
+            assert oracle.open(key, bad, v["seq"], aad, sealed) is None
+
+
+def test_nist_vectors(oracle, kat):
+    # deps/cifra/src/testmodes.c:395-433
+    for v in kat["nist"]:
+        key, iv, aad, pt = (bytes.fromhex(v[k]) for k in ("key", "iv", "aad", "pt"))
+        sealed = oracle.seal(key, iv, 0, aad, pt)
+        assert sealed.hex() == v["ct"] + v["tag"], v["src"]
+        bad = bytearray(sealed)
+        bad[-1] ^= 0xFF
+        assert oracle.open(key, iv, 0, aad, bytes(bad)) is None
+
+
+def test_fusion_vectors(oracle, fusion_vectors):
+    # 528 vectors produced by lib/fusion.c itself (tests/golden/gen_golden.py)
+    for v in fusion_vectors["vectors"]:
+        key, iv, seq, aad, pt = materialise(v)
+        sealed = oracle.seal(key, iv, seq, aad, pt)
+        assert check_sealed(v, sealed), v["seed"]
+
+
+def test_open_rejects_short_and_tampered(oracle):
+    key, iv = bytes(range(16)), bytes(range(12))
+    assert oracle.open(key, iv, 0, b"", b"\0" * 15) is None  # inlen < 16 -> SIZE_MAX (lib/fusion.c:1160-1161)
+    sealed = oracle.seal(key, iv, 7, b"hdr", b"payload!")
+    for i in range(len(sealed)):
+        bad = bytearray(sealed)
+        bad[i] ^= 1
+        assert oracle.open(key, iv, 7, b"hdr", bytes(bad)) is None
+    assert oracle.open(key, iv, 8, b"hdr", sealed) is None  # wrong seq
+    assert oracle.open(key, iv, 7, b"hdx", sealed) is None  # wrong AAD
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="oracle/_ref/libfusion_ref.so not built (needs /root/reference)")
+def test_random_differential_vs_fusion(oracle):
+    # t/fusion.c:385-466 shape: random (key, iv, seq, aadlen < 256, textlen < 256), both directions
+    ref = FusionRef()
+    rng = np.random.default_rng(1234)
+    for i in range(1500):
+        ks = 16 if i % 2 == 0 else 32
+        key, iv = rng.bytes(ks), rng.bytes(12)
+        seq = int(rng.integers(0, 2**63))
+        aad, pt = rng.bytes(int(rng.integers(0, 256))), rng.bytes(int(rng.integers(0, 256)))
+        a = oracle.seal(key, iv, seq, aad, pt)
+        assert a == ref.seal(key, iv, seq, aad, pt)
+        assert ref.open(key, iv, seq, aad, a) == pt
+        assert oracle.open(key, iv, seq, aad, a) == pt
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="oracle/_ref/libfusion_ref.so not built (needs /root/reference)")
+def test_batch_helpers_match_fusion(oracle):
+    # the batch layout used by the GPU tests, checked between both checkers
+    from picotls_amd.records import RecordBatch
+
+    ref = FusionRef()
+    rng = np.random.default_rng(5)
+    lens = rng.integers(0, 3000, 64)
+    lens[:4] = [0, 1, 16, 4096]
+    b = RecordBatch.build(lens, rng.integers(0, 40, 64), seqs=rng.integers(0, 2**40, 64), key_idx=rng.integers(0, 3, 64))
+    keys, ivs = np.frombuffer(rng.bytes(3 * 32), np.uint8), np.frombuffer(rng.bytes(3 * 12), np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(b.aad_bytes), np.uint8)
+    out_o, out_r = np.zeros(b.sealed_bytes, np.uint8), np.zeros(b.sealed_bytes, np.uint8)
+    oracle.seal_batch(keys, ivs, 32, b.seal, pt, aad, out_o)
+    ref.run_batch(True, keys, ivs, 32, b.seal, pt, aad, out_r, nthreads=2)
+    assert np.array_equal(out_o, out_r)
+    back_o, back_r = np.zeros(b.pt_bytes, np.uint8), np.zeros(b.pt_bytes, np.uint8)
+    ok_o, ok_r = np.zeros(b.n, np.uint8), np.zeros(b.n, np.uint8)
+    oracle.open_batch(keys, ivs, 32, b.open, out_o, aad, back_o, ok_o)
+    _, fails = ref.run_batch(False, keys, ivs, 32, b.open, out_r, aad, back_r, ok=ok_r, nthreads=3)
+    assert fails == 0 and ok_o.all() and ok_r.all()
+    assert np.array_equal(back_o, back_r)
+    for i in range(b.n):
+        s, ln = int(b.seal["in_off"][i]), int(lens[i])
+        assert np.array_equal(back_o[s:s + ln], pt[s:s + ln])
