@@ -173,6 +173,7 @@ def spot_check(wl, b, keys, ivs, d_pt, d_aad, d_sealed, begin, nsample: int = 64
     for r in sub:
         ln, al = int(r["len"]), int(r["aad_len"])
         pt_parts.append(d_pt[int(r["in_off"]):int(r["in_off"]) + ln].cpu().numpy())
+        pt_parts.append(np.zeros(16, np.uint8))  # room for the tag (sealed in place)
         aad_parts.append(d_aad[int(r["aad_off"]):int(r["aad_off"]) + al].cpu().numpy())
         new_in.append(off)
         new_aad.append(aoff)
@@ -182,7 +183,7 @@ def spot_check(wl, b, keys, ivs, d_pt, d_aad, d_sealed, begin, nsample: int = 64
     recs["in_off"] = new_in
     recs["out_off"] = new_in
     recs["aad_off"] = new_aad
-    pt = np.concatenate(pt_parts + [np.zeros(16 * len(sub) + 1, np.uint8)])
+    pt = np.concatenate(pt_parts + [np.zeros(1, np.uint8)])
     aad = np.concatenate(aad_parts + [np.zeros(1, np.uint8)])
     out = np.zeros(len(pt), np.uint8)
     ref.run_batch(True, keys, ivs, wl.key_size, recs, pt, aad, out, nthreads=1)
@@ -203,6 +204,15 @@ def cpu_baseline(wl, seconds: float):
     except Exception as e:
         return {"value": None, "unit": "GiB/s", "cores": 0, "kind": "reference", "sample": f"unavailable: {e}"}
     cpus = sorted(os.sched_getaffinity(0))
+    # the box grants a CPU share smaller than the visible CPU set (OMP_NUM_THREADS / nproc report it)
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(cpus)
+    try:
+        import subprocess
+
+        share = min(share, int(subprocess.run(["nproc"], capture_output=True, text=True).stdout.strip() or share))
+    except Exception:
+        pass
+    cpus = cpus[:max(1, min(share, len(cpus)))]
     nthreads = len(cpus)
     n = min(wl.nrecs, max(1, (256 << 20) // (wl.rec_len or 8192)))  # ~256 MiB sample of the same workload
     b = wl.descriptors(0, n)

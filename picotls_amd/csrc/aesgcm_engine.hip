@@ -157,7 +157,7 @@ __global__ void keyset_setup_kernel(const uint8_t *__restrict__ keys, const uint
         u32 t = w[j - 1];
         if (j % nk == 0) {
             t = sub_word((t >> 8) | (t << 24)) ^ rcon;
-            rcon = (rcon << 1) ^ ((rcon & 0x80) ? 0x1b : 0);
+            rcon = ((rcon << 1) ^ ((rcon & 0x80) ? 0x1b : 0)) & 0xff;
         } else if (nk > 6 && j % nk == 4) {
             t = sub_word(t);
         }
@@ -783,7 +783,7 @@ static int single(ptls_mi355x_keyset_t *ks, size_t key_idx, bool open, void *out
     const size_t off_in = 0, off_out = (inbytes + 15) & ~(size_t)15, off_aad = off_out + ((outbytes + 15) & ~(size_t)15),
                  off_rec = off_aad + ((aadlen + 15) & ~(size_t)15), off_ok = off_rec + 64, total = off_ok + 16;
     HIP_TRY(hipMalloc((void **)&d, total));
-    ptls_mi355x_record_t r = {off_in, off_out, seq, (u32)off_aad, (u32)len, 0, (uint16_t)aadlen, 0};
+    ptls_mi355x_record_t r = {0, 0, seq, 0, (u32)len, 0, (uint16_t)aadlen, 0};  // offsets relative to the arenas below
     int ret = -1;
     ptls_mi355x_keyset_t view = *ks;
     view.d_keys = ks->d_keys + key_idx;
