@@ -28,6 +28,7 @@
 // 4c..4c+3 = AES state column c. GHASH elements use the same byte order (byte 0 holds x^0..x^7, MSB first).
 
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 #include <string.h>
 #include <stdio.h>
@@ -85,8 +86,18 @@ struct KeyEntry {
 };
 static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 
+#ifndef GHASH_BATCH
+#define GHASH_BATCH 0      // 1: issue GHASH table lookups in batches of 8
+#endif
+
 #define ENGINE_G 8                 // lanes per record
-#define ENGINE_WG 1024             // threads per workgroup
+#ifndef ENGINE_NB
+#define ENGINE_NB 1                // AES-CTR blocks per lane per step (independent chains in flight)
+#endif
+#ifndef ENGINE_WG
+#define ENGINE_WG 1024             // threads per workgroup (one workgroup per CU)
+#endif
+#define ENGINE_WAVES_PER_SIMD (ENGINE_WG / 256)
 #define LDS_AES_BYTES 65536        // Te0/Te2, 32-bank replicated
 #define GHASH_TABLE_BYTES 8192     // 32 windows x 16 entries x 16 B
 #define LDS_BYTES (LDS_AES_BYTES + ENGINE_G * GHASH_TABLE_BYTES)
@@ -251,72 +262,157 @@ __device__ void build_ghash_tables(lds_u8 *lds, const KeyEntry *__restrict__ key
 // LDS byte address of Te0[byte r of w] in this lane's bank: byte0 = bank*4 (from laneoff), byte1 = byte r of w.
 #define TE_ADDR(w, r, laneoff) __builtin_amdgcn_perm((w), (laneoff), 0x0c0c0000u | ((4u + (r)) << 8))
 
-__device__ __forceinline__ u32 te0(const lds_u8 *lds, u32 w, int r, u32 laneoff)
+// LDS is addressed absolutely: the kernels declare no static __shared__ data, so their dynamic region starts at LDS
+// address 0 (checked at kernel entry by check_lds_base) and a v_perm result is directly a ds_read address; going
+// through the extern array's symbol would cost one v_add per lookup.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wint-to-pointer-cast"
+__device__ __forceinline__ u32 lds_load32(u32 addr) { return *(const lds_u32 *)addr; }
+__device__ __forceinline__ u32x4 lds_load128(u32 addr) { return *(const lds_u32x4 *)addr; }
+#pragma clang diagnostic pop
+
+__device__ __forceinline__ void check_lds_base(const void *smem)
 {
-    return *(const lds_u32 *)(lds + TE_ADDR(w, r, laneoff));
+    if ((u32)(size_t)(const lds_u8 *)smem != 0)
+        __builtin_trap();
 }
-__device__ __forceinline__ u32 te2(const lds_u8 *lds, u32 w, int r, u32 laneoff)
+
+__device__ __forceinline__ u32 te0(const lds_u8 *, u32 w, int r, u32 laneoff) { return lds_load32(TE_ADDR(w, r, laneoff)); }
+__device__ __forceinline__ u32 te2(const lds_u8 *, u32 w, int r, u32 laneoff) { return lds_load32(TE_ADDR(w, r, laneoff) + 128); }
+
+// rounds FIRST .. NR of AES (T-table rounds, then the final SubBytes/ShiftRows/AddRoundKey) on NB independent
+// LE-column states; the NB blocks advance in lockstep so each round has 16*NB independent LDS lookups in flight.
+template <int NR, int FIRST, int NB>
+__device__ __forceinline__ void aes_rounds_n(const lds_u8 *lds, u32 laneoff, const u32 (*rk)[4], u32 (&s)[NB][4])
 {
-    return *(const lds_u32 *)(lds + TE_ADDR(w, r, laneoff) + 128);
+#pragma unroll
+    for (int r = FIRST; r < NR; ++r) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            const u32 s0 = s[i][0], s1 = s[i][1], s2 = s[i][2], s3 = s[i][3];
+            s[i][0] = xor3(te0(lds, s0, 0, laneoff), te2(lds, s2, 2, laneoff), rk[r][0]) ^
+                      rotl8(te0(lds, s1, 1, laneoff) ^ te2(lds, s3, 3, laneoff));
+            s[i][1] = xor3(te0(lds, s1, 0, laneoff), te2(lds, s3, 2, laneoff), rk[r][1]) ^
+                      rotl8(te0(lds, s2, 1, laneoff) ^ te2(lds, s0, 3, laneoff));
+            s[i][2] = xor3(te0(lds, s2, 0, laneoff), te2(lds, s0, 2, laneoff), rk[r][2]) ^
+                      rotl8(te0(lds, s3, 1, laneoff) ^ te2(lds, s1, 3, laneoff));
+            s[i][3] = xor3(te0(lds, s3, 0, laneoff), te2(lds, s1, 2, laneoff), rk[r][3]) ^
+                      rotl8(te0(lds, s0, 1, laneoff) ^ te2(lds, s2, 3, laneoff));
+        }
+    }
+    // last round: SubBytes + ShiftRows + AddRoundKey; S(x) is byte 1/2 of Te0[x] and byte 0/3 of Te2[x]
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        u32 o[4];
+#pragma unroll
+        for (int col = 0; col < 4; ++col) {
+            const u32 a = te2(lds, s[i][col], 0, laneoff);
+            const u32 b = te0(lds, s[i][(col + 1) & 3], 1, laneoff);
+            const u32 c = te0(lds, s[i][(col + 2) & 3], 2, laneoff);
+            const u32 d = te2(lds, s[i][(col + 3) & 3], 3, laneoff);
+            const u32 x = __builtin_amdgcn_perm(b, a, 0x0c0c0500u);
+            const u32 y = __builtin_amdgcn_perm(d, c, 0x07020c0cu);
+            o[col] = __builtin_amdgcn_bitop3_b32(x, y, rk[NR][col], 0x56);  // (x | y) ^ rk
+        }
+#pragma unroll
+        for (int col = 0; col < 4; ++col)
+            s[i][col] = o[col];
+    }
 }
 
 template <int NR>
 __device__ __forceinline__ void aes_encrypt_tt(const lds_u8 *lds, u32 laneoff, const u32 (*rk)[4], u32 &s0, u32 &s1, u32 &s2,
                                                u32 &s3)
 {
+    u32 st[1][4] = {{s0, s1, s2, s3}};
+    aes_rounds_n<NR, 1, 1>(lds, laneoff, rk, st);
+    s0 = st[0][0], s1 = st[0][1], s2 = st[0][2], s3 = st[0][3];
+}
+
+// Counter-mode round caching. Within one record only the counter word changes, and while the counter stays below
+// 2^16 only its two low bytes do. Round 1 then has 2 varying lookups (the other 14 fold into per-record constants) and
+// round 2 has 8 (columns 2 and 3 of the round-1 output are constant): 138 instead of 160 T-table lookups per block.
+struct CtrCache {
+    u32 a0, a1, t2, t3, b0, b1, b2, b3;
+};
+
+// n0..n2: nonce words already XORed with round key 0; rk03: round key 0, word 3 (the counter word's high bytes are 0)
+template <int NR>
+__device__ __forceinline__ CtrCache ctr_cache_init(const lds_u8 *lds, u32 laneoff, const u32 (*rk)[4], u32 n0, u32 n1, u32 n2)
+{
+    const u32 h3 = rk[0][3];
+    CtrCache c;
+    c.a0 = xor3(te0(lds, n0, 0, laneoff), te2(lds, n2, 2, laneoff), rk[1][0]) ^ rotl8(te0(lds, n1, 1, laneoff));
+    c.a1 = xor3(te0(lds, n1, 0, laneoff), rotl8(te0(lds, n2, 1, laneoff)), rk[1][1]) ^ rotl8(te2(lds, n0, 3, laneoff));
+    c.t2 = xor3(te0(lds, n2, 0, laneoff), te2(lds, n0, 2, laneoff), rk[1][2]) ^
+           rotl8(te0(lds, h3, 1, laneoff) ^ te2(lds, n1, 3, laneoff));
+    c.t3 = xor3(te0(lds, h3, 0, laneoff), te2(lds, n1, 2, laneoff), rk[1][3]) ^
+           rotl8(te0(lds, n0, 1, laneoff) ^ te2(lds, n2, 3, laneoff));
+    c.b0 = xor3(te2(lds, c.t2, 2, laneoff), rotl8(te2(lds, c.t3, 3, laneoff)), rk[2][0]);
+    c.b1 = xor3(rotl8(te0(lds, c.t2, 1, laneoff)), te2(lds, c.t3, 2, laneoff), rk[2][1]);
+    c.b2 = xor3(te0(lds, c.t2, 0, laneoff), rotl8(te0(lds, c.t3, 1, laneoff)), rk[2][2]);
+    c.b3 = xor3(te0(lds, c.t3, 0, laneoff), rotl8(te2(lds, c.t2, 3, laneoff)), rk[2][3]);
+    return c;
+}
+
+// AES of NB counter blocks (nonce || ctr_i), every ctr_i < 2^16; s[i][3] holds bswap32(ctr_i) ^ rk[0][3] on entry
+// (words 0..2 are ignored) and the keystream block on return.
+template <int NR, int NB>
+__device__ __forceinline__ void aes_ctr_cached_n(const lds_u8 *lds, u32 laneoff, const u32 (*rk)[4], const CtrCache &c,
+                                                 u32 (&s)[NB][4])
+{
 #pragma unroll
-    for (int r = 1; r < NR; ++r) {
-        u32 t0 = xor3(te0(lds, s0, 0, laneoff), te2(lds, s2, 2, laneoff), rk[r][0]) ^
-                 rotl8(te0(lds, s1, 1, laneoff) ^ te2(lds, s3, 3, laneoff));
-        u32 t1 = xor3(te0(lds, s1, 0, laneoff), te2(lds, s3, 2, laneoff), rk[r][1]) ^
-                 rotl8(te0(lds, s2, 1, laneoff) ^ te2(lds, s0, 3, laneoff));
-        u32 t2 = xor3(te0(lds, s2, 0, laneoff), te2(lds, s0, 2, laneoff), rk[r][2]) ^
-                 rotl8(te0(lds, s3, 1, laneoff) ^ te2(lds, s1, 3, laneoff));
-        u32 t3 = xor3(te0(lds, s3, 0, laneoff), te2(lds, s1, 2, laneoff), rk[r][3]) ^
-                 rotl8(te0(lds, s0, 1, laneoff) ^ te2(lds, s2, 3, laneoff));
-        s0 = t0, s1 = t1, s2 = t2, s3 = t3;
+    for (int i = 0; i < NB; ++i) {
+        const u32 s3 = s[i][3];
+        const u32 u0 = c.a0 ^ rotl8(te2(lds, s3, 3, laneoff));
+        const u32 u1 = c.a1 ^ te2(lds, s3, 2, laneoff);
+        s[i][0] = xor3(c.b0, te0(lds, u0, 0, laneoff), rotl8(te0(lds, u1, 1, laneoff)));
+        s[i][1] = xor3(c.b1, te0(lds, u1, 0, laneoff), rotl8(te2(lds, u0, 3, laneoff)));
+        s[i][2] = xor3(c.b2, te2(lds, u0, 2, laneoff), rotl8(te2(lds, u1, 3, laneoff)));
+        s[i][3] = xor3(c.b3, rotl8(te0(lds, u0, 1, laneoff)), te2(lds, u1, 2, laneoff));
     }
-    // last round: SubBytes + ShiftRows + AddRoundKey; S(x) is byte 1/2 of Te0[x] and byte 0/3 of Te2[x]
-    u32 a, b, c, d, x, y, o[4];
-    const u32 st[4] = {s0, s1, s2, s3};
-#pragma unroll
-    for (int col = 0; col < 4; ++col) {
-        a = te2(lds, st[col], 0, laneoff);
-        b = te0(lds, st[(col + 1) & 3], 1, laneoff);
-        c = te0(lds, st[(col + 2) & 3], 2, laneoff);
-        d = te2(lds, st[(col + 3) & 3], 3, laneoff);
-        x = __builtin_amdgcn_perm(b, a, 0x0c0c0500u);
-        y = __builtin_amdgcn_perm(d, c, 0x07020c0cu);
-        o[col] = __builtin_amdgcn_bitop3_b32(x, y, rk[NR][col], 0x56);  // (x | y) ^ rk
-    }
-    s0 = o[0], s1 = o[1], s2 = o[2], s3 = o[3];
+    aes_rounds_n<NR, 3, NB>(lds, laneoff, rk, s);
 }
 
 // ------------------------------------------------------------------------------------------------ GHASH (tables)
 
-// returns a * H^(t+1), where tsel = 0x10000 | (t * 8192): table base for the lane
-__device__ __forceinline__ u32x4 gmul_tab(const lds_u8 *lds, u32x4 a, u32 tsel)
+// returns a * H^(t+1), where tsel = 0x10000 | (t * 8192): table base for the lane.
+// The 32 window lookups are independent; they are issued in four batches of 8 (32 VGPRs in flight) and folded with
+// 3-input XORs, so one multiply costs a few overlapped LDS round trips rather than a chain of 16.
+__device__ __forceinline__ u32x4 gmul_tab(const lds_u8 *, u32x4 a, u32 tsel)
 {
-    u32 r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+    u32x4 acc = {0, 0, 0, 0};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const u32 w = a[q];
         const u32 hi = w & 0xf0f0f0f0u, lo = (w << 4) & 0xf0f0f0f0u;
+#if GHASH_BATCH
+        u32x4 e[8];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const u32 sel = 0x0c020100u | (4u + k);
-            const u32 ahi = __builtin_amdgcn_perm(hi, tsel, sel);
-            const u32 alo = __builtin_amdgcn_perm(lo, tsel, sel);
-            const u32x4 e0 = *(const lds_u32x4 *)(lds + ahi + (8 * q + 2 * k) * 256);
-            const u32x4 e1 = *(const lds_u32x4 *)(lds + alo + (8 * q + 2 * k + 1) * 256);
-            r0 = xor3(r0, e0[0], e1[0]);
-            r1 = xor3(r1, e0[1], e1[1]);
-            r2 = xor3(r2, e0[2], e1[2]);
-            r3 = xor3(r3, e0[3], e1[3]);
+            e[2 * k] = lds_load128(__builtin_amdgcn_perm(hi, tsel, sel) + (8 * q + 2 * k) * 256);
+            e[2 * k + 1] = lds_load128(__builtin_amdgcn_perm(lo, tsel, sel) + (8 * q + 2 * k + 1) * 256);
         }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            u32 x0 = xor3(e[0][c], e[1][c], e[2][c]), x1 = xor3(e[3][c], e[4][c], e[5][c]);
+            acc[c] = xor3(acc[c], xor3(x0, x1, e[6][c]), e[7][c]);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // at most 8 entries (32 VGPRs) in flight
+#else
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const u32 sel = 0x0c020100u | (4u + k);
+            const u32x4 e0 = lds_load128(__builtin_amdgcn_perm(hi, tsel, sel) + (8 * q + 2 * k) * 256);
+            const u32x4 e1 = lds_load128(__builtin_amdgcn_perm(lo, tsel, sel) + (8 * q + 2 * k + 1) * 256);
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                acc[c] = xor3(acc[c], e0[c], e1[c]);
+        }
+#endif
     }
-    u32x4 r = {r0, r1, r2, r3};
-    return r;
+    return acc;
 }
 
 // ------------------------------------------------------------------------------------------------ byte-exact I/O
@@ -366,8 +462,10 @@ struct BatchArgs {
 
 #define RUN_SCAN_CAP 256  // records examined per key-run scan (multi-key batches)
 
-// Seals / opens the records [rec0 + slot] of one record group; all G lanes of a record cooperate (see file header).
-template <int NR, bool OPEN>
+// Seals / opens one record per G-lane group (see file header). Lane j owns GHASH stream positions j + G*m, m = 0..K-1,
+// and runs them NB at a time: the NB AES-CTR blocks of a step are independent (NB x 16 LDS lookups per round in
+// flight); their GHASH folds stay sequential (Horner with H^G, the record's last position with H^(G-j)).
+template <int NR, bool OPEN, int NB>
 __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u8 *lds, const u32 (&rk)[NR + 1][4], u32 iv0,
                                               u32 iv1, u32 iv2, u64 rec, bool valid, u32 j, u32 laneoff, u32 tsel_horner,
                                               u32 tsel_last)
@@ -397,52 +495,96 @@ __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u
     u32x4 acc = {0, 0, 0, 0};
     u32x4 ek0 = {0, 0, 0, 0};
 
-    for (u32 k = 0; k < Kmax; ++k) {
-        const bool act = k < K;
-        const int logical = (int)(j + G * k) - P;
-        const int b = logical - (int)na;
-        const bool is_data = act && logical >= (int)na && b < (int)nb;
-        const bool is_aad = act && logical >= 0 && logical < (int)na;
-        const bool is_len = act && logical == (int)(na + nb);
+    // counters run from 1 (J0) to nb + 1: the cached rounds need them below 2^16 for every record of the wave
+    const bool cached = !__any(valid && nb + 1 >= 65536u);
+    CtrCache cc = {};
+    if (cached)
+        cc = ctr_cache_init<NR>(lds, laneoff, rk, n0, n1, n2);
 
-        // AES-CTR: data lanes encrypt counter 2+b; every other lane encrypts J0 (only the length lane keeps it)
-        u32 s0 = n0, s1 = n1, s2 = n2;
-        u32 s3 = bswap32(is_data ? (u32)(b + 2) : 1u) ^ rk[0][3];
-        aes_encrypt_tt<NR>(lds, laneoff, rk, s0, s1, s2, s3);
-        const u32x4 ks = {s0, s1, s2, s3};
+    // data block of lane j at position m: b = j + G*m - P - na; a full 16-byte input block is loaded one step
+    // ahead, so its HBM latency hides under the AES of the current step
+    auto full_block = [&](u32 m, int &b) -> bool {
+        b = (int)(j + G * m) - P - (int)na;
+        return m < K && b >= 0 && b < (int)nb && L - 16u * (u32)b >= 16;
+    };
+    u32x4 nxt[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        int b;
+        nxt[i] = u32x4{0, 0, 0, 0};
+        if (full_block(i, b))
+            nxt[i] = *(const u32x4_u *)(src + 16u * (u32)b);
+    }
 
-        u32x4 X = {0, 0, 0, 0};
-        if (is_data) {
-            const u32 rem = L - 16u * (u32)b;
-            const uint8_t *ip = src + 16u * (u32)b;
-            uint8_t *op = dst + 16u * (u32)b;
-            if (rem >= 16) {
-                const u32x4 v = *(const u32x4_u *)ip;
-                const u32x4 o = v ^ ks;
-                *(u32x4_u *)op = o;
-                X = OPEN ? v : o;
-            } else {
-                const u32x4 v = load_partial(ip, rem);
-                const u32x4 o = mask_tail(v ^ ks, rem);
-                store_partial(op, o, rem);
-                X = OPEN ? v : o;
-            }
-        } else if (is_aad) {
-            const u32 rem = A - 16u * (u32)logical;
-            const uint8_t *ap = aadp + 16u * (u32)logical;
-            X = rem >= 16 ? *(const u32x4_u *)ap : load_partial(ap, rem);
-        } else if (is_len) {
-            const u64 abits = (u64)A * 8, cbits = (u64)L * 8;
-            X[0] = bswap32((u32)(abits >> 32));
-            X[1] = bswap32((u32)abits);
-            X[2] = bswap32((u32)(cbits >> 32));
-            X[3] = bswap32((u32)cbits);
-            ek0 = ks;
+    for (u32 m0 = 0; m0 < Kmax; m0 += NB) {
+        u32x4 cur[NB];
+        u32 st[NB][4];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            cur[i] = nxt[i];
+            int bn;
+            if (full_block(m0 + NB + i, bn))
+                nxt[i] = *(const u32x4_u *)(src + 16u * (u32)bn);
+            // AES-CTR input: data positions encrypt counter 2+b, all others J0 (kept by the length lane as E(K, J0))
+            const int logical = (int)(j + G * (m0 + i)) - P;
+            const int b = logical - (int)na;
+            const bool is_data = m0 + i < K && logical >= (int)na && b < (int)nb;
+            st[i][0] = n0, st[i][1] = n1, st[i][2] = n2;
+            st[i][3] = bswap32(is_data ? (u32)(b + 2) : 1u) ^ rk[0][3];
         }
-        acc ^= X;
-        const u32x4 prod = gmul_tab(lds, acc, k + 1 == K ? tsel_last : tsel_horner);
-        if (act)
-            acc = prod;
+        if (cached)
+            aes_ctr_cached_n<NR, NB>(lds, laneoff, rk, cc, st);
+        else
+            aes_rounds_n<NR, 1, NB>(lds, laneoff, rk, st);
+        __builtin_amdgcn_sched_barrier(0);
+
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            const u32 m = m0 + i;
+            const bool act = m < K;
+            const int logical = (int)(j + G * m) - P;
+            const int b = logical - (int)na;
+            const bool is_data = act && logical >= (int)na && b < (int)nb;
+            const bool is_aad = act && logical >= 0 && logical < (int)na;
+            const bool is_len = act && logical == (int)(na + nb);
+            const u32x4 ks = {st[i][0], st[i][1], st[i][2], st[i][3]};
+
+            u32x4 X = {0, 0, 0, 0};
+            if (is_data) {
+                const u32 rem = L - 16u * (u32)b;
+                uint8_t *op = dst + 16u * (u32)b;
+                if (rem >= 16) {
+                    const u32x4 v = cur[i];
+                    const u32x4 o = v ^ ks;
+                    *(u32x4_u *)op = o;
+                    X = OPEN ? v : o;
+                } else {
+                    const u32x4 v = load_partial(src + 16u * (u32)b, rem);
+                    const u32x4 o = mask_tail(v ^ ks, rem);
+                    store_partial(op, o, rem);
+                    X = OPEN ? v : o;
+                }
+            } else if (is_aad) {
+                const u32 rem = A - 16u * (u32)logical;
+                const uint8_t *ap = aadp + 16u * (u32)logical;
+                X = rem >= 16 ? *(const u32x4_u *)ap : load_partial(ap, rem);
+            } else if (is_len) {
+                const u64 abits = (u64)A * 8, cbits = (u64)L * 8;
+                X[0] = bswap32((u32)(abits >> 32));
+                X[1] = bswap32((u32)abits);
+                X[2] = bswap32((u32)(cbits >> 32));
+                X[3] = bswap32((u32)cbits);
+                ek0 = ks;
+            }
+            acc ^= X;
+            // scheduling fence: keeps the 32 table loads of this fold from being hoisted next to the other blocks'
+            // work (that hoisting spills them to scratch)
+            __builtin_amdgcn_sched_barrier(0);
+            const u32x4 prod = gmul_tab(lds, acc, m + 1 == K ? tsel_last : tsel_horner);
+            if (act)
+                acc = prod;
+            __builtin_amdgcn_sched_barrier(0);
+        }
     }
 
     // XOR over the G lanes of the record
@@ -468,12 +610,15 @@ __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u
 // Persistent kernel: workgroup w owns the contiguous record range [n*w/grid, n*(w+1)/grid) and walks it in key runs
 // (maximal stretches of equal key_idx, at most RUN_SCAN_CAP records); the GHASH tables in LDS are rebuilt only when
 // the key changes, so a single-key batch builds them once and a key-sorted many-connection batch once per key.
+// ENGINE_WG threads and 128+ KiB of LDS per workgroup: exactly one workgroup (ENGINE_WG/256 waves per SIMD) per CU, so
+// the register allocator may use the whole per-wave budget instead of chasing an occupancy the LDS budget rules out.
 template <int NR, bool OPEN>
-__global__ __launch_bounds__(ENGINE_WG) void gcm_batch_kernel(BatchArgs args)
+__global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGINE_WAVES_PER_SIMD, ENGINE_WAVES_PER_SIMD))) void gcm_batch_kernel(BatchArgs args)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     lds_u8 *lds = (lds_u8 *)smem;
     lds_u32 *s_run = (lds_u32 *)(lds + LDS_BYTES);  // scratch word after the tables
+    check_lds_base(smem);
     constexpr int G = ENGINE_G;
     constexpr int RPW = 64 / G;  // records per wave-iteration
 
@@ -534,7 +679,7 @@ __global__ __launch_bounds__(ENGINE_WG) void gcm_batch_kernel(BatchArgs args)
         const u64 ngroups = (run_end - pos + RPW - 1) / RPW;
         for (u64 grp = wave; grp < ngroups; grp += waves_per_wg) {
             const u64 rec = pos + grp * RPW + slot;
-            process_group<NR, OPEN>(args, lds, rk, iv0, iv1, iv2, rec, rec < run_end, j, laneoff, tsel_horner, tsel_last);
+            process_group<NR, OPEN, ENGINE_NB>(args, lds, rk, iv0, iv1, iv2, rec, rec < run_end, j, laneoff, tsel_horner, tsel_last);
         }
         pos = run_end;
     }
@@ -547,6 +692,7 @@ __global__ __launch_bounds__(256) void ecb_kernel(const KeyEntry *keys, const u3
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     lds_u8 *lds = (lds_u8 *)smem;
+    check_lds_base(smem);
     build_aes_tables(lds);
     __syncthreads();
     const u32 laneoff = (threadIdx.x & 31) * 4;
