@@ -47,67 +47,43 @@ def parse():
     return p.parse_args()
 
 
-class Rank:
-    def __init__(self, gpus: int):
-        import torch
+def make_rank(gpus: int):
+    import torch
 
-        self.torch = torch
-        self.world = int(os.environ.get("WORLD_SIZE", "1"))
-        self.rank = int(os.environ.get("RANK", "0"))
-        self.local = int(os.environ.get("LOCAL_RANK", "0"))
-        if self.world != gpus:
-            if self.world == 1 and gpus > 1:
-                raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
-        torch.cuda.set_device(self.local)
-        self.dev = torch.device("cuda", self.local)
-        self.dist = None
-        if self.world > 1:
-            import torch.distributed as dist
+    from picotls_amd.dist import RankContext
 
-            dist.init_process_group("nccl", device_id=self.dev)
-            self.dist = dist
-
-    def barrier(self):
-        if self.dist is not None:
-            self.dist.barrier()
-
-    def max(self, x: float) -> float:
-        if self.dist is None:
-            return x
-        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
-
-    def sum(self, x: float) -> float:
-        if self.dist is None:
-            return x
-        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.dev)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return float(t.item())
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and gpus > 1:
+        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    return RankContext.from_env("nccl", device=torch.device("cuda", local))
 
 
-def run_workload(R: Rank, wl, steps: int, warmup: int, verify: int, shard_global: bool):
+def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool):
     import torch
     import picotls_amd as pa
     from picotls_amd.records import algorithmic_bytes
     from picotls_amd.workloads import payload_torch
 
-    if shard_global:  # strong scaling: the global batch is split across ranks
-        per = wl.nrecs // R.world
-        begin = R.rank * per
-        end = wl.nrecs if R.rank == R.world - 1 else begin + per
+    from picotls_amd.dist import shard_for_rank, shard_weights
+
+    if shard_global:  # strong scaling: the global batch is split across ranks (by bytes for mixed lengths)
+        weights = None if wl.rec_len is not None else shard_weights(wl.lens(0, wl.nrecs))
+        begin, end = shard_for_rank(wl.nrecs, R.rank, R.world, weights)
     else:  # weak scaling: every rank processes a full batch (its own records)
         begin, end = 0, wl.nrecs
     b = wl.descriptors(begin, end)
     keys, ivs = wl.keys()
     ks = pa.Keyset(keys, ivs, wl.key_size)
-    dev = R.dev
+    dev = R.device
     d_seal = torch.from_numpy(b.seal.view(np.uint8).copy()).to(dev)
     d_open = torch.from_numpy(b.open.view(np.uint8).copy()).to(dev)
     d_aad = torch.from_numpy(wl.aad_arena(b, begin)).to(dev)
     d_pt = payload_torch(wl.seed + 7919 * (R.rank if not shard_global else 0), b.pt_bytes, dev)
+    zero_slot_padding(d_pt, b.seal, dev)  # so the round-trip check can compare whole arenas
     d_sealed = torch.empty(b.sealed_bytes, dtype=torch.uint8, device=dev)
-    d_back = torch.empty(b.pt_bytes, dtype=torch.uint8, device=dev)
+    d_back = torch.zeros(b.pt_bytes, dtype=torch.uint8, device=dev)
     d_ok = torch.zeros(b.n, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
@@ -155,6 +131,21 @@ def run_workload(R: Rank, wl, steps: int, warmup: int, verify: int, shard_global
     ks.free()
     torch.cuda.empty_cache()
     return res
+
+
+def zero_slot_padding(arena, recs, dev):
+    """Zeroes the bytes between the end of each record and the next 16-byte slot boundary."""
+    import torch
+
+    lens = recs["len"].astype(np.int64)
+    pad = (-lens) % 16
+    if not pad.any():
+        return
+    starts = torch.from_numpy(recs["in_off"].astype(np.int64) + lens).to(dev)
+    padt = torch.from_numpy(pad).to(dev)
+    for p in range(15):
+        sel = starts[padt > p] + p
+        arena[sel] = 0
 
 
 def spot_check(wl, b, keys, ivs, d_pt, d_aad, d_sealed, begin, nsample: int = 64):
@@ -253,6 +244,92 @@ def cpu_baseline(wl, seconds: float):
             "open_GiBps": round(b.payload_bytes * reps / 2**30 / t_open, 3)}
 
 
+def run_e2e(R, wl, nchunks: int = 16, reps: int = 3):
+    """Records that start and end in host memory (socket / NIC buffers): pinned host -> H2D -> seal -> D2H, then
+    the sealed records back through H2D -> open -> D2H. Serial (one stream) and pipelined (chunks over three
+    streams, so copies in both directions overlap the kernels). Payload GiB/s per direction (seal+open averaged)."""
+    import torch
+    import picotls_amd as pa
+
+    b = wl.descriptors(0, wl.nrecs)
+    keys, ivs = wl.keys()
+    ks = pa.Keyset(keys, ivs, wl.key_size)
+    dev = R.device
+    from picotls_amd.workloads import payload_np
+
+    h_pt = torch.from_numpy(payload_np(wl.seed, 0, b.pt_bytes).copy()).pin_memory()
+    h_sealed = torch.empty(b.sealed_bytes, dtype=torch.uint8).pin_memory()
+    h_back = torch.empty(b.pt_bytes, dtype=torch.uint8).pin_memory()
+    d_aad = torch.from_numpy(wl.aad_arena(b, 0)).to(dev)
+    d_pt = torch.empty(b.pt_bytes, dtype=torch.uint8, device=dev)
+    d_sealed = torch.empty(b.sealed_bytes, dtype=torch.uint8, device=dev)
+    d_back = torch.empty(b.pt_bytes, dtype=torch.uint8, device=dev)
+    d_ok = torch.empty(b.n, dtype=torch.uint8, device=dev)
+    # chunk c covers records [r0, r1): contiguous byte ranges in every arena; descriptors are rebased per chunk
+    bounds = np.linspace(0, b.n, nchunks + 1).astype(np.int64)
+    chunks = []
+    for c in range(nchunks):
+        r0, r1 = int(bounds[c]), int(bounds[c + 1])
+        if r1 <= r0:
+            continue
+        seal = b.seal[r0:r1].copy()
+        opn = b.open[r0:r1].copy()
+        p0, s0 = int(b.seal["in_off"][r0]), int(b.seal["out_off"][r0])
+        p1 = int(b.seal["in_off"][r1 - 1]) + (int(b.seal["len"][r1 - 1]) + 15) // 16 * 16
+        s1 = int(b.seal["out_off"][r1 - 1]) + (int(b.seal["len"][r1 - 1]) + 31) // 16 * 16
+        seal["in_off"] -= p0
+        seal["out_off"] -= s0
+        opn["in_off"] -= s0
+        opn["out_off"] -= p0
+        chunks.append((r0, r1, p0, p1, s0, s1, torch.from_numpy(seal.view(np.uint8).copy()).to(dev),
+                       torch.from_numpy(opn.view(np.uint8).copy()).to(dev)))
+    streams = [torch.cuda.Stream(dev) for _ in range(3)]
+
+    def one_pass(pipelined: bool):
+        for i, (r0, r1, p0, p1, s0, s1, ds, do) in enumerate(chunks):
+            st = streams[i % 3] if pipelined else torch.cuda.current_stream(dev)
+            with torch.cuda.stream(st):
+                d_pt[p0:p1].copy_(h_pt[p0:p1], non_blocking=True)
+                pa.seal_batch(ks, ds.data_ptr(), r1 - r0, d_pt.data_ptr() + p0, d_aad.data_ptr(), d_sealed.data_ptr() + s0,
+                              st.cuda_stream)
+                h_sealed[s0:s1].copy_(d_sealed[s0:s1], non_blocking=True)
+        torch.cuda.synchronize(dev)
+        t_seal = time.perf_counter()
+        for i, (r0, r1, p0, p1, s0, s1, ds, do) in enumerate(chunks):
+            st = streams[i % 3] if pipelined else torch.cuda.current_stream(dev)
+            with torch.cuda.stream(st):
+                d_sealed[s0:s1].copy_(h_sealed[s0:s1], non_blocking=True)
+                pa.open_batch(ks, do.data_ptr(), r1 - r0, d_sealed.data_ptr() + s0, d_aad.data_ptr(), d_back.data_ptr() + p0,
+                              d_ok.data_ptr() + r0, st.cuda_stream)
+                h_back[p0:p1].copy_(d_back[p0:p1], non_blocking=True)
+        torch.cuda.synchronize(dev)
+        return t_seal
+
+    out = {}
+    for mode in ("serial", "pipelined"):
+        one_pass(mode == "pipelined")
+        ts = to = 0.0
+        for _ in range(reps):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            t_mid = one_pass(mode == "pipelined")
+            t1 = time.perf_counter()
+            ts += t_mid - t0
+            to += t1 - t_mid
+        gib = b.payload_bytes * reps / 2**30
+        out[mode] = {"seal_GiBps": round(gib / ts, 2), "open_GiBps": round(gib / to, 2),
+                     "seal_open_GiBps": round(2 * gib / (ts + to), 2)}
+    ok = bool(d_ok.min().item() == 1)
+    m = np.zeros(b.pt_bytes, bool)
+    for o, ln in zip(b.seal["in_off"], b.seal["len"]):
+        m[int(o):int(o) + int(ln)] = True
+    same = bool(np.array_equal(h_back.numpy()[m], h_pt.numpy()[m]))
+    out.update({"records": b.n, "payload_bytes": b.payload_bytes, "chunks": len(chunks), "verified": ok and same,
+                "note": "pinned host buffers; PCIe Gen5 x16 ~63 GB/s/direction bounds this path"})
+    ks.free()
+    return out
+
+
 def traffic_from_profiles(workload: str):
     """Corrected HBM bytes per seal launch from the committed rocprofv3 PMC summary (profiles/*pmc*.json)."""
     path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
@@ -268,16 +345,16 @@ def main():
     args = parse()
     from picotls_amd.workloads import WORKLOADS
 
-    R = Rank(args.gpus)
+    from picotls_amd.dist import aggregate_throughput
+
+    R = make_rank(args.gpus)
     wl = WORKLOADS[args.workload]
     if args.records:
         wl = wl.scaled(args.records)
     shard_global = args.workload == "shard1200"
     res = run_workload(R, wl, args.steps, args.warmup, args.verify, shard_global)
 
-    wall = R.max(res["wall_s"])
-    total_payload = R.sum(float(res["payload_bytes"]))
-    value = 2 * total_payload * args.steps / wall / 2**30
+    value, wall = aggregate_throughput(R, res["payload_bytes"], res["wall_s"], args.steps)
     seal_s, open_s = res["seal_ms"] / 1e3, res["open_ms"] / 1e3
     achieved = res["seal_alg_bytes"] / seal_s / 1e9
     out = {
@@ -314,9 +391,8 @@ def main():
         if args.records:
             w2 = w2.scaled(max(1, args.records * (wl.rec_len or 8192) // (w2.rec_len or 8192)))
         r2 = run_workload(R, w2, args.steps, args.warmup, args.verify, name == "shard1200")
-        wall2 = R.max(r2["wall_s"])
-        tot2 = R.sum(float(r2["payload_bytes"]))
-        extra[name] = {"value": round(2 * tot2 * args.steps / wall2 / 2**30, 3), "unit": "GiB/s",
+        v2, _ = aggregate_throughput(R, r2["payload_bytes"], r2["wall_s"], args.steps)
+        extra[name] = {"value": round(v2, 3), "unit": "GiB/s",
                        "records_per_gpu": r2["records"], "record_len": w2.rec_len,
                        "seal_GiBps": round(r2["payload_bytes"] / (r2["seal_ms"] / 1e3) / 2**30, 3),
                        "open_GiBps": round(r2["payload_bytes"] / (r2["open_ms"] / 1e3) / 2**30, 3),
@@ -326,14 +402,15 @@ def main():
                                     "fusion_spot_check": r2.get("fusion_spot_check")}}
     if extra:
         out["extra"] = extra
+    if args.e2e:
+        out["e2e_host_buffers"] = run_e2e(R, WORKLOADS[args.workload].scaled(min(wl.nrecs, max(1, (4 << 30) // (wl.rec_len or 8192)))))
     if R.rank == 0 and R.world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds)
     elif R.rank == 0:
         out["cpu_baseline"] = None
     if R.rank == 0:
         print(json.dumps(out), flush=True)
-    if R.dist is not None:
-        R.dist.destroy_process_group()
+    R.close()
 
 
 if __name__ == "__main__":
