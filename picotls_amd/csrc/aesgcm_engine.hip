@@ -280,11 +280,96 @@ __device__ __forceinline__ void check_lds_base(const void *smem)
 __device__ __forceinline__ u32 te0(const lds_u8 *, u32 w, int r, u32 laneoff) { return lds_load32(TE_ADDR(w, r, laneoff)); }
 __device__ __forceinline__ u32 te2(const lds_u8 *, u32 w, int r, u32 laneoff) { return lds_load32(TE_ADDR(w, r, laneoff) + 128); }
 
+// Explicitly scheduled lookups (ENGINE_ASM_ROUNDS): the reads are issued from inline asm, so the compiler neither
+// reorders them nor inserts waits for them; lgkm_wait<N>() waits until at most N LDS/SMEM operations are outstanding
+// and, through its in/out operands, orders every use of the named values after that wait. LDS returns in order, so
+// waiting for <= N outstanding guarantees every read issued more than N reads ago has landed (other outstanding ops only
+// make the wait stricter).
+#ifndef ENGINE_ASM_ROUNDS
+#define ENGINE_ASM_ROUNDS 0
+#endif
+__device__ __forceinline__ u32 te0_issue(u32 w, int r, u32 laneoff)
+{
+    u32 v;
+    asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(TE_ADDR(w, r, laneoff)));
+    return v;
+}
+__device__ __forceinline__ u32 te2_issue(u32 w, int r, u32 laneoff)
+{
+    u32 v;
+    asm volatile("ds_read_b32 %0, %1 offset:128" : "=v"(v) : "v"(TE_ADDR(w, r, laneoff)));
+    return v;
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait(u32 &a, u32 &b)
+{
+    asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N));
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait(u32 &a, u32 &b, u32 &c, u32 &d)
+{
+    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "i"(N));
+}
+
+// One full T-table round with all 16 lookups issued back to back (column-major) and the columns combined as their
+// four reads land.
+__device__ __forceinline__ void aes_round_asm(u32 (&s)[4], const u32 (&rk)[4], u32 laneoff)
+{
+    u32 e[4][4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        e[c][0] = te0_issue(s[c], 0, laneoff);
+        e[c][1] = te2_issue(s[(c + 2) & 3], 2, laneoff);
+        e[c][2] = te0_issue(s[(c + 1) & 3], 1, laneoff);
+        e[c][3] = te2_issue(s[(c + 3) & 3], 3, laneoff);
+    }
+    lgkm_wait<12>(e[0][0], e[0][1], e[0][2], e[0][3]);
+    s[0] = xor3(e[0][0], e[0][1], rk[0]) ^ rotl8(e[0][2] ^ e[0][3]);
+    lgkm_wait<8>(e[1][0], e[1][1], e[1][2], e[1][3]);
+    s[1] = xor3(e[1][0], e[1][1], rk[1]) ^ rotl8(e[1][2] ^ e[1][3]);
+    lgkm_wait<4>(e[2][0], e[2][1], e[2][2], e[2][3]);
+    s[2] = xor3(e[2][0], e[2][1], rk[2]) ^ rotl8(e[2][2] ^ e[2][3]);
+    lgkm_wait<0>(e[3][0], e[3][1], e[3][2], e[3][3]);
+    s[3] = xor3(e[3][0], e[3][1], rk[3]) ^ rotl8(e[3][2] ^ e[3][3]);
+}
+
+__device__ __forceinline__ void aes_last_round_asm(u32 (&s)[4], const u32 (&rk)[4], u32 laneoff)
+{
+    u32 e[4][4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        e[c][0] = te2_issue(s[c], 0, laneoff);
+        e[c][1] = te0_issue(s[(c + 1) & 3], 1, laneoff);
+        e[c][2] = te0_issue(s[(c + 2) & 3], 2, laneoff);
+        e[c][3] = te2_issue(s[(c + 3) & 3], 3, laneoff);
+    }
+    u32 o[4];
+#define LAST_COL(c, N)                                                                                                 \
+    lgkm_wait<N>(e[c][0], e[c][1], e[c][2], e[c][3]);                                                                  \
+    o[c] = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(e[c][1], e[c][0], 0x0c0c0500u),                          \
+                                       __builtin_amdgcn_perm(e[c][3], e[c][2], 0x07020c0cu), rk[c], 0x56)
+    LAST_COL(0, 12);
+    LAST_COL(1, 8);
+    LAST_COL(2, 4);
+    LAST_COL(3, 0);
+#undef LAST_COL
+    s[0] = o[0], s[1] = o[1], s[2] = o[2], s[3] = o[3];
+}
+
 // rounds FIRST .. NR of AES (T-table rounds, then the final SubBytes/ShiftRows/AddRoundKey) on NB independent
 // LE-column states; the NB blocks advance in lockstep so each round has 16*NB independent LDS lookups in flight.
 template <int NR, int FIRST, int NB>
 __device__ __forceinline__ void aes_rounds_n(const lds_u8 *lds, u32 laneoff, const u32 (*rk)[4], u32 (&s)[NB][4])
 {
+#if ENGINE_ASM_ROUNDS
+    if constexpr (NB == 1) {
+#pragma unroll
+        for (int r = FIRST; r < NR; ++r)
+            aes_round_asm(s[0], rk[r], laneoff);
+        aes_last_round_asm(s[0], rk[NR], laneoff);
+        return;
+    }
+#endif
 #pragma unroll
     for (int r = FIRST; r < NR; ++r) {
 #pragma unroll
@@ -361,6 +446,29 @@ template <int NR, int NB>
 __device__ __forceinline__ void aes_ctr_cached_n(const lds_u8 *lds, u32 laneoff, const u32 (*rk)[4], const CtrCache &c,
                                                  u32 (&s)[NB][4])
 {
+#if ENGINE_ASM_ROUNDS
+    if constexpr (NB == 1) {
+        const u32 s3 = s[0][3];
+        u32 f0 = te2_issue(s3, 3, laneoff), f1 = te2_issue(s3, 2, laneoff);
+        lgkm_wait<0>(f0, f1);
+        const u32 u0 = c.a0 ^ rotl8(f0), u1 = c.a1 ^ f1;
+        u32 g[8];
+        g[0] = te0_issue(u0, 0, laneoff), g[1] = te0_issue(u1, 1, laneoff);
+        g[2] = te0_issue(u1, 0, laneoff), g[3] = te2_issue(u0, 3, laneoff);
+        g[4] = te2_issue(u0, 2, laneoff), g[5] = te2_issue(u1, 3, laneoff);
+        g[6] = te0_issue(u0, 1, laneoff), g[7] = te2_issue(u1, 2, laneoff);
+        lgkm_wait<6>(g[0], g[1]);
+        s[0][0] = xor3(c.b0, g[0], rotl8(g[1]));
+        lgkm_wait<4>(g[2], g[3]);
+        s[0][1] = xor3(c.b1, g[2], rotl8(g[3]));
+        lgkm_wait<2>(g[4], g[5]);
+        s[0][2] = xor3(c.b2, g[4], rotl8(g[5]));
+        lgkm_wait<0>(g[6], g[7]);
+        s[0][3] = xor3(c.b3, rotl8(g[6]), g[7]);
+        aes_rounds_n<NR, 3, NB>(lds, laneoff, rk, s);
+        return;
+    }
+#endif
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
         const u32 s3 = s[i][3];
