@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget of the cpu_baseline leg")
     p.add_argument("--e2e", action="store_true", help="also time pinned-host -> H2D -> seal -> D2H (DESIGN.md)")
+    p.add_argument("--schedule", default="auto", choices=["auto", "lockstep", "chunked"],
+                   help="batch schedule (ptls_mi355x_keyset_set_schedule)")
     p.add_argument("--verify", type=int, default=1, help="verify round trip + fusion spot checks after timing")
     return p.parse_args()
 
@@ -60,7 +62,7 @@ def make_rank(gpus: int):
     return RankContext.from_env("nccl", device=torch.device("cuda", local))
 
 
-def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool):
+def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool, schedule: str = "auto"):
     import torch
     import picotls_amd as pa
     from picotls_amd.records import algorithmic_bytes
@@ -76,6 +78,7 @@ def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool
     b = wl.descriptors(begin, end)
     keys, ivs = wl.keys()
     ks = pa.Keyset(keys, ivs, wl.key_size)
+    ks.set_schedule(schedule)
     dev = R.device
     d_seal = torch.from_numpy(b.seal.view(np.uint8).copy()).to(dev)
     d_open = torch.from_numpy(b.open.view(np.uint8).copy()).to(dev)
@@ -254,6 +257,7 @@ def run_e2e(R, wl, nchunks: int = 16, reps: int = 3):
     b = wl.descriptors(0, wl.nrecs)
     keys, ivs = wl.keys()
     ks = pa.Keyset(keys, ivs, wl.key_size)
+    ks.set_schedule(schedule)
     dev = R.device
     from picotls_amd.workloads import payload_np
 
@@ -352,7 +356,7 @@ def main():
     if args.records:
         wl = wl.scaled(args.records)
     shard_global = args.workload == "shard1200"
-    res = run_workload(R, wl, args.steps, args.warmup, args.verify, shard_global)
+    res = run_workload(R, wl, args.steps, args.warmup, args.verify, shard_global, args.schedule)
 
     value, wall = aggregate_throughput(R, res["payload_bytes"], res["wall_s"], args.steps)
     seal_s, open_s = res["seal_ms"] / 1e3, res["open_ms"] / 1e3
@@ -390,7 +394,7 @@ def main():
         w2 = WORKLOADS[name]
         if args.records:
             w2 = w2.scaled(max(1, args.records * (wl.rec_len or 8192) // (w2.rec_len or 8192)))
-        r2 = run_workload(R, w2, args.steps, args.warmup, args.verify, name == "shard1200")
+        r2 = run_workload(R, w2, args.steps, args.warmup, args.verify, name == "shard1200", args.schedule)
         v2, _ = aggregate_throughput(R, r2["payload_bytes"], r2["wall_s"], args.steps)
         extra[name] = {"value": round(v2, 3), "unit": "GiB/s",
                        "records_per_gpu": r2["records"], "record_len": w2.rec_len,

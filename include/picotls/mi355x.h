@@ -89,6 +89,20 @@ int ptls_mi355x_keyset_get_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, void *iv
 int ptls_mi355x_keyset_set_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, const void *iv);
 
 /**
+ * Batch schedule used by seal_batch / open_batch on this keyset (no reference counterpart: fusion processes one record
+ * per call). Results are identical under every schedule; only the work distribution differs.
+ *   AUTO      chunked for keysets of more than one key, lockstep otherwise (the default)
+ *   LOCKSTEP  one record per 8-lane group, whole records; best for uniform lengths under one key
+ *   CHUNKED   records cut into 1 KiB GHASH units pulled by waves from a queue and recombined with H^64; balances
+ *             mixed lengths and short per-connection key runs
+ * Returns 0, or -1 for an unknown schedule.
+ */
+#define PTLS_MI355X_SCHEDULE_AUTO 0
+#define PTLS_MI355X_SCHEDULE_LOCKSTEP 1
+#define PTLS_MI355X_SCHEDULE_CHUNKED 2
+int ptls_mi355x_keyset_set_schedule(ptls_mi355x_keyset_t *ks, int schedule);
+
+/**
  * Seals nrecs records in one launch. recs, in, aad, out are DEVICE pointers. Asynchronous on `stream`.
  * Returns 0 on success, a negative value on invalid arguments or launch failure.
  */

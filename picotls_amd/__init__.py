@@ -35,6 +35,7 @@ ABI_FUNCTIONS = (
     "ptls_mi355x_keyset_key_size",
     "ptls_mi355x_keyset_get_iv",
     "ptls_mi355x_keyset_set_iv",
+    "ptls_mi355x_keyset_set_schedule",
     "ptls_mi355x_seal_batch",
     "ptls_mi355x_open_batch",
     "ptls_mi355x_ecb_batch",
@@ -72,6 +73,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.ptls_mi355x_keyset_key_size.restype = sz
     lib.ptls_mi355x_keyset_get_iv.argtypes = [vp, sz, vp]
     lib.ptls_mi355x_keyset_set_iv.argtypes = [vp, sz, vp]
+    lib.ptls_mi355x_keyset_set_schedule.argtypes = [vp, ci]
     lib.ptls_mi355x_seal_batch.argtypes = [vp, vp, sz, vp, vp, vp, vp]
     lib.ptls_mi355x_open_batch.argtypes = [vp, vp, sz, vp, vp, vp, vp, vp]
     lib.ptls_mi355x_ecb_batch.argtypes = [vp, vp, vp, vp, sz, vp]
@@ -144,6 +146,15 @@ class Keyset:
     def set_iv(self, iv: bytes, idx: int = 0) -> None:
         if load_library().ptls_mi355x_keyset_set_iv(self.handle, idx, _buf(bytes(iv))) != 0:
             raise _err("set_iv")
+
+    SCHEDULES = {"auto": 0, "lockstep": 1, "chunked": 2}
+
+    def set_schedule(self, schedule: str) -> None:
+        """Batch schedule (ptls_mi355x_keyset_set_schedule): "auto", "lockstep" or "chunked"."""
+        if schedule not in self.SCHEDULES:
+            raise ValueError(f"unknown schedule {schedule!r}")
+        if load_library().ptls_mi355x_keyset_set_schedule(self.handle, self.SCHEDULES[schedule]) != 0:
+            raise _err("set_schedule")
 
 
 def seal_batch(ks: Keyset, recs_ptr: int, nrecs: int, in_ptr: int, aad_ptr: int, out_ptr: int, stream: int = 0) -> None:

@@ -82,7 +82,7 @@ __constant__ SboxTable c_sbox = make_sbox();
 struct KeyEntry {
     u32 rk[15][4];  // round keys, LE column words
     u32 iv[4];      // static IV as LE words (word 3 = 0)
-    u32 h[16][4];   // H^1 .. H^16 as GHASH elements (LE words)
+    u32 h[16][4];   // GHASH elements (LE words): [0..7] = H^1..H^8, [8] = H^CHUNK_BLOCKS, [9..15] = 0
 };
 static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 
@@ -103,6 +103,21 @@ static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 #define LDS_BYTES (LDS_AES_BYTES + ENGINE_G * GHASH_TABLE_BYTES)
 #define LDS_ALLOC (LDS_BYTES + 16)  // + scratch word for the key-run scan
 
+// Chunked schedule (many-key batches): records are cut into units of at most CHUNK_BLOCKS GHASH-stream blocks, and
+// the per-unit GHASH partials are recombined with H^CHUNK_BLOCKS (one more 8 KiB table, LDS table slot 8).
+#define CHUNK_BLOCKS 64
+#define CHUNK_STEPS (CHUNK_BLOCKS / ENGINE_G)
+#define CHUNK_MAX_UNITS 64   // records longer than CHUNK_MAX_UNITS units (> ~64 KiB) are processed as one unit
+#define CRUN_RECS 256        // records per run (one key)
+#define CRUN_UNITS 1024      // units per run
+#define CLDS_CTL (LDS_BYTES + GHASH_TABLE_BYTES)                // 16 control words
+#define CLDS_UBASE (CLDS_CTL + 64)                              // u32[CRUN_RECS + 1]: first unit of each record
+#define CLDS_EK0 (CLDS_UBASE + 4 * (CRUN_RECS + 16))            // 16 B per record: E(K, J0)
+#define CLDS_PART (CLDS_EK0 + 16 * CRUN_RECS)                   // 16 B per unit: GHASH partial
+#define CLDS_ALLOC (CLDS_PART + 16 * CRUN_UNITS)
+static_assert(CLDS_ALLOC <= 160 * 1024, "chunked schedule LDS budget");
+static_assert(CHUNK_BLOCKS % ENGINE_G == 0, "units are whole steps");
+
 // ------------------------------------------------------------------------------------------------ small helpers
 
 __device__ __forceinline__ u32 bswap32(u32 x) { return __builtin_bswap32(x); }
@@ -120,6 +135,18 @@ __device__ __forceinline__ void gf_mulx_be(u32 &b0, u32 &b1, u32 &b2, u32 &b3)
 }
 
 // ------------------------------------------------------------------------------------------------ keyset setup
+
+// x = x * y in GF(2^128), big-endian words (SP 800-38D Algorithm 1); setup only
+__device__ void gf_mul_be(u32 (&x)[4], const u32 (&y)[4])
+{
+    u32 z0 = 0, z1 = 0, z2 = 0, z3 = 0, v0 = y[0], v1 = y[1], v2 = y[2], v3 = y[3];
+    for (int b = 0; b < 128; ++b) {
+        if ((x[b >> 5] >> (31 - (b & 31))) & 1)
+            z0 ^= v0, z1 ^= v1, z2 ^= v2, z3 ^= v3;
+        gf_mulx_be(v0, v1, v2, v3);
+    }
+    x[0] = z0, x[1] = z1, x[2] = z2, x[3] = z3;
+}
 
 __device__ __forceinline__ u32 sub_word(u32 w)
 {
@@ -191,19 +218,20 @@ __global__ void keyset_setup_kernel(const uint8_t *__restrict__ keys, const uint
     aes_plain(rk, nr, s);
     // H as big-endian words for the bitwise multiply (SP 800-38D Algorithm 1)
     const u32 h0 = bswap32(s[0]), h1 = bswap32(s[1]), h2 = bswap32(s[2]), h3 = bswap32(s[3]);
-    u32 p0 = h0, p1 = h1, p2 = h2, p3 = h3;  // current power
-    for (int n = 0; n < 16; ++n) {
-        e->h[n][0] = bswap32(p0), e->h[n][1] = bswap32(p1), e->h[n][2] = bswap32(p2), e->h[n][3] = bswap32(p3);
-        // p = p * H
-        u32 z0 = 0, z1 = 0, z2 = 0, z3 = 0, v0 = h0, v1 = h1, v2 = h2, v3 = h3;
-        u32 x[4] = {p0, p1, p2, p3};
-        for (int b = 0; b < 128; ++b) {
-            if ((x[b >> 5] >> (31 - (b & 31))) & 1)
-                z0 ^= v0, z1 ^= v1, z2 ^= v2, z3 ^= v3;
-            gf_mulx_be(v0, v1, v2, v3);
-        }
-        p0 = z0, p1 = z1, p2 = z2, p3 = z3;
+    const u32 hb[4] = {h0, h1, h2, h3};
+    u32 p[4] = {h0, h1, h2, h3};  // current power, big-endian words
+    for (int n = 1; n <= CHUNK_BLOCKS; ++n) {
+        if (n <= 8)
+            for (int c = 0; c < 4; ++c)
+                e->h[n - 1][c] = bswap32(p[c]);
+        if (n == CHUNK_BLOCKS)
+            for (int c = 0; c < 4; ++c)
+                e->h[8][c] = bswap32(p[c]);
+        gf_mul_be(p, hb);
     }
+    for (int n = 9; n < 16; ++n)
+        for (int c = 0; c < 4; ++c)
+            e->h[n][c] = 0;
 }
 
 // ------------------------------------------------------------------------------------------------ LDS tables
@@ -228,9 +256,9 @@ __device__ void build_aes_tables(lds_u8 *lds)
 // GHASH tables for H^1..H^G of one key: table t (H^(t+1)), window p (x^(4p)..x^(4p+3)), entry n (4-bit value, MSB
 // = coefficient of x^(4p)) = sum over set bits of n of x^(4p+q) * H^(t+1). Thread (t, p, q) computes
 // V_q = x^(4p+q) * H^(t+1) and, via shuffles with its 3 window neighbours, entries n = 4q .. 4q+3.
-__device__ void build_ghash_tables(lds_u8 *lds, const KeyEntry *__restrict__ key)
+__device__ void build_ghash_tables(lds_u8 *lds, const KeyEntry *__restrict__ key, u32 ntables = ENGINE_G)
 {
-    for (u32 idx = threadIdx.x; idx < ENGINE_G * 128; idx += blockDim.x) {
+    for (u32 idx = threadIdx.x; idx < ntables * 128; idx += blockDim.x) {
         u32 t = idx >> 7, i = idx & 127, p = i >> 2, q = i & 3;
         u32 b0 = bswap32(key->h[t][0]), b1 = bswap32(key->h[t][1]), b2 = bswap32(key->h[t][2]), b3 = bswap32(key->h[t][3]);
         for (u32 k = 0; k < i; ++k)
@@ -484,7 +512,7 @@ __device__ __forceinline__ void aes_ctr_cached_n(const lds_u8 *lds, u32 laneoff,
 
 // ------------------------------------------------------------------------------------------------ GHASH (tables)
 
-// returns a * H^(t+1), where tsel = 0x10000 | (t * 8192): table base for the lane.
+// returns a * (table t's power), where tsel = 0x10000 + t * 8192: table base for the lane (t < 8: H^(t+1)).
 // The 32 window lookups are independent; they are issued in four batches of 8 (32 VGPRs in flight) and folded with
 // 3-input XORs, so one multiply costs a few overlapped LDS round trips rather than a chain of 16.
 __device__ __forceinline__ u32x4 gmul_tab(const lds_u8 *, u32x4 a, u32 tsel)
@@ -570,28 +598,28 @@ struct BatchArgs {
 
 #define RUN_SCAN_CAP 256  // records examined per key-run scan (multi-key batches)
 
-// Seals / opens one record per G-lane group (see file header). Lane j owns GHASH stream positions j + G*m, m = 0..K-1,
-// and runs them NB at a time: the NB AES-CTR blocks of a step are independent (NB x 16 LDS lookups per round in
-// flight); their GHASH folds stay sequential (Horner with H^G, the record's last position with H^(G-j)).
+// GHASH/CTR work of one G-lane group on steps [m_lo, m_hi) of record r's stream (see file header): lane j owns stream
+// positions j + G*m and runs them NB at a time. The NB AES-CTR blocks of a step are independent (NB x 16 LDS lookups
+// per round in flight); their GHASH folds stay sequential (Horner with H^G, the segment's last step with H^(G-j)).
+// On return every lane of the group holds the segment's GHASH partial sum(X_i * H^(end - i)) and the length lane
+// (lane G-1, when the segment holds the length block) holds E(K, J0) in ek0. Invalid groups pass m_lo == m_hi.
 template <int NR, bool OPEN, int NB>
-__device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u8 *lds, const u32 (&rk)[NR + 1][4], u32 iv0,
-                                              u32 iv1, u32 iv2, u64 rec, bool valid, u32 j, u32 laneoff, u32 tsel_horner,
-                                              u32 tsel_last)
+__device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 *lds, const u32 (&rk)[NR + 1][4], u32 iv0,
+                                            u32 iv1, u32 iv2, const ptls_mi355x_record_t &r, bool valid, u32 m_lo,
+                                            u32 m_hi, u32 j, u32 laneoff, u32 tsel_horner, u32 tsel_last, u32x4 &acc,
+                                            u32x4 &ek0, bool finish, u64 rec)
 {
     constexpr int G = ENGINE_G;
-    ptls_mi355x_record_t r = {};
-    if (valid)
-        r = args.recs[rec];
     const u32 L = r.len, A = r.aad_len;
     const u32 na = (A + 15) >> 4, nb = (L + 15) >> 4;
     const u32 total = na + nb + 1;
-    const u32 K = valid ? (total + G - 1) / G : 0;
+    const u32 K = (total + G - 1) / G;
     const int P = (int)(K * G) - (int)total;
 
-    u32 Kmax = K;
+    u32 Smax = m_hi - m_lo;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1)
-        Kmax = max(Kmax, (u32)__shfl_xor((int)Kmax, off, 64));
+        Smax = max(Smax, (u32)__shfl_xor((int)Smax, off, 64));
 
     const u32 n0 = iv0 ^ rk[0][0];
     const u32 n1 = iv1 ^ bswap32((u32)(r.seq >> 32)) ^ rk[0][1];
@@ -600,8 +628,8 @@ __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u
     uint8_t *dst = args.out + r.out_off;
     const uint8_t *aadp = args.aad + r.aad_off;
 
-    u32x4 acc = {0, 0, 0, 0};
-    u32x4 ek0 = {0, 0, 0, 0};
+    acc = u32x4{0, 0, 0, 0};
+    ek0 = u32x4{0, 0, 0, 0};
 
     // counters run from 1 (J0) to nb + 1: the cached rounds need them below 2^16 for every record of the wave
     const bool cached = !__any(valid && nb + 1 >= 65536u);
@@ -609,22 +637,23 @@ __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u
     if (cached)
         cc = ctr_cache_init<NR>(lds, laneoff, rk, n0, n1, n2);
 
-    // data block of lane j at position m: b = j + G*m - P - na; a full 16-byte input block is loaded one step
-    // ahead, so its HBM latency hides under the AES of the current step
+    // data block of lane j at step m: b = j + G*m - P - na; a full 16-byte input block is loaded one step ahead, so
+    // its HBM latency hides under the AES of the current step
     auto full_block = [&](u32 m, int &b) -> bool {
         b = (int)(j + G * m) - P - (int)na;
-        return m < K && b >= 0 && b < (int)nb && L - 16u * (u32)b >= 16;
+        return m < m_hi && b >= 0 && b < (int)nb && L - 16u * (u32)b >= 16;
     };
     u32x4 nxt[NB];
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
         int b;
         nxt[i] = u32x4{0, 0, 0, 0};
-        if (full_block(i, b))
+        if (full_block(m_lo + i, b))
             nxt[i] = *(const u32x4_u *)(src + 16u * (u32)b);
     }
 
-    for (u32 m0 = 0; m0 < Kmax; m0 += NB) {
+    for (u32 s0 = 0; s0 < Smax; s0 += NB) {
+        const u32 m0 = m_lo + s0;
         u32x4 cur[NB];
         u32 st[NB][4];
 #pragma unroll
@@ -636,7 +665,7 @@ __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u
             // AES-CTR input: data positions encrypt counter 2+b, all others J0 (kept by the length lane as E(K, J0))
             const int logical = (int)(j + G * (m0 + i)) - P;
             const int b = logical - (int)na;
-            const bool is_data = m0 + i < K && logical >= (int)na && b < (int)nb;
+            const bool is_data = m0 + i < m_hi && logical >= (int)na && b < (int)nb;
             st[i][0] = n0, st[i][1] = n1, st[i][2] = n2;
             st[i][3] = bswap32(is_data ? (u32)(b + 2) : 1u) ^ rk[0][3];
         }
@@ -649,7 +678,7 @@ __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
             const u32 m = m0 + i;
-            const bool act = m < K;
+            const bool act = m < m_hi;
             const int logical = (int)(j + G * m) - P;
             const int b = logical - (int)na;
             const bool is_data = act && logical >= (int)na && b < (int)nb;
@@ -688,14 +717,14 @@ __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u
             // scheduling fence: keeps the 32 table loads of this fold from being hoisted next to the other blocks'
             // work (that hoisting spills them to scratch)
             __builtin_amdgcn_sched_barrier(0);
-            const u32x4 prod = gmul_tab(lds, acc, m + 1 == K ? tsel_last : tsel_horner);
+            const u32x4 prod = gmul_tab(lds, acc, m + 1 == m_hi ? tsel_last : tsel_horner);
             if (act)
                 acc = prod;
             __builtin_amdgcn_sched_barrier(0);
         }
     }
 
-    // XOR over the G lanes of the record
+    // XOR over the G lanes of the group
 #pragma unroll
     for (int off = 1; off < G; off <<= 1) {
         acc[0] ^= (u32)__shfl_xor((int)acc[0], off, 64);
@@ -703,7 +732,9 @@ __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u
         acc[2] ^= (u32)__shfl_xor((int)acc[2], off, 64);
         acc[3] ^= (u32)__shfl_xor((int)acc[3], off, 64);
     }
-    if (valid && j == G - 1) {
+    // whole record (finish): tag = GHASH ^ E(K, J0), written after the ciphertext (seal) or compared with the
+    // received one (open)
+    if (finish && valid && j == G - 1) {
         const u32x4 tag = acc ^ ek0;
         if (OPEN) {
             const u32x4 rt = *(const u32x4_u *)(src + L);
@@ -713,6 +744,22 @@ __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u
             *(u32x4_u *)(dst + L) = tag;
         }
     }
+}
+
+// Seals / opens one whole record per G-lane group.
+template <int NR, bool OPEN, int NB>
+__device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u8 *lds, const u32 (&rk)[NR + 1][4], u32 iv0,
+                                              u32 iv1, u32 iv2, u64 rec, bool valid, u32 j, u32 laneoff, u32 tsel_horner,
+                                              u32 tsel_last)
+{
+    constexpr int G = ENGINE_G;
+    ptls_mi355x_record_t r = {};
+    if (valid)
+        r = args.recs[rec];
+    const u32 K = valid ? (((r.aad_len + 15u) >> 4) + ((r.len + 15u) >> 4) + 1 + G - 1) / G : 0;
+    u32x4 acc, ek0;
+    gcm_segment<NR, OPEN, NB>(args, lds, rk, iv0, iv1, iv2, r, valid, 0, K, j, laneoff, tsel_horner, tsel_last, acc, ek0,
+                              true, rec);
 }
 
 // Persistent kernel: workgroup w owns the contiguous record range [n*w/grid, n*(w+1)/grid) and walks it in key runs
@@ -738,8 +785,8 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     const u32 laneoff = (lane & 31) * 4;
     const u32 wave = threadIdx.x >> 6;
     const u32 waves_per_wg = blockDim.x >> 6;
-    const u32 tsel_horner = 0x10000u | (u32)(G - 1) * GHASH_TABLE_BYTES;
-    const u32 tsel_last = 0x10000u | (u32)(G - 1 - j) * GHASH_TABLE_BYTES;
+    const u32 tsel_horner = 0x10000u + (u32)(G - 1) * GHASH_TABLE_BYTES;
+    const u32 tsel_last = 0x10000u + (u32)(G - 1 - j) * GHASH_TABLE_BYTES;
 
     const u64 n = args.nrecs;
     const u64 beg = n * blockIdx.x / gridDim.x, end = n * (blockIdx.x + 1) / gridDim.x;
@@ -793,6 +840,180 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     }
 }
 
+// Chunked schedule for many-key / mixed-length batches. The lockstep kernel above gives each G-lane group a whole
+// record, so a wave runs as long as its longest record and a key run (~64 records of a connection) as long as its
+// longest record too; with U[64 B, 16 KiB] lengths and a workgroup barrier per key that halves throughput twice.
+// Here a run's records are cut into units of at most CHUNK_BLOCKS GHASH-stream blocks, counted from the END of the
+// stream (so every unit but a record's first is exactly CHUNK_BLOCKS long), and waves pull units from a per-run LDS
+// counter. A unit's group computes the partial P_k = sum over its blocks of X_i * H^(end_k - i) (k = units after it);
+// GHASH = sum_k P_k * H^(k * CHUNK_BLOCKS), which the combine pass evaluates by Horner with the H^CHUNK_BLOCKS table.
+// Single-unit records finish inside the unit as in the lockstep kernel.
+template <int NR, bool OPEN>
+__global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGINE_WAVES_PER_SIMD, ENGINE_WAVES_PER_SIMD))) void gcm_chunked_kernel(BatchArgs args)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    lds_u8 *lds = (lds_u8 *)smem;
+    check_lds_base(smem);
+    lds_u32 *s_ctl = (lds_u32 *)(lds + CLDS_CTL);  // [0] run length, [1] next unit, [2] truncated length, [4..7] scan
+    lds_u32 *s_ubase = (lds_u32 *)(lds + CLDS_UBASE);
+    lds_u32x4 *s_ek0 = (lds_u32x4 *)(lds + CLDS_EK0);
+    lds_u32x4 *s_part = (lds_u32x4 *)(lds + CLDS_PART);
+    constexpr int G = ENGINE_G;
+    constexpr int RPW = 64 / G;
+
+    build_aes_tables(lds);
+
+    const u32 lane = threadIdx.x & 63;
+    const u32 j = lane % G;
+    const u32 slot = lane / G;
+    const u32 laneoff = (lane & 31) * 4;
+    const u32 wave = threadIdx.x >> 6;
+    const u32 tsel_horner = 0x10000u + (u32)(G - 1) * GHASH_TABLE_BYTES;
+    const u32 tsel_last = 0x10000u + (u32)(G - 1 - j) * GHASH_TABLE_BYTES;
+    const u32 tsel_chunk = 0x10000u + 8u * GHASH_TABLE_BYTES;
+
+    const u64 n = args.nrecs;
+    const u64 beg = n * blockIdx.x / gridDim.x, end = n * (blockIdx.x + 1) / gridDim.x;
+    u32 loaded_key = 0xffffffffu;
+
+    for (u64 pos = beg; pos < end;) {
+        // ---- the run: records [pos, pos + run_n) with one key, at most CRUN_RECS records and CRUN_UNITS units
+        const u32 key_idx = args.multi_key ? args.recs[pos].key_idx : 0u;
+        const u32 lim = (u32)min(end - pos, (u64)CRUN_RECS);
+        if (threadIdx.x == 0) {
+            s_ctl[0] = lim;
+            s_ctl[1] = 0;
+        }
+        __syncthreads();
+        if (args.multi_key)
+            for (u32 t = threadIdx.x; t < lim; t += blockDim.x)
+                if (args.recs[pos + t].key_idx != key_idx)
+                    atomicMin((u32 *)&s_ctl[0], t);
+        __syncthreads();
+        u32 run_n = s_ctl[0];
+        // units per record, exclusive prefix sum into s_ubase (threads 0..CRUN_RECS-1, one record each)
+        u32 nc = 0;
+        if (threadIdx.x < run_n) {
+            const ptls_mi355x_record_t r = args.recs[pos + threadIdx.x];
+            const u32 steps = (((r.aad_len + 15u) >> 4) + ((r.len + 15u) >> 4) + 1 + G - 1) / G;
+            nc = (steps + CHUNK_STEPS - 1) / CHUNK_STEPS;
+            if (nc > CHUNK_MAX_UNITS)
+                nc = 1;  // very long record: one group runs it whole
+        }
+        u32 incl = nc;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const u32 y = (u32)__shfl_up((int)incl, off, 64);
+            if (lane >= (u32)off)
+                incl += y;
+        }
+        if (threadIdx.x < CRUN_RECS && lane == 63)
+            s_ctl[4 + wave] = incl;
+        if (threadIdx.x == 0)
+            s_ctl[2] = run_n;
+        __syncthreads();
+        if (threadIdx.x < CRUN_RECS) {
+            for (u32 w = 0; w < wave; ++w)
+                incl += s_ctl[4 + w];
+            s_ubase[threadIdx.x + 1] = incl;
+            const u32 excl = incl - nc;
+            // the first record whose units overflow the run's partial slots ends the run (never the first record)
+            if (threadIdx.x < run_n && incl > CRUN_UNITS && excl <= CRUN_UNITS)
+                s_ctl[2] = max(threadIdx.x, 1u);
+        }
+        if (threadIdx.x == 0)
+            s_ubase[0] = 0;
+        __syncthreads();
+        run_n = s_ctl[2];
+        const u32 total_units = s_ubase[run_n];
+        const u64 run_end = pos + run_n;
+
+        if (key_idx >= args.nkeys) {  // invalid key: nothing is written except a failed ok byte
+            if (OPEN)
+                for (u64 t = pos + threadIdx.x; t < run_end; t += blockDim.x)
+                    args.ok[t] = 0;
+            __syncthreads();
+            pos = run_end;
+            continue;
+        }
+        if (key_idx != loaded_key) {
+            build_ghash_tables(lds, args.keys + key_idx, 9);  // H^1..H^8 and H^CHUNK_BLOCKS
+            __syncthreads();
+            loaded_key = key_idx;
+        }
+        const KeyEntry *key = args.keys + key_idx;
+        u32 rk[NR + 1][4];
+#pragma unroll
+        for (int r = 0; r <= NR; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                rk[r][c] = __builtin_amdgcn_readfirstlane(key->rk[r][c]);
+        const u32 iv0 = __builtin_amdgcn_readfirstlane(key->iv[0]), iv1 = __builtin_amdgcn_readfirstlane(key->iv[1]),
+                  iv2 = __builtin_amdgcn_readfirstlane(key->iv[2]);
+
+        // ---- units: each wave takes RPW consecutive units (one per group) at a time
+        for (;;) {
+            u32 ub = 0;
+            if (lane == 0)
+                ub = atomicAdd((u32 *)&s_ctl[1], (u32)RPW);
+            ub = __builtin_amdgcn_readfirstlane(ub);
+            if (ub >= total_units)
+                break;
+            const u32 u = ub + slot;
+            const bool valid = u < total_units;
+            u32 lo = 0, hi = run_n;  // record ri: s_ubase[ri] <= u < s_ubase[ri + 1]
+            while (hi - lo > 1) {
+                const u32 mid = (lo + hi) >> 1;
+                if (s_ubase[mid] <= u)
+                    lo = mid;
+                else
+                    hi = mid;
+            }
+            const u32 ri = lo;
+            const u32 first = s_ubase[ri], unc = s_ubase[ri + 1] - first;
+            const u32 k_back = unc - 1 - (u - first);
+            ptls_mi355x_record_t r = {};
+            if (valid)
+                r = args.recs[pos + ri];
+            const u32 steps = (((r.aad_len + 15u) >> 4) + ((r.len + 15u) >> 4) + 1 + G - 1) / G;
+            u32 m_hi = steps - k_back * CHUNK_STEPS;
+            u32 m_lo = k_back + 1 == unc ? 0u : m_hi - CHUNK_STEPS;
+            if (!valid)
+                m_lo = m_hi = 0;
+            u32x4 acc, ek0;
+            gcm_segment<NR, OPEN, 1>(args, lds, rk, iv0, iv1, iv2, r, valid, m_lo, m_hi, j, laneoff, tsel_horner,
+                                     tsel_last, acc, ek0, unc == 1, pos + ri);
+            if (valid && unc > 1 && j == G - 1) {
+                s_part[u] = acc;
+                if (k_back == 0)
+                    s_ek0[ri] = ek0;
+            }
+        }
+        __syncthreads();
+
+        // ---- combine the partials of multi-unit records (one thread per record)
+        for (u32 t = threadIdx.x; t < run_n; t += blockDim.x) {
+            const u32 first = s_ubase[t], unc = s_ubase[t + 1] - first;
+            if (unc < 2)
+                continue;
+            u32x4 acc = s_part[first];
+            for (u32 i = 1; i < unc; ++i)
+                acc = gmul_tab(lds, acc, tsel_chunk) ^ s_part[first + i];
+            const u32x4 tag = acc ^ s_ek0[t];
+            const ptls_mi355x_record_t r = args.recs[pos + t];
+            if (OPEN) {
+                const u32x4 rt = *(const u32x4_u *)(args.in + r.in_off + r.len);
+                const u32x4 d = rt ^ tag;
+                args.ok[pos + t] = (d[0] | d[1] | d[2] | d[3]) == 0;
+            } else {
+                *(u32x4_u *)(args.out + r.out_off + r.len) = tag;
+            }
+        }
+        __syncthreads();
+        pos = run_end;
+    }
+}
+
 // AES-ECB of independent blocks (one block per thread, keys from the keyset)
 template <int NR>
 __global__ __launch_bounds__(256) void ecb_kernel(const KeyEntry *keys, const u32 *key_idx, const uint8_t *in, uint8_t *out,
@@ -841,6 +1062,7 @@ struct st_ptls_mi355x_keyset_t {
     int nr;
     KeyEntry *d_keys;
     int ncu;
+    int schedule;
 };
 
 static int engine_init_attrs(void)
@@ -852,6 +1074,10 @@ static int engine_init_attrs(void)
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<10, true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<14, false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<14, true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_chunked_kernel<10, false>, hipFuncAttributeMaxDynamicSharedMemorySize, CLDS_ALLOC));
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_chunked_kernel<10, true>, hipFuncAttributeMaxDynamicSharedMemorySize, CLDS_ALLOC));
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_chunked_kernel<14, false>, hipFuncAttributeMaxDynamicSharedMemorySize, CLDS_ALLOC));
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_chunked_kernel<14, true>, hipFuncAttributeMaxDynamicSharedMemorySize, CLDS_ALLOC));
     HIP_TRY(hipFuncSetAttribute((const void *)ecb_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
     HIP_TRY(hipFuncSetAttribute((const void *)ecb_kernel<14>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
     done = 1;
@@ -922,6 +1148,14 @@ void ptls_mi355x_keyset_free(ptls_mi355x_keyset_t *ks)
     free(ks);
 }
 
+int ptls_mi355x_keyset_set_schedule(ptls_mi355x_keyset_t *ks, int schedule)
+{
+    if (ks == NULL || schedule < PTLS_MI355X_SCHEDULE_AUTO || schedule > PTLS_MI355X_SCHEDULE_CHUNKED)
+        return fail("%s", "set_schedule: invalid arguments");
+    ks->schedule = schedule;
+    return 0;
+}
+
 size_t ptls_mi355x_keyset_size(const ptls_mi355x_keyset_t *ks) { return ks->nkeys; }
 size_t ptls_mi355x_keyset_key_size(const ptls_mi355x_keyset_t *ks) { return ks->key_size; }
 
@@ -945,6 +1179,15 @@ int ptls_mi355x_keyset_set_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, const vo
     return 0;
 }
 
+// Schedule choice (ptls_mi355x_keyset_set_schedule): AUTO = chunked for many-key keysets (short key runs, lengths
+// varying per connection), lockstep for one key.
+static bool use_chunked(const ptls_mi355x_keyset_t *ks)
+{
+    if (ks->schedule != PTLS_MI355X_SCHEDULE_AUTO)
+        return ks->schedule == PTLS_MI355X_SCHEDULE_CHUNKED;
+    return ks->nkeys > 1;
+}
+
 static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
                         const void *aad, void *out, uint8_t *ok, void *stream)
 {
@@ -964,7 +1207,19 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
     if (grid < 1)
         grid = 1;
     hipStream_t s = (hipStream_t)stream;
-    if (ks->nr == 10) {
+    if (use_chunked(ks)) {
+        if (ks->nr == 10) {
+            if (open)
+                gcm_chunked_kernel<10, true><<<(unsigned)grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
+            else
+                gcm_chunked_kernel<10, false><<<(unsigned)grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
+        } else {
+            if (open)
+                gcm_chunked_kernel<14, true><<<(unsigned)grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
+            else
+                gcm_chunked_kernel<14, false><<<(unsigned)grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
+        }
+    } else if (ks->nr == 10) {
         if (open)
             gcm_batch_kernel<10, true><<<(unsigned)grid, ENGINE_WG, LDS_ALLOC, s>>>(a);
         else

@@ -169,11 +169,16 @@ def _random_batch(rng, n, max_len, max_aad, key_size, nkeys=1, sort_keys=True):
     return b, keys, ivs, pt, aad
 
 
+SCHEDULES = ["lockstep", "chunked"]
+
+
+@pytest.mark.parametrize("schedule", SCHEDULES)
 @pytest.mark.parametrize("key_size,nkeys,sort_keys", [(16, 1, True), (32, 1, True), (16, 7, True), (32, 50, False)])
-def test_random_batch_vs_fusion(ref, key_size, nkeys, sort_keys):
+def test_random_batch_vs_fusion(ref, key_size, nkeys, sort_keys, schedule):
     rng = np.random.default_rng(key_size * 1000 + nkeys)
     b, keys, ivs, pt, aad = _random_batch(rng, 3000, 3000, 64, key_size, nkeys, sort_keys)
     ks = pa.Keyset(keys, ivs, key_size)
+    ks.set_schedule(schedule)
     sealed = gpu_seal(ks, b.seal, pt, aad, b.sealed_bytes)
     expect = np.zeros(b.sealed_bytes, np.uint8)
     ref.run_batch(True, keys, ivs, key_size, b.seal, pt, aad, expect, nthreads=8)
@@ -185,7 +190,8 @@ def test_random_batch_vs_fusion(ref, key_size, nkeys, sort_keys):
     assert not back[~m].any()  # nothing outside the records was written
 
 
-def test_every_length_0_to_300_vs_oracle(oracle):
+@pytest.mark.parametrize("schedule", SCHEDULES)
+def test_every_length_0_to_300_vs_oracle(oracle, schedule):
     # all stream layouts around the G-lane boundaries (partial blocks, AAD-only, empty records)
     rng = np.random.default_rng(7)
     lens = np.arange(0, 301)
@@ -194,16 +200,19 @@ def test_every_length_0_to_300_vs_oracle(oracle):
     pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
     aad = np.frombuffer(rng.bytes(b.aad_bytes), np.uint8)
     ks = pa.Keyset(keys, ivs, 16)
+    ks.set_schedule(schedule)
     sealed = gpu_seal(ks, b.seal, pt, aad, b.sealed_bytes)
     expect = np.zeros(b.sealed_bytes, np.uint8)
     oracle.seal_batch(keys, ivs, 16, b.seal, pt, aad, expect)
     assert np.array_equal(sealed, expect)
 
 
-def test_tamper_rejected_per_record(ref):
+@pytest.mark.parametrize("schedule", SCHEDULES)
+def test_tamper_rejected_per_record(ref, schedule):
     rng = np.random.default_rng(11)
     b, keys, ivs, pt, aad = _random_batch(rng, 512, 2000, 40, 16)
     ks = pa.Keyset(keys, ivs, 16)
+    ks.set_schedule(schedule)
     sealed = gpu_seal(ks, b.seal, pt, aad, b.sealed_bytes)
     bad = sealed.copy()
     badaad = aad.copy()
@@ -277,19 +286,56 @@ def test_empty_batch_and_bad_args():
         pa.Keyset(bytes(24), bytes(12), 24)
 
 
-def test_max_tls_record_and_large_records(ref):
-    # PTLS_MAX_PLAINTEXT_RECORD_SIZE (lib/picotls.c:52) + the 256-byte TLS 1.3 expansion allowance, and beyond
+@pytest.mark.parametrize("schedule", SCHEDULES)
+def test_max_tls_record_and_large_records(ref, schedule):
+    # PTLS_MAX_PLAINTEXT_RECORD_SIZE (lib/picotls.c:52) + the 256-byte TLS 1.3 expansion allowance, and beyond; for the
+    # chunked schedule also records of exactly 64 units (the most it splits: 64 * 1 KiB of GHASH stream) and 65
+    # (processed whole)
     rng = np.random.default_rng(17)
-    lens = [16384, 16384 + 256, 65536, 1 << 20, 16383, 16385]
-    b = RecordBatch.build(lens, [5, 5, 13, 13, 0, 32])
+    lens = [16384, 16384 + 256, 65536, 1 << 20, 16383, 16385, 64 * 1024 - 32, 64 * 1024 - 16, 64 * 1024 - 15]
+    b = RecordBatch.build(lens, [5, 5, 13, 13, 0, 32, 0, 0, 0])
     keys, ivs = np.frombuffer(rng.bytes(16), np.uint8), np.frombuffer(rng.bytes(12), np.uint8)
     pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
     aad = np.frombuffer(rng.bytes(b.aad_bytes), np.uint8)
     ks = pa.Keyset(keys, ivs, 16)
+    ks.set_schedule(schedule)
     sealed = gpu_seal(ks, b.seal, pt, aad, b.sealed_bytes)
     expect = np.zeros(b.sealed_bytes, np.uint8)
     ref.run_batch(True, keys, ivs, 16, b.seal, pt, aad, expect, nthreads=4)
     assert np.array_equal(sealed, expect)
+
+
+@pytest.mark.parametrize("nkeys", [1, 3])
+def test_chunked_long_runs_and_key_changes(ref, nkeys):
+    # chunked schedule: key runs longer than its 256-record / 1024-unit run window (runs are cut and resumed), keys
+    # changing mid-window, open of the same batch, and records of every unit count 1..20
+    rng = np.random.default_rng(19 + nkeys)
+    n = 700
+    lens = np.concatenate([np.full(300, 16384), rng.integers(0, 20 * 1024, n - 300)])
+    key_idx = np.sort(rng.integers(0, nkeys, n))
+    b = RecordBatch.build(lens, rng.integers(0, 30, n), seqs=rng.integers(0, 2**40, n, dtype=np.uint64),
+                          key_idx=key_idx)
+    keys = np.frombuffer(rng.bytes(nkeys * 32), np.uint8)
+    ivs = np.frombuffer(rng.bytes(nkeys * 12), np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(max(b.aad_bytes, 1)), np.uint8)
+    ks = pa.Keyset(keys, ivs, 32)
+    ks.set_schedule("chunked")
+    sealed = gpu_seal(ks, b.seal, pt, aad, b.sealed_bytes)
+    expect = np.zeros(b.sealed_bytes, np.uint8)
+    ref.run_batch(True, keys, ivs, 32, b.seal, pt, aad, expect, nthreads=8)
+    assert np.array_equal(sealed, expect)
+    back, ok = gpu_open(ks, b.open, sealed, aad, b.pt_bytes)
+    assert ok.all()
+    m = record_mask(b.seal, b.pt_bytes)
+    assert np.array_equal(back[m], pt[m])
+
+
+def test_schedule_argument_checked():
+    ks = pa.Keyset(bytes(16), bytes(12), 16)
+    with pytest.raises(ValueError):
+        ks.set_schedule("fastest")
+    assert pa.load_library().ptls_mi355x_keyset_set_schedule(ks.handle, 7) == -1
 
 
 def test_picotls_vtable_pairs():

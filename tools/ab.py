@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--records", type=int, default=262144)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--schedule", type=int, default=0, help="ptls_mi355x_keyset_set_schedule value (0 auto)")
     a = ap.parse_args()
     wl = WORKLOADS[a.workload].scaled(a.records)
     b = wl.descriptors(0, wl.nrecs)
@@ -50,6 +51,8 @@ def main():
     for p, lib in libs:
         kss[p] = ctypes.c_void_p(lib.ptls_mi355x_keyset_new(keys.ctypes.data, ivs.ctypes.data, wl.nkeys, wl.key_size))
         assert kss[p].value, p
+        if a.schedule and hasattr(lib, "ptls_mi355x_keyset_set_schedule"):
+            assert lib.ptls_mi355x_keyset_set_schedule(kss[p], a.schedule) == 0
     sealed = torch.empty(b.sealed_bytes, dtype=torch.uint8, device=dev)
     back = torch.empty(b.pt_bytes, dtype=torch.uint8, device=dev)
     ok = torch.empty(b.n, dtype=torch.uint8, device=dev)

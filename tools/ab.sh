@@ -1,4 +1,6 @@
 set +e
 cd $GRAFT_REPO_ROOT
-timeout -k 10 400 python tools/ab.py tools/variants/*.so --workload ${1:-tls16k} --records ${2:-262144} > gpurun_out/ab.log 2>&1
-rc=$?; cat gpurun_out/ab.log | grep -v amdgpu.ids; exit $rc
+# usage: tools/ab.sh <workload> <records> [extra ab.py args]
+w=${1:-tls16k}; n=${2:-262144}; shift 2
+timeout -k 10 400 python tools/ab.py tools/variants/*.so --workload $w --records $n "$@" > gpurun_out/ab_$w.log 2>&1
+rc=$?; cat gpurun_out/ab_$w.log | grep -v amdgpu.ids; exit $rc
