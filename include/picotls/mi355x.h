@@ -91,10 +91,11 @@ int ptls_mi355x_keyset_set_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, const vo
 /**
  * Batch schedule used by seal_batch / open_batch on this keyset (no reference counterpart: fusion processes one record
  * per call). Results are identical under every schedule; only the work distribution differs.
- *   AUTO      chunked for keysets of more than one key, lockstep otherwise (the default)
- *   LOCKSTEP  one record per 8-lane group, whole records; best for uniform lengths under one key
- *   CHUNKED   records cut into 1 KiB GHASH units pulled by waves from a queue and recombined with H^64; balances
- *             mixed lengths and short per-connection key runs
+ *   AUTO      = CHUNKED (the default)
+ *   LOCKSTEP  one whole record per 8-lane group, records assigned statically; kept for comparison
+ *   CHUNKED   waves pull work units from a per-run queue. Runs of uniform record lengths use whole records as units;
+ *             other runs cut records into 1 KiB GHASH units recombined with H^64, which balances mixed lengths and
+ *             short per-connection key runs
  * Returns 0, or -1 for an unknown schedule.
  */
 #define PTLS_MI355X_SCHEDULE_AUTO 0

@@ -143,4 +143,9 @@ WORKLOADS = {
                       desc="4M mixed-length records 64 B-16 KiB, AES-256-GCM, 64K traffic keys"),
     "shard1200": Workload("shard1200", 32 << 20, 1200, 13, 16,
                           desc="32M x 1200 B records sharded evenly across GPUs, AES-128-GCM"),
+    # analysis variants (not BASELINE configs): isolate key switching and length mix from the AES-256 cost
+    "mixed1key": Workload("mixed1key", 4 << 20, None, 13, 32,
+                          desc="4M mixed-length records 64 B-16 KiB, AES-256-GCM, one key"),
+    "tls16k256": Workload("tls16k256", 1 << 20, 16384, 5, 32, tls_header_aad=True,
+                          desc="1M x 16384 B TLS records, AES-256-GCM, one key"),
 }

@@ -331,6 +331,30 @@ def test_chunked_long_runs_and_key_changes(ref, nkeys):
     assert np.array_equal(back[m], pt[m])
 
 
+@pytest.mark.parametrize("length,n,nkeys", [(1200, 9000, 1), (16384, 700, 1), (1200, 3000, 5), (1201, 4500, 1)])
+def test_chunked_uniform_runs_vs_fusion(ref, length, n, nkeys):
+    # uniform runs take the whole-record path of the chunked schedule (one-key runs up to 4096 records)
+    rng = np.random.default_rng(length + n + nkeys)
+    lens = np.full(n, length)
+    if length == 1201:
+        lens[::97] = 1200  # within the uniformity slack
+    b = RecordBatch.build(lens, 13, seqs=np.arange(n, dtype=np.uint64) * 3, key_idx=np.sort(rng.integers(0, nkeys, n)))
+    keys = np.frombuffer(rng.bytes(nkeys * 16), np.uint8)
+    ivs = np.frombuffer(rng.bytes(nkeys * 12), np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(b.aad_bytes), np.uint8)
+    ks = pa.Keyset(keys, ivs, 16)
+    ks.set_schedule("chunked")
+    sealed = gpu_seal(ks, b.seal, pt, aad, b.sealed_bytes)
+    expect = np.zeros(b.sealed_bytes, np.uint8)
+    ref.run_batch(True, keys, ivs, 16, b.seal, pt, aad, expect, nthreads=8)
+    assert np.array_equal(sealed, expect)
+    back, ok = gpu_open(ks, b.open, sealed, aad, b.pt_bytes)
+    assert ok.all()
+    m = record_mask(b.seal, b.pt_bytes)
+    assert np.array_equal(back[m], pt[m])
+
+
 def test_schedule_argument_checked():
     ks = pa.Keyset(bytes(16), bytes(12), 16)
     with pytest.raises(ValueError):
