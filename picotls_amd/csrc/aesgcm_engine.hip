@@ -112,12 +112,13 @@ static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 #define CRUN_UNITS 1024      // units per run
 #define WHOLE_RUN_RECS 4096  // records per run when a one-key run is uniform (every record one unit)
 #define UNIFORM_SLACK 2      // a run is uniform when its records' step counts differ by at most this
-#define CLDS_CTL (LDS_BYTES + GHASH_TABLE_BYTES)                // 16 control words
-#define CLDS_UBASE (CLDS_CTL + 128)                             // u32[CRUN_RECS + 1]: first unit of each record
+#define CLDS_CTL (LDS_BYTES + GHASH_TABLE_BYTES)                // 128 control words
+#define CLDS_UBASE (CLDS_CTL + 512)                             // u32[CRUN_RECS + 1]: first unit of each record
 #define CLDS_DONE (CLDS_UBASE + 4 * (CRUN_RECS + 16))           // u32[CRUN_RECS]: finished units per record
 #define CLDS_EK0 (CLDS_DONE + 4 * CRUN_RECS)                    // 16 B per record: E(K, J0)
 #define CLDS_PART (CLDS_EK0 + 16 * CRUN_RECS)                   // 16 B per unit: GHASH partial
-#define CLDS_ALLOC (CLDS_PART + 16 * CRUN_UNITS)
+#define CLDS_FRONT (CLDS_PART + 16 * CRUN_UNITS)                // u32[CRUN_RECS]: records by front-unit size
+#define CLDS_ALLOC (CLDS_FRONT + 4 * CRUN_RECS)
 static_assert(CLDS_ALLOC <= 160 * 1024, "chunked schedule LDS budget");
 static_assert(CHUNK_BLOCKS % ENGINE_G == 0, "units are whole steps");
 
@@ -927,7 +928,8 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     lds_u8 *lds = (lds_u8 *)smem;
     check_lds_base(smem);
     // s_ctl: [1] next unit, [4..7] per-wave unit totals, [8..11] per-wave key boundary, [12..15] per-wave unit cut,
-    // [16..19] / [20..23] per-wave min / max steps
+    // [16..19] / [20..23] per-wave min / max steps, [32 + 16 w + b] per-wave count of front-unit bucket b
+    lds_u32 *s_front = (lds_u32 *)(lds + CLDS_FRONT);
     lds_u32 *s_ctl = (lds_u32 *)(lds + CLDS_CTL);
     lds_u32 *s_ubase = (lds_u32 *)(lds + CLDS_UBASE);
     lds_u32 *s_done = (lds_u32 *)(lds + CLDS_DONE);
@@ -958,7 +960,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         // Threads 0..CRUN_RECS-1 read one descriptor each: the key boundary and the unit counts come from one pass.
         const u32 key_idx = args.multi_key ? args.recs[pos].key_idx : 0u;
         const u32 lim = (u32)min(end - pos, (u64)CRUN_RECS);
-        u32 nc = 0, incl = 0;
+        u32 nc = 0, incl = 0, bkt = 0;
         if (wave < SCAN_WAVES) {
             const u32 t = threadIdx.x;
             bool other_key = false;
@@ -967,8 +969,11 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 const ptls_mi355x_record_t r = args.recs[pos + t];
                 const u32 steps = (((r.aad_len + 15u) >> 4) + ((r.len + 15u) >> 4) + 1 + G - 1) / G;
                 nc = (steps + CHUNK_STEPS - 1) / CHUNK_STEPS;
+                // front-unit size bucket: 0 = very long record run whole (nc forced to 1), else CHUNK_STEPS + 1 -
+                // size of the record's first unit (1 = a full unit, CHUNK_STEPS = one step)
+                bkt = CHUNK_STEPS + 1 - (steps - (nc - 1) * CHUNK_STEPS);
                 if (nc > CHUNK_MAX_UNITS)
-                    nc = 1;  // very long record: one group runs it whole
+                    nc = 1, bkt = 0;
                 other_key = args.multi_key && r.key_idx != key_idx;
                 if (!other_key)
                     smin = smax = steps;
@@ -1019,13 +1024,45 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             if (lane == 0)
                 s_ctl[12 + wave] = cut ? 64 * wave + (u32)__builtin_ctzll(cut) : 0xffffffffu;
         }
+        u32 nhuge = 0;
         if (!whole) {
             __syncthreads();
 #pragma unroll
             for (u32 w = 0; w < SCAN_WAVES; ++w)
                 run_n = min(run_n, max(s_ctl[12 + w], 1u));
+            // Unit order: [front units of very long records][all full units, record-major][the other front units by
+            // size, largest first]. Lockstep waves then draw units of equal or similar length, and the run ends on
+            // its shortest units. Counting sort of the front units by bucket: per-wave counts, then positions.
+            u32 rank = 0;
+            if (wave < SCAN_WAVES) {
+                const bool in = threadIdx.x < run_n;
+#pragma unroll
+                for (u32 b = 0; b <= CHUNK_STEPS; ++b) {
+                    const u64 m = __ballot(in && bkt == b);
+                    if (lane == 0)
+                        s_ctl[32 + 16 * wave + b] = (u32)__popcll(m);
+                    if (in && bkt == b)
+                        rank = (u32)__popcll(m & ((1ull << lane) - 1));
+                }
+            }
+            __syncthreads();
+            if (wave < SCAN_WAVES && threadIdx.x < run_n) {
+                u32 base = rank;
+                for (u32 b = 0; b < bkt; ++b)
+#pragma unroll
+                    for (u32 w = 0; w < SCAN_WAVES; ++w)
+                        base += s_ctl[32 + 16 * w + b];
+                for (u32 w = 0; w < wave; ++w)
+                    base += s_ctl[32 + 16 * w + bkt];
+                s_front[base] = threadIdx.x;
+            }
+#pragma unroll
+            for (u32 w = 0; w < SCAN_WAVES; ++w)
+                nhuge += s_ctl[32 + 16 * w];
+            __syncthreads();
         }
         const u32 total_units = whole ? run_n : s_ubase[run_n];
+        const u32 nfull = total_units - run_n;
         const u64 run_end = pos + run_n;
         PROF_STAMP(t1);
 
@@ -1065,22 +1102,30 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 break;
             const u32 u = ub + slot;
             const bool valid = u < total_units;
-            u32 lo = u, first = u, unc = 1;
-            if (!whole) {
-                u32 hi = run_n;  // record ri: s_ubase[ri] <= u < s_ubase[ri + 1]
-                lo = 0;
-                while (hi - lo > 1) {
-                    const u32 mid = (lo + hi) >> 1;
-                    if (s_ubase[mid] <= u)
-                        lo = mid;
-                    else
-                        hi = mid;
+            u32 lo = u, first = u, unc = 1, k_back = 0;
+            if (!whole && valid) {
+                if (u < nhuge || u >= nhuge + nfull) {  // a front unit
+                    lo = s_front[u < nhuge ? u : u - nfull];
+                    first = s_ubase[lo];
+                    unc = s_ubase[lo + 1] - first;
+                    k_back = unc - 1;
+                } else {  // full unit f: record lo with s_ubase[lo] - lo <= f < s_ubase[lo + 1] - (lo + 1)
+                    const u32 f = u - nhuge;
+                    u32 hi = run_n;
+                    lo = 0;
+                    while (hi - lo > 1) {
+                        const u32 mid = (lo + hi) >> 1;
+                        if (s_ubase[mid] - mid <= f)
+                            lo = mid;
+                        else
+                            hi = mid;
+                    }
+                    first = s_ubase[lo];
+                    unc = s_ubase[lo + 1] - first;
+                    k_back = f - (first - lo);
                 }
-                first = s_ubase[lo];
-                unc = s_ubase[lo + 1] - first;
             }
             const u32 ri = lo;
-            const u32 k_back = unc - 1 - (u - first);
             ptls_mi355x_record_t r = {};
             if (valid)
                 r = args.recs[pos + ri];
@@ -1095,7 +1140,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             if (valid && unc > 1) {  // uniform over the group
                 u32 last = 0;
                 if (j == G - 1) {
-                    s_part[u] = acc;
+                    s_part[first + unc - 1 - k_back] = acc;  // stream order: the front unit first
                     if (k_back == 0)
                         s_ek0[ri] = ek0;
                     __threadfence_block();  // partial and E(K, J0) land before the count that publishes them
