@@ -334,13 +334,19 @@ def run_e2e(R, wl, nchunks: int = 16, reps: int = 3):
     return out
 
 
-def traffic_from_profiles(workload: str):
-    """Corrected HBM bytes per seal launch from the committed rocprofv3 PMC summary (profiles/*pmc*.json)."""
+def traffic_from_profiles(workload: str, records: int):
+    """Corrected HBM bytes per seal launch from the committed rocprofv3 PMC summary (profiles/pmc_<workload>.json),
+    scaled to this run's record count when the profile was taken on a different one."""
     path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     if not os.path.exists(path):
         return None
     try:
-        return json.load(open(path)).get("seal_hbm_bytes_per_launch")
+        d = json.load(open(path))
+        v = d.get("seal_hbm_bytes_per_launch")
+        if v is None:
+            return None
+        n = d.get("records")
+        return round(v * records / n) if n else round(v)
     except Exception:
         return None
 
@@ -380,9 +386,10 @@ def main():
                    "parallelism": f"{R.world} independent per-GPU record shards, no data-path collective"},
         "seal_GiBps": round(res["payload_bytes"] / seal_s / 2**30, 3),
         "open_GiBps": round(res["payload_bytes"] / open_s / 2**30, 3),
-        "roofline": {"bound": "hbm", "kernel": "gcm_batch_kernel<10,seal>" if wl.key_size == 16 else "gcm_batch_kernel<14,seal>",
+        "roofline": {"bound": "hbm", "kernel": f"{'gcm_batch_kernel' if args.schedule == 'lockstep' else 'gcm_chunked_kernel'}"
+                                               f"<{10 if wl.key_size == 16 else 14},seal>",
                      "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic_from_profiles(wl.name),
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic_from_profiles(wl.name, res["records"]),
                      "alg_bytes_per_launch": res["seal_alg_bytes"], "avg_launch_ms": round(res["seal_ms"], 4),
                      "open_achieved": round(res["open_alg_bytes"] / open_s / 1e9, 2)},
         "verified": {"roundtrip": res.get("verified_roundtrip"), "fusion_spot_check": res.get("fusion_spot_check")},

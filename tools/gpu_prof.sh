@@ -1,4 +1,5 @@
-# rocprofv3 passes for one workload: kernel trace + stats, then separate PMC passes (HBM bytes, SQ counters).
+# rocprofv3 passes for one workload: kernel trace + stats, then separate PMC passes (HBM bytes, SQ counters), then the
+# summary (gpurun_out/prof_<tag>_<workload>/summary.{json,md}; copy to profiles/<tag>_<workload>.* and pmc_<workload>.json).
 # usage: bash tools/gpu_prof.sh <workload> <records> <tag>
 set +e
 W=${1:-tls16k}; N=${2:-262144}; TAG=${3:-r1}
@@ -16,5 +17,5 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ
 rc=$?; echo "pmc sq rc=$rc"; [ $rc -gt 1 ] && exit $rc
 timeout -k 10 300 rocprofv3 --pmc SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL --output-format csv -d $OUT -o pmc_sq2 -- python3 $ARGS > $OUT/pmc_sq2.log 2>&1
 rc=$?; echo "pmc sq2 rc=$rc"
-ls $OUT
+python3 $R/tools/prof_summary.py $OUT $OUT/summary $N
 exit 0

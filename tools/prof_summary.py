@@ -11,11 +11,14 @@ import os
 import sys
 
 
+KERNELS = ("gcm_batch_kernel", "gcm_chunked_kernel")
+
+
 def load(path):
     return list(csv.DictReader(open(path))) if os.path.exists(path) else []
 
 
-def main(src, dst_prefix, alg_seal=None, alg_open=None):
+def main(src, dst_prefix, records=None):
     stats = {}
     for r in load(os.path.join(src, "trace_kernel_stats.csv")):
         stats[r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
@@ -23,11 +26,11 @@ def main(src, dst_prefix, alg_seal=None, alg_open=None):
     counters = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2"):
         for r in load(os.path.join(src, f + "_counter_collection.csv")):
-            if "gcm_batch_kernel" in r["Kernel_Name"]:
+            if any(k in r["Kernel_Name"] for k in KERNELS):
                 counters[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    out = {"source": src, "kernels": {}}
+    out = {"source": src, "records": records, "kernels": {}}
     for name, st in stats.items():
-        if "gcm_batch_kernel" not in name and "keyset" not in name:
+        if not any(k in name for k in KERNELS) and "keyset" not in name:
             continue
         k = {"trace": st}
         c = {n: sum(v) / len(v) for n, v in counters.get(name, {}).items()}
@@ -61,4 +64,4 @@ def main(src, dst_prefix, alg_seal=None, alg_open=None):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else None)
