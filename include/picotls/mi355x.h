@@ -124,6 +124,60 @@ int ptls_mi355x_ecb_batch(ptls_mi355x_keyset_t *ks, const uint32_t *key_idx, con
                           void *stream);
 
 /**
+ * TLS 1.3 record protection, batched (the record layer of lib/picotls.c: aead_encrypt :728-738 and
+ * buffer_push_encrypted_records :770-817 on the send side, the decrypt + padding strip of :5952-5974 on the receive
+ * side). The records' aad_off / aad_len are ignored: the AAD is the 5-byte record header.
+ *
+ * seal_tls_records: record i seals recs[i].len payload bytes at in + in_off followed by the inner content type
+ * (recs[i].flags & 0xff; PTLS_CONTENT_TYPE_APPDATA = 23 for application data) and writes the wire record at
+ * out + out_off: header {23, 3, 3, BE16(len + 17)} || ciphertext (len + 1 bytes) || tag, len + 22 bytes in total.
+ * len must not exceed PTLS_MAX_PLAINTEXT_RECORD_SIZE (16384), as in buffer_push_encrypted_records.
+ *
+ * open_tls_records: record i is the wire record at in + in_off, whose recs[i].len = header length field - 16 (the
+ * ciphertext including the inner type and padding). The plaintext (len bytes) goes to out + out_off. ok[i] = 1 only
+ * if the tag verifies, the header is {23, 3, 3, BE16(len + 16)} and an inner content type is found; results (may be
+ * NULL) gives the content length after stripping the type and the zero padding, the inner type and a status.
+ */
+#define PTLS_MI355X_TLS_OK 0
+#define PTLS_MI355X_TLS_BAD_MAC 1            /* PTLS_ALERT_BAD_RECORD_MAC */
+#define PTLS_MI355X_TLS_BAD_HEADER 2         /* outer type not application_data, wrong version or length */
+#define PTLS_MI355X_TLS_UNEXPECTED_MESSAGE 3 /* PTLS_ALERT_UNEXPECTED_MESSAGE: no content type, or empty alert/handshake */
+typedef struct st_ptls_mi355x_tls_result_t {
+    uint32_t plain_len;   /* content bytes at out + out_off */
+    uint8_t content_type; /* inner content type */
+    uint8_t status;       /* PTLS_MI355X_TLS_* */
+    uint16_t reserved;
+} ptls_mi355x_tls_result_t;
+
+int ptls_mi355x_seal_tls_records(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
+                                 void *out, void *stream);
+int ptls_mi355x_open_tls_records(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
+                                 void *out, uint8_t *ok, ptls_mi355x_tls_result_t *results, void *stream);
+
+/**
+ * QUIC header protection, batched. One entry per packet: the 16-byte sample at base + sample_off and the index of the
+ * header-protection key in hp_ks. mask[i] (16 bytes at masks + 16 i) = AES-ECB(hp key, sample), i.e. the first
+ * keystream block of the AES-CTR cipher initialised with the sample, which is what ptls_aead_encrypt_s writes into
+ * supp->output (include/picotls.h:441-456, lib/picotls.c ptls_aead__do_encrypt_s; fusion fuses it into the seal,
+ * lib/fusion.c:425-430,636-651). Entries with key_idx >= the keyset size get a zero mask. DEVICE pointers.
+ */
+typedef struct st_ptls_mi355x_hp_t {
+    uint64_t sample_off; /* byte offset of the 16-byte sample from base */
+    uint32_t key_idx;    /* header-protection key */
+    uint32_t reserved;   /* 0 */
+} ptls_mi355x_hp_t;
+
+/* masks for samples already in memory (a receiver removes header protection before it can open the packet) */
+int ptls_mi355x_hp_mask_batch(ptls_mi355x_keyset_t *hp_ks, const ptls_mi355x_hp_t *hp, size_t n, const void *base,
+                              void *masks, void *stream);
+
+/* seal_batch, then the masks of samples taken from the sealed output (hp[i] for record i; base = out), on one stream:
+ * the sample may cover the tag, as in fusion's supp handling */
+int ptls_mi355x_seal_batch_hp(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
+                              const void *aad, void *out, ptls_mi355x_keyset_t *hp_ks, const ptls_mi355x_hp_t *hp,
+                              void *masks, void *stream);
+
+/**
  * Synchronous single-record helpers on HOST buffers (a batch of one, with H2D/D2H copies). These back the picotls
  * vtable (do_encrypt / do_decrypt) and mirror ptls_aead_encrypt / ptls_aead_decrypt: encrypt writes len+16 bytes;
  * decrypt takes inlen = len+16 and returns the plaintext length or SIZE_MAX (tag mismatch or inlen < 16).

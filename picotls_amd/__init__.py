@@ -8,7 +8,8 @@ operator interface (``include/picotls.h:519-580, 2082-2164``; ``lib/picotls.c:65
 * :data:`aes128gcm` / :data:`aes256gcm` -- algorithm descriptors (``ptls_mi355x_aes{128,256}gcm``)
 * :func:`aead_new_direct` -> :class:`AeadContext` with ``encrypt`` / ``encrypt_s`` / ``decrypt`` / ``get_iv`` /
   ``set_iv`` / ``xor_iv`` (``decrypt`` returns ``None`` where picotls returns ``SIZE_MAX``)
-* :class:`Keyset`, :func:`seal_batch`, :func:`open_batch`, :func:`ecb_batch` -- the batch extension.
+* :class:`Keyset`, :func:`seal_batch`, :func:`open_batch`, :func:`ecb_batch`, :func:`hp_mask_batch`,
+  :func:`seal_batch_hp` -- the batch extension.
 
 There is no CPU fallback: when the shared object or a gfx950 device is missing every entry point raises.
 """
@@ -20,7 +21,8 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from .records import RECORD_DTYPE, RecordBatch, shard_ranges  # noqa: F401
+from .records import (HP_DTYPE, RECORD_DTYPE, TLS_BAD_HEADER, TLS_BAD_MAC, TLS_OK, TLS_RESULT_DTYPE,  # noqa: F401
+                      TLS_UNEXPECTED_MESSAGE, RecordBatch, shard_ranges)
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "_lib", "libptls_mi355x.so")
@@ -38,7 +40,11 @@ ABI_FUNCTIONS = (
     "ptls_mi355x_keyset_set_schedule",
     "ptls_mi355x_seal_batch",
     "ptls_mi355x_open_batch",
+    "ptls_mi355x_seal_tls_records",
+    "ptls_mi355x_open_tls_records",
     "ptls_mi355x_ecb_batch",
+    "ptls_mi355x_hp_mask_batch",
+    "ptls_mi355x_seal_batch_hp",
     "ptls_mi355x_encrypt",
     "ptls_mi355x_decrypt",
     "ptls_mi355x_encrypt_block",
@@ -77,6 +83,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.ptls_mi355x_seal_batch.argtypes = [vp, vp, sz, vp, vp, vp, vp]
     lib.ptls_mi355x_open_batch.argtypes = [vp, vp, sz, vp, vp, vp, vp, vp]
     lib.ptls_mi355x_ecb_batch.argtypes = [vp, vp, vp, vp, sz, vp]
+    lib.ptls_mi355x_hp_mask_batch.argtypes = [vp, vp, sz, vp, vp, vp]
+    lib.ptls_mi355x_seal_tls_records.argtypes = [vp, vp, sz, vp, vp, vp]
+    lib.ptls_mi355x_open_tls_records.argtypes = [vp, vp, sz, vp, vp, vp, vp, vp]
+    lib.ptls_mi355x_seal_batch_hp.argtypes = [vp, vp, sz, vp, vp, vp, vp, vp, vp, vp]
     lib.ptls_mi355x_encrypt.argtypes = [vp, sz, vp, vp, sz, u64, vp, sz]
     lib.ptls_mi355x_decrypt.argtypes = [vp, sz, vp, vp, sz, u64, vp, sz]
     lib.ptls_mi355x_decrypt.restype = sz
@@ -173,6 +183,34 @@ def open_batch(ks: Keyset, recs_ptr: int, nrecs: int, in_ptr: int, aad_ptr: int,
 def ecb_batch(ks: Keyset, key_idx_ptr: int, in_ptr: int, out_ptr: int, nblocks: int, stream: int = 0) -> None:
     if load_library().ptls_mi355x_ecb_batch(ks.handle, key_idx_ptr or None, in_ptr, out_ptr, nblocks, stream or None) != 0:
         raise _err("ptls_mi355x_ecb_batch")
+
+
+def seal_tls_records(ks: Keyset, recs_ptr: int, nrecs: int, in_ptr: int, out_ptr: int, stream: int = 0) -> None:
+    """TLS 1.3 wire records (header || ciphertext || tag) from payloads + inner content types (flags); device pointers."""
+    if load_library().ptls_mi355x_seal_tls_records(ks.handle, recs_ptr, nrecs, in_ptr, out_ptr, stream or None) != 0:
+        raise _err("ptls_mi355x_seal_tls_records")
+
+
+def open_tls_records(ks: Keyset, recs_ptr: int, nrecs: int, in_ptr: int, out_ptr: int, ok_ptr: int, results_ptr: int = 0,
+                     stream: int = 0) -> None:
+    """Opens TLS 1.3 wire records and strips the inner type and padding (TLS_RESULT_DTYPE results); device pointers."""
+    if load_library().ptls_mi355x_open_tls_records(ks.handle, recs_ptr, nrecs, in_ptr, out_ptr, ok_ptr, results_ptr or None,
+                                                   stream or None) != 0:
+        raise _err("ptls_mi355x_open_tls_records")
+
+
+def hp_mask_batch(hp_ks: Keyset, hp_ptr: int, n: int, base_ptr: int, masks_ptr: int, stream: int = 0) -> None:
+    """QUIC header-protection masks (HP_DTYPE entries); device pointers."""
+    if load_library().ptls_mi355x_hp_mask_batch(hp_ks.handle, hp_ptr, n, base_ptr, masks_ptr, stream or None) != 0:
+        raise _err("ptls_mi355x_hp_mask_batch")
+
+
+def seal_batch_hp(ks: Keyset, recs_ptr: int, nrecs: int, in_ptr: int, aad_ptr: int, out_ptr: int, hp_ks: Keyset,
+                  hp_ptr: int, masks_ptr: int, stream: int = 0) -> None:
+    """seal_batch followed by the header-protection masks of samples in the sealed output (fusion's supp)."""
+    if load_library().ptls_mi355x_seal_batch_hp(ks.handle, recs_ptr, nrecs, in_ptr, aad_ptr or None, out_ptr, hp_ks.handle,
+                                                hp_ptr, masks_ptr, stream or None) != 0:
+        raise _err("ptls_mi355x_seal_batch_hp")
 
 
 # ------------------------------------------------------------------------------------------------ picotls mirror

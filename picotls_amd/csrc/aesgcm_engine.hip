@@ -605,10 +605,11 @@ __device__ __forceinline__ u32x4 gmul_group(const lds_u8 *, u32x4 a, u32 tsel, u
 // loads n (< 16) bytes, zero padded
 __device__ __forceinline__ u32x4 load_partial(const uint8_t *p, u32 n)
 {
-    u32 w[4] = {0, 0, 0, 0};
-    for (u32 i = 0; i < n; ++i)
-        w[i >> 2] |= (u32)p[i] << (8 * (i & 3));
-    u32x4 v = {w[0], w[1], w[2], w[3]};
+    u32x4 v = {0, 0, 0, 0};
+#pragma unroll
+    for (u32 i = 0; i < 15; ++i)
+        if (i < n)
+            v[i >> 2] |= (u32)p[i] << (8 * (i & 3));
     return v;
 }
 
@@ -647,19 +648,45 @@ struct BatchArgs {
 
 #define RUN_SCAN_CAP 256  // records examined per key-run scan (multi-key batches)
 
+// TLS 1.3 record framing (FRAME = 1; lib/picotls.c:719-749, :770-817, :5952-5974). Seal: the GCM plaintext is the
+// record's len payload bytes plus the inner content type (flags & 0xff); the wire record at out_off is the 5-byte
+// header {23, 3, 3, BE16(len + 17)} (also the AAD), the ciphertext, the tag. Open: the wire record at in_off is header
+// (the AAD, as received), len ciphertext bytes (inner type and padding included), tag; the plaintext goes to out_off.
+#define TLS_HEADER_SIZE 5
+template <bool OPEN, int FRAME>
+__device__ __forceinline__ u32 gcm_text_len(const ptls_mi355x_record_t &r)
+{
+    return FRAME && !OPEN ? r.len + 1 : r.len;
+}
+template <bool OPEN, int FRAME>
+__device__ __forceinline__ u32 gcm_aad_len(const ptls_mi355x_record_t &r)
+{
+    return FRAME ? (u32)TLS_HEADER_SIZE : (u32)r.aad_len;
+}
+// G-lane steps of a record's GHASH stream [pad | AAD | text | length]
+template <bool OPEN, int FRAME>
+__device__ __forceinline__ u32 gcm_steps(const ptls_mi355x_record_t &r)
+{
+    return (((gcm_aad_len<OPEN, FRAME>(r) + 15u) >> 4) + ((gcm_text_len<OPEN, FRAME>(r) + 15u) >> 4) + 1 + ENGINE_G - 1) /
+           ENGINE_G;
+}
+
 // GHASH/CTR work of one G-lane group on steps [m_lo, m_hi) of record r's stream (see file header): lane j owns stream
 // positions j + G*m and runs them NB at a time. The NB AES-CTR blocks of a step are independent (NB x 16 LDS lookups
 // per round in flight); their GHASH folds stay sequential (Horner with H^G, the segment's last step with H^(G-j)).
 // On return every lane of the group holds the segment's GHASH partial sum(X_i * H^(end - i)) and the length lane
 // (lane G-1, when the segment holds the length block) holds E(K, J0) in ek0. Invalid groups pass m_lo == m_hi.
-template <int NR, bool OPEN, int NB>
+template <int NR, bool OPEN, int NB, int FRAME = 0>
 __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 *lds, const u32 (&rk)[NR + 1][4], u32 iv0,
                                             u32 iv1, u32 iv2, const ptls_mi355x_record_t &r, bool valid, u32 m_lo,
                                             u32 m_hi, u32 j, u32 laneoff, u32 tsel_horner, u32 tsel_last, u32x4 &acc,
                                             u32x4 &ek0, bool finish, u64 rec)
 {
     constexpr int G = ENGINE_G;
-    const u32 L = r.len, A = r.aad_len;
+    constexpr bool SEAL_FRAME = FRAME && !OPEN, OPEN_FRAME = FRAME && OPEN;
+    const u32 L = gcm_text_len<OPEN, FRAME>(r), A = gcm_aad_len<OPEN, FRAME>(r);
+    // bytes of text readable at src (a framed seal reads len payload bytes; its last text byte is the content type)
+    const u32 Lsrc = SEAL_FRAME ? L - 1 : L;
     const u32 na = (A + 15) >> 4, nb = (L + 15) >> 4;
     const u32 total = na + nb + 1;
     const u32 K = (total + G - 1) / G;
@@ -673,9 +700,9 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     const u32 n0 = iv0 ^ rk[0][0];
     const u32 n1 = iv1 ^ bswap32((u32)(r.seq >> 32)) ^ rk[0][1];
     const u32 n2 = iv2 ^ bswap32((u32)r.seq) ^ rk[0][2];
-    const uint8_t *src = args.in + r.in_off;
-    uint8_t *dst = args.out + r.out_off;
-    const uint8_t *aadp = args.aad + r.aad_off;
+    const uint8_t *src = args.in + r.in_off + (OPEN_FRAME ? TLS_HEADER_SIZE : 0);
+    uint8_t *dst = args.out + r.out_off + (SEAL_FRAME ? TLS_HEADER_SIZE : 0);
+    const uint8_t *aadp = OPEN_FRAME ? args.in + r.in_off : args.aad + r.aad_off;
 
     acc = u32x4{0, 0, 0, 0};
     ek0 = u32x4{0, 0, 0, 0};
@@ -690,7 +717,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     // its HBM latency hides under the AES of the current step
     auto full_block = [&](u32 m, int &b) -> bool {
         b = (int)(j + G * m) - P - (int)na;
-        return m < m_hi && b >= 0 && b < (int)nb && L - 16u * (u32)b >= 16;
+        return m < m_hi && b >= 0 && b < (int)nb && Lsrc - 16u * (u32)b >= 16;
     };
     u32x4 nxt[NB];
 #pragma unroll
@@ -739,21 +766,33 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             if (is_data) {
                 const u32 rem = L - 16u * (u32)b;
                 uint8_t *op = dst + 16u * (u32)b;
-                if (rem >= 16) {
+                if (rem >= 16 && (!SEAL_FRAME || Lsrc - 16u * (u32)b >= 16)) {
                     const u32x4 v = cur[i];
                     const u32x4 o = v ^ ks;
                     *(u32x4_u *)op = o;
                     X = OPEN ? v : o;
                 } else {
-                    const u32x4 v = load_partial(src + 16u * (u32)b, rem);
-                    const u32x4 o = mask_tail(v ^ ks, rem);
-                    store_partial(op, o, rem);
+                    const u32 srem = Lsrc - 16u * (u32)b;
+                    u32x4 v = load_partial(src + 16u * (u32)b, srem);
+                    if (SEAL_FRAME)  // the inner content type follows the payload
+                        v[srem >> 2] |= (u32)(r.flags & 0xffu) << (8 * (srem & 3));
+                    const u32x4 o = rem >= 16 ? v ^ ks : mask_tail(v ^ ks, rem);
+                    if (rem >= 16)
+                        *(u32x4_u *)op = o;
+                    else
+                        store_partial(op, o, rem);
                     X = OPEN ? v : o;
                 }
             } else if (is_aad) {
-                const u32 rem = A - 16u * (u32)logical;
-                const uint8_t *ap = aadp + 16u * (u32)logical;
-                X = rem >= 16 ? *(const u32x4_u *)ap : load_partial(ap, rem);
+                if (SEAL_FRAME) {  // the record header: built here, written to the wire, and authenticated
+                    const u32 wl = L + 16;
+                    X = u32x4{0x00030317u | ((wl >> 8) & 0xffu) << 24, wl & 0xffu, 0, 0};
+                    store_partial(args.out + r.out_off, X, TLS_HEADER_SIZE);
+                } else {
+                    const u32 rem = A - 16u * (u32)logical;
+                    const uint8_t *ap = aadp + 16u * (u32)logical;
+                    X = rem >= 16 ? *(const u32x4_u *)ap : load_partial(ap, rem);
+                }
             } else if (is_len) {
                 const u64 abits = (u64)A * 8, cbits = (u64)L * 8;
                 X[0] = bswap32((u32)(abits >> 32));
@@ -805,7 +844,7 @@ __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u
     ptls_mi355x_record_t r = {};
     if (valid)
         r = args.recs[rec];
-    const u32 K = valid ? (((r.aad_len + 15u) >> 4) + ((r.len + 15u) >> 4) + 1 + G - 1) / G : 0;
+    const u32 K = valid ? gcm_steps<OPEN, 0>(r) : 0;
     u32x4 acc, ek0;
     gcm_segment<NR, OPEN, NB>(args, lds, rk, iv0, iv1, iv2, r, valid, 0, K, j, laneoff, tsel_horner, tsel_last, acc, ek0,
                               true, rec);
@@ -921,7 +960,7 @@ __device__ __forceinline__ unsigned long long stamp()
 // GHASH = sum_k P_k * H^(k * CHUNK_BLOCKS). The group that completes a record's last outstanding unit (LDS counter per
 // record) evaluates that sum by Horner with the H^CHUNK_BLOCKS table and finishes the tag, inside the unit loop.
 // Single-unit records finish inside their unit as in the lockstep kernel.
-template <int NR, bool OPEN>
+template <int NR, bool OPEN, int FRAME>
 __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGINE_WAVES_PER_SIMD, ENGINE_WAVES_PER_SIMD))) void gcm_chunked_kernel(BatchArgs args)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -967,7 +1006,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             u32 smin = 0xffffffffu, smax = 0;
             if (t < lim) {
                 const ptls_mi355x_record_t r = args.recs[pos + t];
-                const u32 steps = (((r.aad_len + 15u) >> 4) + ((r.len + 15u) >> 4) + 1 + G - 1) / G;
+                const u32 steps = gcm_steps<OPEN, FRAME>(r);
                 nc = (steps + CHUNK_STEPS - 1) / CHUNK_STEPS;
                 // front-unit size bucket: 0 = very long record run whole (nc forced to 1), else CHUNK_STEPS + 1 -
                 // size of the record's first unit (1 = a full unit, CHUNK_STEPS = one step)
@@ -1129,13 +1168,13 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             ptls_mi355x_record_t r = {};
             if (valid)
                 r = args.recs[pos + ri];
-            const u32 steps = (((r.aad_len + 15u) >> 4) + ((r.len + 15u) >> 4) + 1 + G - 1) / G;
+            const u32 steps = gcm_steps<OPEN, FRAME>(r);
             u32 m_hi = steps - k_back * CHUNK_STEPS;
             u32 m_lo = k_back + 1 == unc ? 0u : m_hi - CHUNK_STEPS;
             if (!valid)
                 m_lo = m_hi = 0;
             u32x4 acc, ek0;
-            gcm_segment<NR, OPEN, 1>(args, lds, rk, iv0, iv1, iv2, r, valid, m_lo, m_hi, j, laneoff, tsel_horner,
+            gcm_segment<NR, OPEN, 1, FRAME>(args, lds, rk, iv0, iv1, iv2, r, valid, m_lo, m_hi, j, laneoff, tsel_horner,
                                      tsel_last, acc, ek0, unc == 1, pos + ri);
             if (valid && unc > 1) {  // uniform over the group
                 u32 last = 0;
@@ -1155,11 +1194,12 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                     const u32x4 tag = g ^ s_ek0[ri];
                     if (j != G - 1) {
                     } else if (OPEN) {
-                        const u32x4 rt = *(const u32x4_u *)(args.in + r.in_off + r.len);
+                        const u32x4 rt = *(const u32x4_u *)(args.in + r.in_off + (FRAME ? TLS_HEADER_SIZE : 0) +
+                                                            gcm_text_len<OPEN, FRAME>(r));
                         const u32x4 d = rt ^ tag;
                         args.ok[pos + ri] = (d[0] | d[1] | d[2] | d[3]) == 0;
                     } else {
-                        *(u32x4_u *)(args.out + r.out_off + r.len) = tag;
+                        *(u32x4_u *)(args.out + r.out_off + (FRAME ? TLS_HEADER_SIZE : 0) + gcm_text_len<OPEN, FRAME>(r)) = tag;
                     }
                 }
             }
@@ -1182,10 +1222,11 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     }
 }
 
-// AES-ECB of independent blocks (one block per thread, keys from the keyset)
+// AES-ECB of independent blocks (one block per thread, keys from the keyset). Blocks whose key index is out of range
+// produce zeros.
 template <int NR>
-__global__ __launch_bounds__(256) void ecb_kernel(const KeyEntry *keys, const u32 *key_idx, const uint8_t *in, uint8_t *out,
-                                                  u64 nblocks)
+__global__ __launch_bounds__(256) void ecb_kernel(const KeyEntry *keys, u32 nkeys, const u32 *key_idx, const uint8_t *in,
+                                                  uint8_t *out, u64 nblocks)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     lds_u8 *lds = (lds_u8 *)smem;
@@ -1194,16 +1235,84 @@ __global__ __launch_bounds__(256) void ecb_kernel(const KeyEntry *keys, const u3
     __syncthreads();
     const u32 laneoff = (threadIdx.x & 31) * 4;
     for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < nblocks; i += (u64)gridDim.x * blockDim.x) {
-        const KeyEntry *k = keys + (key_idx != nullptr ? key_idx[i] : 0);
-        u32 rk[NR + 1][4];
-        for (int r = 0; r <= NR; ++r)
-            for (int c = 0; c < 4; ++c)
-                rk[r][c] = k->rk[r][c];
-        const u32x4 v = *(const u32x4_u *)(in + 16 * i);
-        u32 s0 = v[0] ^ rk[0][0], s1 = v[1] ^ rk[0][1], s2 = v[2] ^ rk[0][2], s3 = v[3] ^ rk[0][3];
-        aes_encrypt_tt<NR>(lds, laneoff, rk, s0, s1, s2, s3);
-        const u32x4 o = {s0, s1, s2, s3};
+        const u32 ki = key_idx != nullptr ? key_idx[i] : 0u;
+        u32x4 o = {0, 0, 0, 0};
+        if (ki < nkeys) {
+            const KeyEntry *k = keys + ki;
+            u32 rk[NR + 1][4];
+            for (int r = 0; r <= NR; ++r)
+                for (int c = 0; c < 4; ++c)
+                    rk[r][c] = k->rk[r][c];
+            const u32x4 v = *(const u32x4_u *)(in + 16 * i);
+            u32 s0 = v[0] ^ rk[0][0], s1 = v[1] ^ rk[0][1], s2 = v[2] ^ rk[0][2], s3 = v[3] ^ rk[0][3];
+            aes_encrypt_tt<NR>(lds, laneoff, rk, s0, s1, s2, s3);
+            o = u32x4{s0, s1, s2, s3};
+        }
         *(u32x4_u *)(out + 16 * i) = o;
+    }
+}
+
+// QUIC header-protection masks (fusion's supp, lib/fusion.c:425-430,636-651): mask[i] = AES-ECB(hp key, the 16-byte
+// sample at base + hp[i].sample_off). Runs after the seal kernel on the same stream, so the sample may cover the tag.
+template <int NR>
+__global__ __launch_bounds__(256) void hp_kernel(const KeyEntry *keys, u32 nkeys, const ptls_mi355x_hp_t *hp, const uint8_t *base,
+                                                 uint8_t *masks, u64 n)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    lds_u8 *lds = (lds_u8 *)smem;
+    check_lds_base(smem);
+    build_aes_tables(lds);
+    __syncthreads();
+    const u32 laneoff = (threadIdx.x & 31) * 4;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        const ptls_mi355x_hp_t h = hp[i];
+        u32x4 o = {0, 0, 0, 0};
+        if (h.key_idx < nkeys) {
+            const KeyEntry *k = keys + h.key_idx;
+            u32 rk[NR + 1][4];
+            for (int r = 0; r <= NR; ++r)
+                for (int c = 0; c < 4; ++c)
+                    rk[r][c] = k->rk[r][c];
+            const u32x4 v = *(const u32x4_u *)(base + h.sample_off);
+            u32 s0 = v[0] ^ rk[0][0], s1 = v[1] ^ rk[0][1], s2 = v[2] ^ rk[0][2], s3 = v[3] ^ rk[0][3];
+            aes_encrypt_tt<NR>(lds, laneoff, rk, s0, s1, s2, s3);
+            o = u32x4{s0, s1, s2, s3};
+        }
+        *(u32x4_u *)(masks + 16 * i) = o;
+    }
+}
+
+// After opening framed TLS records: outer header check, then the receive-side padding strip of lib/picotls.c:5960-5968
+// (the inner content type is the last non-zero plaintext byte; an all-zero plaintext, or an empty alert / handshake
+// record, is an unexpected message). One thread per record; ok[i] becomes 1 only for status 0.
+__global__ __launch_bounds__(256) void tls_unpad_kernel(const ptls_mi355x_record_t *recs, u64 n, const uint8_t *in,
+                                                        const uint8_t *out, uint8_t *ok, ptls_mi355x_tls_result_t *res)
+{
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        const ptls_mi355x_record_t r = recs[i];
+        ptls_mi355x_tls_result_t o = {0, 0, 0, 0};
+        const uint8_t *h = in + r.in_off;
+        if (!ok[i]) {
+            o.status = PTLS_MI355X_TLS_BAD_MAC;
+        } else if (h[0] != 23 || h[1] != 3 || h[2] != 3 || ((u32)h[3] << 8 | h[4]) != r.len + 16) {
+            o.status = PTLS_MI355X_TLS_BAD_HEADER;
+        } else {
+            const uint8_t *p = out + r.out_off;
+            u32 len = r.len;
+            while (len != 0 && p[len - 1] == 0)
+                --len;
+            if (len == 0) {
+                o.status = PTLS_MI355X_TLS_UNEXPECTED_MESSAGE;
+            } else {
+                o.content_type = p[len - 1];
+                o.plain_len = len - 1;
+                if (o.plain_len == 0 && (o.content_type == 21 || o.content_type == 22))
+                    o.status = PTLS_MI355X_TLS_UNEXPECTED_MESSAGE;
+            }
+        }
+        ok[i] = o.status == 0;
+        if (res != nullptr)
+            res[i] = o;
     }
 }
 
@@ -1242,12 +1351,22 @@ static int engine_init_attrs(void)
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<10, true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<14, false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<14, true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
-    HIP_TRY(hipFuncSetAttribute((const void *)gcm_chunked_kernel<10, false>, hipFuncAttributeMaxDynamicSharedMemorySize, CLDS_ALLOC));
-    HIP_TRY(hipFuncSetAttribute((const void *)gcm_chunked_kernel<10, true>, hipFuncAttributeMaxDynamicSharedMemorySize, CLDS_ALLOC));
-    HIP_TRY(hipFuncSetAttribute((const void *)gcm_chunked_kernel<14, false>, hipFuncAttributeMaxDynamicSharedMemorySize, CLDS_ALLOC));
-    HIP_TRY(hipFuncSetAttribute((const void *)gcm_chunked_kernel<14, true>, hipFuncAttributeMaxDynamicSharedMemorySize, CLDS_ALLOC));
+#define CHUNKED_ATTR(nr, open, frame)                                                                                  \
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_chunked_kernel<nr, open, frame>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                CLDS_ALLOC))
+    CHUNKED_ATTR(10, false, 0);
+    CHUNKED_ATTR(10, true, 0);
+    CHUNKED_ATTR(14, false, 0);
+    CHUNKED_ATTR(14, true, 0);
+    CHUNKED_ATTR(10, false, 1);
+    CHUNKED_ATTR(10, true, 1);
+    CHUNKED_ATTR(14, false, 1);
+    CHUNKED_ATTR(14, true, 1);
+#undef CHUNKED_ATTR
     HIP_TRY(hipFuncSetAttribute((const void *)ecb_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
     HIP_TRY(hipFuncSetAttribute((const void *)ecb_kernel<14>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
+    HIP_TRY(hipFuncSetAttribute((const void *)hp_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
+    HIP_TRY(hipFuncSetAttribute((const void *)hp_kernel<14>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
     done = 1;
     return 0;
 }
@@ -1366,7 +1485,7 @@ int ptls_mi355x_keyset_set_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, const vo
 static bool use_chunked(const ptls_mi355x_keyset_t *ks) { return ks->schedule != PTLS_MI355X_SCHEDULE_LOCKSTEP; }
 
 static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
-                        const void *aad, void *out, uint8_t *ok, void *stream)
+                        const void *aad, void *out, uint8_t *ok, void *stream, int frame = 0)
 {
     if (ks == NULL || (nrecs != 0 && (recs == NULL || in == NULL || out == NULL || (open && ok == NULL))))
         return fail("%s", "batch: invalid arguments");
@@ -1384,17 +1503,30 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
     if (grid < 1)
         grid = 1;
     hipStream_t s = (hipStream_t)stream;
-    if (use_chunked(ks)) {
+#define CHUNKED_LAUNCH(nr, op, frame) gcm_chunked_kernel<nr, op, frame><<<(unsigned)grid, ENGINE_WG, CLDS_ALLOC, s>>>(a)
+    if (frame) {
         if (ks->nr == 10) {
             if (open)
-                gcm_chunked_kernel<10, true><<<(unsigned)grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
+                CHUNKED_LAUNCH(10, true, 1);
             else
-                gcm_chunked_kernel<10, false><<<(unsigned)grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
+                CHUNKED_LAUNCH(10, false, 1);
         } else {
             if (open)
-                gcm_chunked_kernel<14, true><<<(unsigned)grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
+                CHUNKED_LAUNCH(14, true, 1);
             else
-                gcm_chunked_kernel<14, false><<<(unsigned)grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
+                CHUNKED_LAUNCH(14, false, 1);
+        }
+    } else if (use_chunked(ks)) {
+        if (ks->nr == 10) {
+            if (open)
+                CHUNKED_LAUNCH(10, true, 0);
+            else
+                CHUNKED_LAUNCH(10, false, 0);
+        } else {
+            if (open)
+                CHUNKED_LAUNCH(14, true, 0);
+            else
+                CHUNKED_LAUNCH(14, false, 0);
         }
     } else if (ks->nr == 10) {
         if (open)
@@ -1435,11 +1567,67 @@ int ptls_mi355x_ecb_batch(ptls_mi355x_keyset_t *ks, const uint32_t *key_idx, con
         grid = (u64)ks->ncu * 4;
     hipStream_t s = (hipStream_t)stream;
     if (ks->nr == 10)
-        ecb_kernel<10><<<(unsigned)grid, 256, LDS_AES_BYTES, s>>>(ks->d_keys, key_idx, (const uint8_t *)in, (uint8_t *)out, nblocks);
+        ecb_kernel<10><<<(unsigned)grid, 256, LDS_AES_BYTES, s>>>(ks->d_keys, (u32)ks->nkeys, key_idx, (const uint8_t *)in,
+                                                                  (uint8_t *)out, nblocks);
     else
-        ecb_kernel<14><<<(unsigned)grid, 256, LDS_AES_BYTES, s>>>(ks->d_keys, key_idx, (const uint8_t *)in, (uint8_t *)out, nblocks);
+        ecb_kernel<14><<<(unsigned)grid, 256, LDS_AES_BYTES, s>>>(ks->d_keys, (u32)ks->nkeys, key_idx, (const uint8_t *)in,
+                                                                  (uint8_t *)out, nblocks);
     HIP_TRY(hipGetLastError());
     return 0;
+}
+
+int ptls_mi355x_seal_tls_records(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
+                                 void *out, void *stream)
+{
+    return launch_batch(ks, false, recs, nrecs, in, NULL, out, NULL, stream, 1);
+}
+
+int ptls_mi355x_open_tls_records(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
+                                 void *out, uint8_t *ok, ptls_mi355x_tls_result_t *results, void *stream)
+{
+    if (launch_batch(ks, true, recs, nrecs, in, NULL, out, ok, stream, 1) != 0)
+        return -1;
+    if (nrecs == 0)
+        return 0;
+    u64 grid = (nrecs + 255) / 256;
+    if (grid > (u64)ks->ncu * 4)
+        grid = (u64)ks->ncu * 4;
+    tls_unpad_kernel<<<(unsigned)grid, 256, 0, (hipStream_t)stream>>>(recs, nrecs, (const uint8_t *)in, (const uint8_t *)out,
+                                                                       ok, results);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int ptls_mi355x_hp_mask_batch(ptls_mi355x_keyset_t *hp_ks, const ptls_mi355x_hp_t *hp, size_t n, const void *base,
+                              void *masks, void *stream)
+{
+    if (hp_ks == NULL || (n != 0 && (hp == NULL || base == NULL || masks == NULL)))
+        return fail("%s", "hp_mask: invalid arguments");
+    if (n == 0)
+        return 0;
+    u64 grid = (n + 255) / 256;
+    if (grid > (u64)hp_ks->ncu * 4)
+        grid = (u64)hp_ks->ncu * 4;
+    hipStream_t s = (hipStream_t)stream;
+    if (hp_ks->nr == 10)
+        hp_kernel<10><<<(unsigned)grid, 256, LDS_AES_BYTES, s>>>(hp_ks->d_keys, (u32)hp_ks->nkeys, hp, (const uint8_t *)base,
+                                                                 (uint8_t *)masks, n);
+    else
+        hp_kernel<14><<<(unsigned)grid, 256, LDS_AES_BYTES, s>>>(hp_ks->d_keys, (u32)hp_ks->nkeys, hp, (const uint8_t *)base,
+                                                                 (uint8_t *)masks, n);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int ptls_mi355x_seal_batch_hp(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
+                              const void *aad, void *out, ptls_mi355x_keyset_t *hp_ks, const ptls_mi355x_hp_t *hp,
+                              void *masks, void *stream)
+{
+    if (hp_ks == NULL || (nrecs != 0 && (hp == NULL || masks == NULL)))
+        return fail("%s", "seal_batch_hp: invalid arguments");
+    if (launch_batch(ks, false, recs, nrecs, in, aad, out, NULL, stream) != 0)
+        return -1;
+    return ptls_mi355x_hp_mask_batch(hp_ks, hp, nrecs, out, masks, stream);
 }
 
 int ptls_mi355x_encrypt_block(ptls_mi355x_keyset_t *ks, size_t key_idx, void *out, const void *in)

@@ -24,6 +24,15 @@ RECORD_DTYPE = np.dtype(
 )
 assert RECORD_DTYPE.itemsize == 40
 
+# ptls_mi355x_hp_t: one QUIC header-protection sample per packet
+HP_DTYPE = np.dtype([("sample_off", "<u8"), ("key_idx", "<u4"), ("reserved", "<u4")])
+assert HP_DTYPE.itemsize == 16
+
+# ptls_mi355x_tls_result_t: per-record outcome of ptls_mi355x_open_tls_records
+TLS_RESULT_DTYPE = np.dtype([("plain_len", "<u4"), ("content_type", "u1"), ("status", "u1"), ("reserved", "<u2")])
+assert TLS_RESULT_DTYPE.itemsize == 8
+TLS_OK, TLS_BAD_MAC, TLS_BAD_HEADER, TLS_UNEXPECTED_MESSAGE = 0, 1, 2, 3
+
 
 def _round16(x):
     if isinstance(x, np.ndarray):
