@@ -58,8 +58,12 @@ def make_rank(gpus: int):
     if world == 1 and gpus > 1:
         raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the multi-rank path on a one-GPU box: every rank on cuda:0, gloo for the barrier/reductions
+    one_device = os.environ.get("PTLS_BENCH_ONE_DEVICE") == "1"
+    if one_device:
+        local = 0
     torch.cuda.set_device(local)
-    return RankContext.from_env("nccl", device=torch.device("cuda", local))
+    return RankContext.from_env("gloo" if one_device else "nccl", device=torch.device("cuda", local))
 
 
 def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool, schedule: str = "auto"):
@@ -247,7 +251,7 @@ def cpu_baseline(wl, seconds: float):
             "open_GiBps": round(b.payload_bytes * reps / 2**30 / t_open, 3)}
 
 
-def run_e2e(R, wl, nchunks: int = 16, reps: int = 3):
+def run_e2e(R, wl, nchunks: int = 16, reps: int = 3, schedule: str = "auto"):
     """Records that start and end in host memory (socket / NIC buffers): pinned host -> H2D -> seal -> D2H, then
     the sealed records back through H2D -> open -> D2H. Serial (one stream) and pipelined (chunks over three
     streams, so copies in both directions overlap the kernels). Payload GiB/s per direction (seal+open averaged)."""
@@ -414,7 +418,8 @@ def main():
     if extra:
         out["extra"] = extra
     if args.e2e:
-        out["e2e_host_buffers"] = run_e2e(R, WORKLOADS[args.workload].scaled(min(wl.nrecs, max(1, (4 << 30) // (wl.rec_len or 8192)))))
+        out["e2e_host_buffers"] = run_e2e(R, WORKLOADS[args.workload].scaled(min(wl.nrecs, max(1, (4 << 30) // (wl.rec_len or 8192)))),
+                                          schedule=args.schedule)
     if R.rank == 0 and R.world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds)
     elif R.rank == 0:
