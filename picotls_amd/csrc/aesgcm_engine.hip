@@ -86,6 +86,9 @@ struct KeyEntry {
 };
 static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 
+#ifndef ENGINE_FAST_STEP
+#define ENGINE_FAST_STEP 1         // wave-uniform fast path for steps where every lane holds a full text block
+#endif
 #ifndef GHASH_BATCH
 #define GHASH_BATCH 0      // 1: issue GHASH table lookups in batches of 8
 #endif
@@ -763,6 +766,17 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             const u32x4 ks = {st[i][0], st[i][1], st[i][2], st[i][3]};
 
             u32x4 X = {0, 0, 0, 0};
+#if ENGINE_FAST_STEP
+            // steady state: every active lane of the wave holds a full 16-byte text block (one uniform branch, no
+            // per-case dispatch)
+            const bool full = is_data && Lsrc - 16u * (u32)b >= 16;
+            if (__all(!act || full)) {
+                const u32x4 o = cur[i] ^ ks;
+                if (act)
+                    *(u32x4_u *)(dst + 16u * (u32)b) = o;
+                X = OPEN ? cur[i] : o;
+            } else
+#endif
             if (is_data) {
                 const u32 rem = L - 16u * (u32)b;
                 uint8_t *op = dst + 16u * (u32)b;
@@ -801,11 +815,10 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                 X[3] = bswap32((u32)cbits);
                 ek0 = ks;
             }
-            acc ^= X;
             // scheduling fence: keeps the 32 table loads of this fold from being hoisted next to the other blocks'
             // work (that hoisting spills them to scratch)
             __builtin_amdgcn_sched_barrier(0);
-            const u32x4 prod = gmul_tab(lds, acc, m + 1 == m_hi ? tsel_last : tsel_horner);
+            const u32x4 prod = gmul_tab(lds, acc ^ X, m + 1 == m_hi ? tsel_last : tsel_horner);
             if (act)
                 acc = prod;
             __builtin_amdgcn_sched_barrier(0);
