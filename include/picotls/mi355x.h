@@ -178,6 +178,32 @@ int ptls_mi355x_seal_batch_hp(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record
                               void *masks, void *stream);
 
 /**
+ * QUIC-LB connection-ID encryption, batched (draft-ietf-quic-load-balancers; lib/quiclb-impl.h:100-162, the cipher
+ * behind ptls_fusion_quiclb lib/fusion.c:2186-2233 / ptls_openssl_quiclb). Entry i transforms len bytes at
+ * in + in_off into out + out_off (may alias) under the AES-128 key key_idx of ks (a keyset created with key_size 16;
+ * its IVs are unused): encrypt = 1 gives ptls_cipher_encrypt on a context made with ptls_cipher_new(&quiclb, 1, key),
+ * encrypt = 0 the inverse (is_enc = 0). len is PTLS_QUICLB_MIN_BLOCK_SIZE (7) .. PTLS_QUICLB_MAX_BLOCK_SIZE (19)
+ * (include/picotls.h:116-122); entries with another len or an out-of-range key_idx are skipped (nothing written), where
+ * the reference asserts. DEVICE pointers; returns -1 on invalid arguments or a keyset that is not AES-128.
+ */
+#define PTLS_MI355X_QUICLB_MIN_LEN 7
+#define PTLS_MI355X_QUICLB_MAX_LEN 19
+typedef struct st_ptls_mi355x_cid_t {
+    uint64_t in_off;
+    uint64_t out_off;
+    uint32_t key_idx;
+    uint8_t len;
+    uint8_t encrypt;
+    uint16_t reserved; /* 0 */
+} ptls_mi355x_cid_t;
+
+int ptls_mi355x_quiclb_batch(ptls_mi355x_keyset_t *ks, const ptls_mi355x_cid_t *cids, size_t n, const void *in, void *out,
+                             void *stream);
+/* one CID on HOST buffers (backs the ptls_mi355x_quiclb cipher object): returns 0, or -1 on invalid arguments */
+int ptls_mi355x_quiclb_transform(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const void *input, size_t len,
+                                 int encrypt);
+
+/**
  * Synchronous single-record helpers on HOST buffers (a batch of one, with H2D/D2H copies). These back the picotls
  * vtable (do_encrypt / do_decrypt) and mirror ptls_aead_encrypt / ptls_aead_decrypt: encrypt writes len+16 bytes;
  * decrypt takes inlen = len+16 and returns the plaintext length or SIZE_MAX (tag mismatch or inlen < 16).

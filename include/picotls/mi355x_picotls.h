@@ -17,6 +17,8 @@ extern "C" {
 #endif
 
 extern ptls_cipher_algorithm_t ptls_mi355x_aes128ctr, ptls_mi355x_aes256ctr;
+/* QUIC-LB connection-ID cipher, the counterpart of ptls_fusion_quiclb (include/picotls/fusion.h:121, lib/fusion.c:2226-2233) */
+extern ptls_cipher_algorithm_t ptls_mi355x_quiclb;
 extern ptls_aead_algorithm_t ptls_mi355x_aes128gcm, ptls_mi355x_aes256gcm;
 
 /**

@@ -72,6 +72,7 @@ class GcmOracle:
         lib.oracle_gcm_open.restype = sz
         lib.oracle_seal_batch.argtypes = [vp, vp, sz, vp, sz, vp, vp, vp]
         lib.oracle_open_batch.argtypes = [vp, vp, sz, vp, sz, vp, vp, vp, vp]
+        lib.oracle_quiclb_transform.argtypes = [vp, vp, vp, sz, ctypes.c_int]
         self.lib = lib
 
     def aes_encrypt(self, key: bytes, block: bytes) -> bytes:
@@ -105,6 +106,13 @@ class GcmOracle:
             return None
         return bytes(out[:r])
 
+    def quiclb(self, key: bytes, data: bytes, encrypt: bool) -> bytes:
+        """picotls_quiclb_transform (lib/quiclb-impl.h:107-162) restated in oracle/gcm_ref.c."""
+        out = bytearray(len(data))
+        if self.lib.oracle_quiclb_transform(_ptr(key), _ptr(out), _ptr(bytes(data)), len(data), 1 if encrypt else 0) != 0:
+            raise ValueError("QUIC-LB length must be 7..19")
+        return bytes(out)
+
     def seal_batch(self, keys, ivs, key_size, recs, in_arena, aad_arena, out_arena):
         self.lib.oracle_seal_batch(_ptr(keys), _ptr(ivs), key_size, _ptr(recs), len(recs), _ptr(in_arena),
                                    _ptr(aad_arena), _ptr(out_arena))
@@ -134,6 +142,7 @@ class FusionRef:
         lib.ref_fusion_raw_seal.argtypes = [vp, sz, vp, sz, vp, sz, vp]
         lib.ref_seal_with_hp.argtypes = [vp, sz, vp, u64, vp, sz, vp, sz, vp, vp, sz, vp]
         lib.ref_aesecb.argtypes = [vp, sz, vp, vp]
+        lib.ref_quiclb.argtypes = [vp, vp, vp, sz, ci]
         self.lib = lib
         if not lib.ref_cpu_supported():
             raise RuntimeError("host CPU lacks AES-NI/PCLMUL/AVX2: lib/fusion.c cannot run here")
@@ -168,6 +177,12 @@ class FusionRef:
     def aesecb(self, key, block):
         out = bytearray(16)
         self.lib.ref_aesecb(_ptr(key), len(key), _ptr(out), _ptr(block))
+        return bytes(out)
+
+    def quiclb(self, key: bytes, data: bytes, encrypt: bool) -> bytes:
+        """ptls_fusion_quiclb through ptls_cipher_new / ptls_cipher_encrypt (t/quiclb.c:36-45)."""
+        out = bytearray(len(data))
+        self.lib.ref_quiclb(_ptr(key), _ptr(out), _ptr(bytes(data)), len(data), 1 if encrypt else 0)
         return bytes(out)
 
     def run_batch(self, is_seal, keys, ivs, key_size, recs, in_arena, aad_arena, out_arena, ok=None, nthreads=1,

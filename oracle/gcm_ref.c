@@ -18,6 +18,8 @@
  *                                             lib/fusion.c:1127-1134 (calc_counter): nonce = iv ^ (0^32 || seq_be64)
  *   - vtable semantics                        lib/fusion.c:1136-1171 (aead_do_encrypt / aead_do_decrypt:
  *                                             inlen < 16 -> SIZE_MAX)
+ *   - QUIC-LB CID cipher                      lib/quiclb-impl.h:47-162 (picotls_quiclb_transform), the cipher of
+ *                                             ptls_fusion_quiclb (lib/fusion.c:2186-2233); pinned by t/quiclb.c:27-30
  *
  * Parity pinning: tests/test_oracle.py checks this file against the known-answer vectors held in the
  * reference's own tests (t/fusion.c:80,85,128-227,239-280,310-332,353-359 and t/picotls.c ECB vectors), stored as
@@ -305,4 +307,63 @@ void oracle_open_batch(const uint8_t *keys, const uint8_t *ivs, size_t key_size,
             diff |= tag[k] ^ in[r->in_off + r->len + k];
         ok[i] = diff == 0;
     }
+}
+
+/* ---------------------------------------------------------------- QUIC-LB CID cipher (lib/quiclb-impl.h) */
+
+/* One Feistel round (lib/quiclb-impl.h:47-70 picotls_quiclb_one_round): dest = x ^ AES((y & mask) | len_pass), with
+ * len_pass = 0^112 || len || round (:133-135). Blocks are 16 bytes; only the first (len + 1) / 2 bytes of a half matter. */
+static void quiclb_round(const uint8_t *rk, int nr, uint8_t dest[16], const uint8_t x[16], const uint8_t y[16],
+                         const uint8_t mask[16], size_t len, int rnd)
+{
+    uint8_t t[16];
+    for (int i = 0; i < 16; ++i)
+        t[i] = y[i] & mask[i];
+    t[14] |= (uint8_t)len;
+    t[15] |= (uint8_t)rnd;
+    oracle_aes_encrypt_rk(rk, nr, t, t);
+    for (int i = 0; i < 16; ++i)
+        dest[i] = t[i] ^ x[i];
+}
+
+/* picotls_quiclb_transform (lib/quiclb-impl.h:107-162) for 7 <= len <= 19 with an AES-128 key; returns -1 otherwise.
+ * The masks (:111-125) are derived rather than tabulated: the left half keeps bytes [0, len/2) plus the high nibble of
+ * the middle byte when len is odd; the right half keeps that middle byte's low nibble (its byte 0) and the bytes after
+ * it. split (:72-84) and merge (:86-100) follow the reference byte for byte. */
+int oracle_quiclb_transform(const uint8_t key[16], uint8_t *output, const uint8_t *input, size_t len, int encrypt)
+{
+    if (len < 7 || len > 19)
+        return -1;
+    uint8_t rk[240];
+    const int nr = oracle_aes_expand(rk, key, 16);
+    const size_t half = len / 2, hl = (len + 1) / 2, odd = len & 1;
+    uint8_t ml[16] = {0}, mr[16] = {0};
+    for (size_t i = 0; i < half; ++i)
+        ml[i] = 0xff, mr[i + odd] = 0xff;
+    if (odd)
+        ml[half] = 0xf0, mr[0] = 0x0f;
+    uint8_t a[16] = {0}, b[16] = {0}, l1[16], r1[16], l[16], r[16];
+    for (size_t i = 0; i < hl; ++i)
+        a[i] = input[i], b[i] = input[i + half];
+    if (encrypt) { /* (:149-154): l0 = a, r0 = b */
+        quiclb_round(rk, nr, r1, b, a, ml, len, 1);
+        quiclb_round(rk, nr, l1, a, r1, mr, len, 2);
+        quiclb_round(rk, nr, r, r1, l1, ml, len, 3);
+        quiclb_round(rk, nr, l, l1, r, mr, len, 4);
+    } else { /* (:155-161): l2 = a, r2 = b */
+        quiclb_round(rk, nr, l1, a, b, mr, len, 4);
+        quiclb_round(rk, nr, r1, b, l1, ml, len, 3);
+        quiclb_round(rk, nr, l, l1, r1, mr, len, 2);
+        quiclb_round(rk, nr, r, r1, l, ml, len, 1);
+    }
+    uint8_t tmp[19];
+    size_t o = 0;
+    for (size_t i = 0; i < half; ++i)
+        tmp[o++] = l[i];
+    if (odd)
+        tmp[o++] = (l[half] & 0xf0) | (r[0] & 0x0f);
+    for (size_t i = 0; i < half; ++i)
+        tmp[o++] = r[i + odd];
+    memcpy(output, tmp, len); /* output may alias input */
+    return 0;
 }

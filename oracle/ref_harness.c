@@ -202,3 +202,11 @@ void ref_aesecb(const uint8_t *key, size_t key_size, uint8_t *out, const uint8_t
     ptls_fusion_aesecb_encrypt(&ecb, out, in);
     ptls_fusion_aesecb_dispose(&ecb);
 }
+
+/* QUIC-LB through picotls' cipher API on fusion's object (ptls_fusion_quiclb, lib/fusion.c:2226-2233), as t/quiclb.c:36-45 */
+void ref_quiclb(const uint8_t *key, uint8_t *out, const uint8_t *in, size_t len, int encrypt)
+{
+    ptls_cipher_context_t *ctx = ptls_cipher_new(&ptls_fusion_quiclb, encrypt, key);
+    ptls_cipher_encrypt(ctx, out, in, len);
+    ptls_cipher_free(ctx);
+}

@@ -9,7 +9,8 @@ operator interface (``include/picotls.h:519-580, 2082-2164``; ``lib/picotls.c:65
 * :func:`aead_new_direct` -> :class:`AeadContext` with ``encrypt`` / ``encrypt_s`` / ``decrypt`` / ``get_iv`` /
   ``set_iv`` / ``xor_iv`` (``decrypt`` returns ``None`` where picotls returns ``SIZE_MAX``)
 * :class:`Keyset`, :func:`seal_batch`, :func:`open_batch`, :func:`ecb_batch`, :func:`hp_mask_batch`,
-  :func:`seal_batch_hp` -- the batch extension.
+  :func:`seal_batch_hp`, :func:`quiclb_batch` -- the batch extension.
+* :class:`QuicLbCipher` -- mirror of ``ptls_mi355x_quiclb`` (fusion's ``ptls_fusion_quiclb``).
 
 There is no CPU fallback: when the shared object or a gfx950 device is missing every entry point raises.
 """
@@ -21,7 +22,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from .records import (HP_DTYPE, RECORD_DTYPE, TLS_BAD_HEADER, TLS_BAD_MAC, TLS_OK, TLS_RESULT_DTYPE,  # noqa: F401
+from .records import (CID_DTYPE, HP_DTYPE, QUICLB_MAX_LEN, QUICLB_MIN_LEN, RECORD_DTYPE, TLS_BAD_HEADER, TLS_BAD_MAC, TLS_OK, TLS_RESULT_DTYPE,  # noqa: F401
                       TLS_UNEXPECTED_MESSAGE, RecordBatch, shard_ranges)
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
@@ -45,6 +46,8 @@ ABI_FUNCTIONS = (
     "ptls_mi355x_ecb_batch",
     "ptls_mi355x_hp_mask_batch",
     "ptls_mi355x_seal_batch_hp",
+    "ptls_mi355x_quiclb_batch",
+    "ptls_mi355x_quiclb_transform",
     "ptls_mi355x_encrypt",
     "ptls_mi355x_decrypt",
     "ptls_mi355x_encrypt_block",
@@ -91,6 +94,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.ptls_mi355x_decrypt.argtypes = [vp, sz, vp, vp, sz, u64, vp, sz]
     lib.ptls_mi355x_decrypt.restype = sz
     lib.ptls_mi355x_encrypt_block.argtypes = [vp, sz, vp, vp]
+    lib.ptls_mi355x_quiclb_batch.argtypes = [vp, vp, sz, vp, vp, vp]
+    lib.ptls_mi355x_quiclb_transform.argtypes = [vp, sz, vp, vp, sz, ci]
     lib.ptls_mi355x_last_error.restype = ctypes.c_char_p
     _lib = lib
     return lib
@@ -213,6 +218,12 @@ def seal_batch_hp(ks: Keyset, recs_ptr: int, nrecs: int, in_ptr: int, aad_ptr: i
         raise _err("ptls_mi355x_seal_batch_hp")
 
 
+def quiclb_batch(ks: Keyset, cids_ptr: int, n: int, in_ptr: int, out_ptr: int, stream: int = 0) -> None:
+    """QUIC-LB CID encryption / decryption (CID_DTYPE entries, AES-128 keyset); device pointers."""
+    if load_library().ptls_mi355x_quiclb_batch(ks.handle, cids_ptr, n, in_ptr, out_ptr, stream or None) != 0:
+        raise _err("ptls_mi355x_quiclb_batch")
+
+
 # ------------------------------------------------------------------------------------------------ picotls mirror
 
 
@@ -300,6 +311,29 @@ class CtrCipher:
         out = bytearray(16)
         if load_library().ptls_mi355x_encrypt_block(self.ks.handle, 0, _buf(out), _buf(bytes(iv16))) != 0:
             raise _err("ptls_mi355x_encrypt_block")
+        return bytes(out)
+
+
+class QuicLbCipher:
+    """Mirror of ptls_cipher_new(&ptls_mi355x_quiclb, is_enc, key) + ptls_cipher_encrypt (t/quiclb.c:36-45): the QUIC-LB
+    CID cipher of lib/quiclb-impl.h, one CID of 7..19 bytes per call."""
+
+    key_size = 16
+    block_size = 8  # PTLS_QUICLB_DEFAULT_BLOCK_SIZE, include/picotls.h:119-122
+
+    def __init__(self, is_enc: bool, key: bytes):
+        if len(key) != 16:
+            raise ValueError("QUIC-LB keys are 16 bytes (PTLS_QUICLB_KEY_SIZE)")
+        self.is_enc = is_enc
+        self.ks = Keyset(key, bytes(12), 16)
+
+    def encrypt(self, data: bytes) -> bytes:
+        if not QUICLB_MIN_LEN <= len(data) <= QUICLB_MAX_LEN:
+            raise ValueError("QUIC-LB transforms 7..19 bytes")
+        out = bytearray(len(data))
+        if load_library().ptls_mi355x_quiclb_transform(self.ks.handle, 0, _buf(out), _buf(bytes(data)), len(data),
+                                                       1 if self.is_enc else 0) != 0:
+            raise _err("ptls_mi355x_quiclb_transform")
         return bytes(out)
 
 

@@ -41,6 +41,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 __attribute__((aligned(1))) u32x4_u;
 
 static_assert(sizeof(ptls_mi355x_record_t) == PTLS_MI355X_RECORD_SIZE, "record descriptor must be 40 bytes");
+static_assert(sizeof(ptls_mi355x_cid_t) == 24, "CID descriptor must be 24 bytes");
 
 // ------------------------------------------------------------------------------------------------ constants
 
@@ -1295,6 +1296,78 @@ __global__ __launch_bounds__(256) void hp_kernel(const KeyEntry *keys, u32 nkeys
     }
 }
 
+// QUIC-LB connection-ID cipher (lib/quiclb-impl.h:100-162, behind ptls_fusion_quiclb lib/fusion.c:2186-2233): a 4-round
+// Feistel network over the two halves of a 7..19-byte CID, each round X ^ AES-ECB((Y & mask) | len_pass) with
+// len_pass = {0 x 14, len, round} (:134-135, :47-70). One thread per CID; blocks are LE words (byte i of the block in
+// word i/4). The middle byte of an odd-length CID belongs to both halves, split by nibble masks (:107-125).
+template <int NR>
+__device__ __forceinline__ u32x4 quiclb_f(const lds_u8 *lds, u32 laneoff, const u32 (*rk)[4], u32x4 y, u32x4 m, u32 len, u32 rnd)
+{
+    u32 s0 = (y[0] & m[0]) ^ rk[0][0], s1 = (y[1] & m[1]) ^ rk[0][1], s2 = (y[2] & m[2]) ^ rk[0][2];
+    u32 s3 = ((y[3] & m[3]) | len << 16 | rnd << 24) ^ rk[0][3];
+    aes_encrypt_tt<NR>(lds, laneoff, rk, s0, s1, s2, s3);
+    return u32x4{s0, s1, s2, s3};
+}
+
+__device__ __forceinline__ void set_byte(u32x4 &v, u32 i, u32 b) { v[i >> 2] |= (b & 0xffu) << (8 * (i & 3)); }
+__device__ __forceinline__ u32 get_byte(const u32x4 &v, u32 i) { return (v[i >> 2] >> (8 * (i & 3))) & 0xffu; }
+
+template <int NR>
+__global__ __launch_bounds__(256) void quiclb_kernel(const KeyEntry *keys, u32 nkeys, const ptls_mi355x_cid_t *cids,
+                                                     const uint8_t *in, uint8_t *out, u64 n)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    lds_u8 *lds = (lds_u8 *)smem;
+    check_lds_base(smem);
+    build_aes_tables(lds);
+    __syncthreads();
+    const u32 laneoff = (threadIdx.x & 31) * 4;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        const ptls_mi355x_cid_t c = cids[i];
+        const u32 L = c.len;
+        if (c.key_idx >= nkeys || L < PTLS_MI355X_QUICLB_MIN_LEN || L > PTLS_MI355X_QUICLB_MAX_LEN)
+            continue;  // invalid entries are not written
+        const KeyEntry *k = keys + c.key_idx;
+        u32 rk[NR + 1][4];
+        for (int r = 0; r <= NR; ++r)
+            for (int w = 0; w < 4; ++w)
+                rk[r][w] = k->rk[r][w];
+        const u32 half = L / 2, odd = L & 1, hl = half + odd;  // bytes per side: (L + 1) / 2
+        // masks (:107-125): left keeps bytes [0, half) and the high nibble of the middle byte; right keeps its low nibble
+        // (byte 0) and the bytes after it
+        u32x4 ml = {0, 0, 0, 0}, mr = {0, 0, 0, 0};
+        for (u32 b = 0; b < half; ++b)
+            set_byte(ml, b, 0xff), set_byte(mr, b + odd, 0xff);
+        if (odd)
+            set_byte(ml, half, 0xf0), set_byte(mr, 0, 0x0f);
+        // split (:72-84): l = in[0, hl), r = in[half, half + hl), zero padded
+        const uint8_t *src = in + c.in_off;
+        u32x4 a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
+        for (u32 t = 0; t < hl; ++t)
+            set_byte(a, t, src[t]), set_byte(b, t, src[half + t]);
+        u32x4 l, r;
+        if (c.encrypt) {  // (:149-154) l0 = a, r0 = b
+            const u32x4 r1 = b ^ quiclb_f<NR>(lds, laneoff, rk, a, ml, L, 1);
+            const u32x4 l1 = a ^ quiclb_f<NR>(lds, laneoff, rk, r1, mr, L, 2);
+            r = r1 ^ quiclb_f<NR>(lds, laneoff, rk, l1, ml, L, 3);
+            l = l1 ^ quiclb_f<NR>(lds, laneoff, rk, r, mr, L, 4);
+        } else {  // (:155-161) l2 = a, r2 = b
+            const u32x4 l1 = a ^ quiclb_f<NR>(lds, laneoff, rk, b, mr, L, 4);
+            const u32x4 r1 = b ^ quiclb_f<NR>(lds, laneoff, rk, l1, ml, L, 3);
+            l = l1 ^ quiclb_f<NR>(lds, laneoff, rk, r1, mr, L, 2);
+            r = r1 ^ quiclb_f<NR>(lds, laneoff, rk, l, ml, L, 1);
+        }
+        // merge (:86-100)
+        uint8_t *dst = out + c.out_off;
+        for (u32 t = 0; t < half; ++t)
+            dst[t] = (uint8_t)get_byte(l, t);
+        if (odd)
+            dst[half] = (uint8_t)((get_byte(l, half) & 0xf0u) | (get_byte(r, 0) & 0x0fu));
+        for (u32 t = 0; t < half; ++t)
+            dst[half + odd + t] = (uint8_t)get_byte(r, t + odd);
+    }
+}
+
 // After opening framed TLS records: outer header check, then the receive-side padding strip of lib/picotls.c:5960-5968
 // (the inner content type is the last non-zero plaintext byte; an all-zero plaintext, or an empty alert / handshake
 // record, is an unexpected message). One thread per record; ok[i] becomes 1 only for status 0.
@@ -1380,6 +1453,7 @@ static int engine_init_attrs(void)
     HIP_TRY(hipFuncSetAttribute((const void *)ecb_kernel<14>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
     HIP_TRY(hipFuncSetAttribute((const void *)hp_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
     HIP_TRY(hipFuncSetAttribute((const void *)hp_kernel<14>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
+    HIP_TRY(hipFuncSetAttribute((const void *)quiclb_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
     done = 1;
     return 0;
 }
@@ -1641,6 +1715,41 @@ int ptls_mi355x_seal_batch_hp(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record
     if (launch_batch(ks, false, recs, nrecs, in, aad, out, NULL, stream) != 0)
         return -1;
     return ptls_mi355x_hp_mask_batch(hp_ks, hp, nrecs, out, masks, stream);
+}
+
+int ptls_mi355x_quiclb_batch(ptls_mi355x_keyset_t *ks, const ptls_mi355x_cid_t *cids, size_t n, const void *in, void *out,
+                             void *stream)
+{
+    if (ks == NULL || (n != 0 && (cids == NULL || in == NULL || out == NULL)))
+        return fail("%s", "quiclb: invalid arguments");
+    if (ks->key_size != 16)
+        return fail("%s", "quiclb: the QUIC-LB cipher is keyed with AES-128 (PTLS_QUICLB_KEY_SIZE)");
+    if (n == 0)
+        return 0;
+    u64 grid = (n + 255) / 256;
+    if (grid > (u64)ks->ncu * 4)
+        grid = (u64)ks->ncu * 4;
+    quiclb_kernel<10><<<(unsigned)grid, 256, LDS_AES_BYTES, (hipStream_t)stream>>>(ks->d_keys, (u32)ks->nkeys, cids,
+                                                                                    (const uint8_t *)in, (uint8_t *)out, n);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int ptls_mi355x_quiclb_transform(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const void *input, size_t len, int encrypt)
+{
+    if (ks == NULL || key_idx >= ks->nkeys || output == NULL || input == NULL || len < PTLS_MI355X_QUICLB_MIN_LEN ||
+        len > PTLS_MI355X_QUICLB_MAX_LEN)
+        return fail("%s", "quiclb_transform: invalid arguments");
+    uint8_t *d = NULL;
+    HIP_TRY(hipMalloc((void **)&d, 96));
+    const ptls_mi355x_cid_t c = {0, 32, (uint32_t)key_idx, (uint8_t)len, (uint8_t)(encrypt != 0), 0};
+    int ret = -1;
+    if (hipMemcpy(d, input, len, hipMemcpyHostToDevice) == hipSuccess && hipMemcpy(d + 64, &c, sizeof(c), hipMemcpyHostToDevice) == hipSuccess &&
+        ptls_mi355x_quiclb_batch(ks, (const ptls_mi355x_cid_t *)(d + 64), 1, d, d, NULL) == 0 &&
+        hipMemcpy(output, d + 32, len, hipMemcpyDeviceToHost) == hipSuccess)
+        ret = 0;
+    hipFree(d);
+    return ret;
 }
 
 int ptls_mi355x_encrypt_block(ptls_mi355x_keyset_t *ks, size_t key_idx, void *out, const void *in)

@@ -8,6 +8,7 @@
  *   aead_do_decrypt     lib/fusion.c:1154-1171  -> ptls_mi355x_decrypt (inlen < 16 -> SIZE_MAX)
  *   aesgcm_get/set_iv   lib/fusion.c:1173-1187
  *   ctr cipher          lib/fusion.c:1051-1101  (one 16-byte AES-CTR block per init, for QUIC header protection)
+ *   quiclb cipher       lib/fusion.c:2186-2233  (QUIC-LB CID encryption, lib/quiclb-impl.h)
  * Unlike fusion, do_encrypt_v (TLS over TCP) is implemented: the iovecs are gathered and sealed as one record.
  */
 #include <assert.h>
@@ -178,6 +179,50 @@ static int aes256gcm_setup(ptls_aead_context_t *ctx, int is_enc, const void *key
 {
     return aesgcm_setup(ctx, is_enc, key, iv, PTLS_AES256_KEY_SIZE);
 }
+
+/* ------------------------------------------------------------------ QUIC-LB CID cipher (lib/fusion.c:2186-2233) */
+
+struct mi355x_quiclb_context {
+    ptls_cipher_context_t super;
+    ptls_mi355x_keyset_t *ks;
+    int is_enc;
+};
+
+static void quiclb_dispose(ptls_cipher_context_t *_ctx)
+{
+    struct mi355x_quiclb_context *ctx = (struct mi355x_quiclb_context *)_ctx;
+    ptls_mi355x_keyset_free(ctx->ks);
+}
+
+static void quiclb_init(ptls_cipher_context_t *ctx, const void *iv)
+{
+    /* no-op, as picotls_quiclb_do_init (lib/quiclb-impl.h:102-105) */
+}
+
+static void quiclb_transform(ptls_cipher_context_t *_ctx, void *output, const void *input, size_t len)
+{
+    struct mi355x_quiclb_context *ctx = (struct mi355x_quiclb_context *)_ctx;
+    /* the reference asserts PTLS_QUICLB_MIN_BLOCK_SIZE <= len <= PTLS_QUICLB_MAX_BLOCK_SIZE (lib/quiclb-impl.h:127) */
+    int ret = ptls_mi355x_quiclb_transform(ctx->ks, 0, output, input, len, ctx->is_enc);
+    assert(ret == 0 && "QUIC-LB: len out of range or MI355X engine failure");
+    (void)ret;
+}
+
+static int quiclb_setup(ptls_cipher_context_t *_ctx, int is_enc, const void *key)
+{
+    struct mi355x_quiclb_context *ctx = (struct mi355x_quiclb_context *)_ctx;
+    static const uint8_t zero_iv[PTLS_AESGCM_IV_SIZE] = {0};
+    if ((ctx->ks = ptls_mi355x_keyset_new(key, zero_iv, 1, PTLS_QUICLB_KEY_SIZE)) == NULL)
+        return PTLS_ERROR_LIBRARY;
+    ctx->super.do_dispose = quiclb_dispose;
+    ctx->super.do_init = quiclb_init;
+    ctx->super.do_transform = quiclb_transform;
+    ctx->is_enc = is_enc;
+    return 0;
+}
+
+ptls_cipher_algorithm_t ptls_mi355x_quiclb = {"QUICLB", PTLS_QUICLB_KEY_SIZE, PTLS_QUICLB_DEFAULT_BLOCK_SIZE, 0,
+                                              sizeof(struct mi355x_quiclb_context), quiclb_setup};
 
 ptls_mi355x_keyset_t *ptls_mi355x_aead_get_keyset(ptls_aead_context_t *ctx)
 {

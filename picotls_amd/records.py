@@ -28,6 +28,12 @@ assert RECORD_DTYPE.itemsize == 40
 HP_DTYPE = np.dtype([("sample_off", "<u8"), ("key_idx", "<u4"), ("reserved", "<u4")])
 assert HP_DTYPE.itemsize == 16
 
+# ptls_mi355x_cid_t (include/picotls/mi355x.h): one QUIC-LB connection ID to encrypt / decrypt
+CID_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("key_idx", "<u4"), ("len", "u1"), ("encrypt", "u1"),
+                      ("reserved", "<u2")])
+assert CID_DTYPE.itemsize == 24
+QUICLB_MIN_LEN, QUICLB_MAX_LEN = 7, 19  # PTLS_QUICLB_{MIN,MAX}_BLOCK_SIZE, include/picotls.h:117-118
+
 # ptls_mi355x_tls_result_t: per-record outcome of ptls_mi355x_open_tls_records
 TLS_RESULT_DTYPE = np.dtype([("plain_len", "<u4"), ("content_type", "u1"), ("status", "u1"), ("reserved", "<u2")])
 assert TLS_RESULT_DTYPE.itemsize == 8

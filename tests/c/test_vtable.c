@@ -154,6 +154,41 @@ static void ecb_kat(void)
     ptls_cipher_free(c);
 }
 
+static void quiclb_test(void)
+{
+    /* t/quiclb.c:25-46 on ptls_mi355x_quiclb, then random CIDs against ptls_fusion_quiclb in both directions */
+    static const uint8_t key[16] = {0xfd, 0xf7, 0x26, 0xa9, 0x89, 0x3e, 0xc0, 0x5c, 0x06, 0x32, 0xd3, 0x95, 0x66, 0x80, 0xba, 0xf0},
+                         pt[19] = {0x31, 0x44, 0x1a, 0x9c, 0x69, 0xc2, 0x75}, ct7[7] = {0x67, 0x94, 0x7d, 0x29, 0xbe, 0x05, 0x4a};
+    OK(strcmp(ptls_mi355x_quiclb.name, ptls_fusion_quiclb.name) == 0 && ptls_mi355x_quiclb.key_size == ptls_fusion_quiclb.key_size &&
+           ptls_mi355x_quiclb.block_size == ptls_fusion_quiclb.block_size && ptls_mi355x_quiclb.iv_size == 0,
+       "quiclb algorithm fields match fusion");
+    for (size_t len = PTLS_QUICLB_MIN_BLOCK_SIZE; len <= PTLS_QUICLB_MAX_BLOCK_SIZE; ++len) {
+        uint8_t tmp[19];
+        ptls_cipher_context_t *c = ptls_cipher_new(&ptls_mi355x_quiclb, 1, key);
+        ptls_cipher_encrypt(c, tmp, pt, len);
+        ptls_cipher_free(c);
+        if (len == sizeof(ct7))
+            OK(memcmp(tmp, ct7, len) == 0, "quiclb draft vector");
+        c = ptls_cipher_new(&ptls_mi355x_quiclb, 0, key);
+        ptls_cipher_encrypt(c, tmp, tmp, len); /* in place, as t/quiclb.c:43 */
+        ptls_cipher_free(c);
+        OK(memcmp(tmp, pt, len) == 0, "quiclb round trip");
+    }
+    for (int i = 0; i < 40; ++i) {
+        uint8_t k[16], in[19], a[19], b[19];
+        size_t len = PTLS_QUICLB_MIN_BLOCK_SIZE + rnd8() % 13;
+        int enc = i & 1;
+        rnd(k, sizeof(k));
+        rnd(in, len);
+        ptls_cipher_context_t *c1 = ptls_cipher_new(&ptls_mi355x_quiclb, enc, k), *c2 = ptls_cipher_new(&ptls_fusion_quiclb, enc, k);
+        ptls_cipher_encrypt(c1, a, in, len);
+        ptls_cipher_encrypt(c2, b, in, len);
+        OK(memcmp(a, b, len) == 0, "quiclb == fusion");
+        ptls_cipher_free(c1);
+        ptls_cipher_free(c2);
+    }
+}
+
 int main(void)
 {
     if (!ptls_fusion_is_supported_by_cpu()) {
@@ -174,6 +209,7 @@ int main(void)
     encrypt_v_test(&ptls_mi355x_aes256gcm, &ptls_fusion_aes256gcm);
     supp_test(&ptls_mi355x_aes128gcm, &ptls_mi355x_aes128ctr, &ptls_fusion_aes128gcm, &ptls_fusion_aes128ctr);
     supp_test(&ptls_mi355x_aes256gcm, &ptls_mi355x_aes256ctr, &ptls_fusion_aes256gcm, &ptls_fusion_aes256ctr);
+    quiclb_test();
     printf("1..%d\n# %d failed\n", ntest, nfail);
     return nfail == 0 ? 0 : 1;
 }

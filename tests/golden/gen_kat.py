@@ -19,6 +19,8 @@ Vector kinds
             AES-256-GCM is pinned by vectors from lib/fusion.c itself (gen_golden.py -> fusion_vectors.json).
   hp_mask   the QUIC header-protection mask fused into seal (supp), t/fusion.c:290-344 second pass:
             mask = AES-ECB(hp_key = 01*16, sample = sealed[2:18])
+  quiclb    the QUIC-LB CID cipher vector of t/quiclb.c:27-30 (7-byte CID; the plaintext array is 19 bytes, zero
+            padded, and every prefix of length 7..19 must round-trip)
 """
 import json
 import os
@@ -123,6 +125,12 @@ kat = {
          "ct": "42831ec2217774244b7221b784d0d49ce3aa212f2c02a4e035c17e2329aca12e21d514b25466931c7d8f6a5aac84aa051ba30b396a0aac973d58e091",
          "tag": "5bc94fbc3221a5db94fae95ae7121a47"},
     ],
+    "quiclb": {
+        "src": "t/quiclb.c:27-30 (draft-ietf-quic-load-balancers-21 vector; round trip for every length 7..19 at :34-46)",
+        "key": "fdf726a9893ec05c0632d3956680baf0",
+        "pt19": "31441a9c69c275" + "00" * 12,
+        "ct7": "67947d29be054a",
+    },
 }
 
 def main():

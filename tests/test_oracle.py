@@ -144,3 +144,52 @@ def test_batch_helpers_match_fusion(oracle):
     for i in range(b.n):
         s, ln = int(b.seal["in_off"][i]), int(lens[i])
         assert np.array_equal(back_o[s:s + ln], pt[s:s + ln])
+
+
+# ------------------------------------------------------------------------------------------------ QUIC-LB (lib/quiclb-impl.h)
+
+
+def _quiclb_vectors():
+    import json
+
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "quiclb_vectors.json")) as f:
+        return json.load(f)["vectors"]
+
+
+def test_quiclb_kat(oracle, kat):
+    # t/quiclb.c:27-46: the draft vector at len 7, and a round trip for every length 7..19
+    v = kat["quiclb"]
+    key, pt19 = bytes.fromhex(v["key"]), bytes.fromhex(v["pt19"])
+    for ln in range(7, 20):
+        ct = oracle.quiclb(key, pt19[:ln], True)
+        if ln == 7:
+            assert ct.hex() == v["ct7"]
+        assert oracle.quiclb(key, ct, False) == pt19[:ln]
+    with pytest.raises(ValueError):
+        oracle.quiclb(key, bytes(6), True)
+    with pytest.raises(ValueError):
+        oracle.quiclb(key, bytes(20), True)
+
+
+def test_quiclb_fusion_vectors(oracle):
+    # tests/golden/quiclb_vectors.json: written by ptls_fusion_quiclb (tests/golden/gen_quiclb.py)
+    from vectors import splitmix_bytes
+
+    vecs = _quiclb_vectors()
+    assert len(vecs) == 78 and {v["len"] for v in vecs} == set(range(7, 20))
+    for v in vecs:
+        blob = splitmix_bytes(v["seed"], 16 + v["len"])
+        key, pt = blob[:16], blob[16:]
+        assert oracle.quiclb(key, pt, True).hex() == v["ct"], v["seed"]
+        assert oracle.quiclb(key, bytes.fromhex(v["ct"]), False) == pt
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="oracle/_ref/libfusion_ref.so not built")
+def test_quiclb_oracle_vs_fusion_random(oracle):
+    ref = FusionRef()
+    rng = np.random.default_rng(31337)
+    for _ in range(400):
+        key, ln = rng.bytes(16), int(rng.integers(7, 20))
+        data = rng.bytes(ln)
+        for enc in (True, False):
+            assert oracle.quiclb(key, data, enc) == ref.quiclb(key, data, enc), (ln, enc)
