@@ -155,6 +155,25 @@ int ptls_mi355x_open_tls_records(ptls_mi355x_keyset_t *ks, const ptls_mi355x_rec
                                  void *out, uint8_t *ok, ptls_mi355x_tls_result_t *results, void *stream);
 
 /**
+ * TLS 1.2 AES-GCM record protection, batched (the tls12 branch of buffer_push_encrypted_records lib/picotls.c:779-799
+ * and handle_input_tls12 :6019-6060; the record IV sizes {4, 8} of ptls_non_temporal_aes{128,256}gcm,
+ * lib/fusion.c:2159-2184). The keyset's static IV is the 4-byte fixed IV followed by 8 zero bytes; recs[i].seq is the
+ * record sequence number that goes into the 13-byte AAD BE64(seq) || type || 3 || 3 || BE16(len) (build_tls12_aad
+ * :753-762); the GCM nonce is fixed IV || the record's 8-byte explicit nonce (ptls_aead_encrypt with seq = record IV).
+ *
+ * seal_tls12_records: in + in_off holds the explicit nonce (8 bytes, big endian, as it goes on the wire) followed by
+ * recs[i].len payload bytes; the content type is recs[i].flags & 0xff. Writes the wire record at out + out_off:
+ * header {type, 3, 3, BE16(len + 24)} || explicit nonce || ciphertext || tag (len + 37 bytes).
+ * open_tls12_records: in + in_off is the wire record, recs[i].len = header length field - 24; the plaintext goes to
+ * out + out_off. ok[i] = 1 only if the tag verifies and the header is {type, 3, 3, BE16(len + 24)}; results (may be
+ * NULL) gets plain_len = len, the record's content type and a status.
+ */
+int ptls_mi355x_seal_tls12_records(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
+                                   void *out, void *stream);
+int ptls_mi355x_open_tls12_records(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
+                                   void *out, uint8_t *ok, ptls_mi355x_tls_result_t *results, void *stream);
+
+/**
  * QUIC header protection, batched. One entry per packet: the 16-byte sample at base + sample_off and the index of the
  * header-protection key in hp_ks. mask[i] (16 bytes at masks + 16 i) = AES-ECB(hp key, sample), i.e. the first
  * keystream block of the AES-CTR cipher initialised with the sample, which is what ptls_aead_encrypt_s writes into

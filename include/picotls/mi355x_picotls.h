@@ -20,6 +20,9 @@ extern ptls_cipher_algorithm_t ptls_mi355x_aes128ctr, ptls_mi355x_aes256ctr;
 /* QUIC-LB connection-ID cipher, the counterpart of ptls_fusion_quiclb (include/picotls/fusion.h:121, lib/fusion.c:2226-2233) */
 extern ptls_cipher_algorithm_t ptls_mi355x_quiclb;
 extern ptls_aead_algorithm_t ptls_mi355x_aes128gcm, ptls_mi355x_aes256gcm;
+/* TLS-1.2-capable variants (record IV sizes {4, 8}, non_temporal, align_bits 6): the counterparts of
+ * ptls_non_temporal_aes{128,256}gcm (include/picotls/fusion.h:117, lib/fusion.c:2159-2184) */
+extern ptls_aead_algorithm_t ptls_mi355x_non_temporal_aes128gcm, ptls_mi355x_non_temporal_aes256gcm;
 
 /**
  * Returns the engine keyset behind an AEAD context created from one of the algorithms above (key index 0), so that a

@@ -196,3 +196,48 @@ class FusionRef:
                                    _ptr(recs), len(recs), _ptr(in_arena), _ptr(aad_arena), _ptr(out_arena), _ptr(ok),
                                    nthreads, _ptr(cpu_arr), ctypes.byref(fails))
         return t, fails.value
+
+
+class Tls12Ref:
+    """ctypes front-end of picotls' own TLS 1.2 record layer over fusion's non-temporal AEADs
+    (oracle/_ref/libtls12_ref.so, oracle/tls12_harness.c): ptls_import of ptls_build_tls12_export_params, then
+    ptls_send (server) / ptls_receive (client)."""
+
+    def __init__(self):
+        path = os.path.join(REF_DIR, "libtls12_ref.so")
+        if not os.path.exists(path):
+            build()
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: build it with `make -C oracle` where /root/reference exists")
+        lib = ctypes.CDLL(path)
+        vp, sz, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64
+        lib.ref_tls12_server_keys.argtypes = [sz, vp, vp, vp, vp]
+        lib.ref_tls12_send.argtypes = [sz, vp, vp, u64, vp, sz, vp, sz]
+        lib.ref_tls12_send.restype = sz
+        lib.ref_tls12_receive.argtypes = [sz, vp, vp, vp, sz, vp, sz]
+        lib.ref_tls12_receive.restype = ctypes.c_long
+        self.lib = lib
+
+    def server_keys(self, key_size: int, master_secret: bytes, randoms: bytes) -> tuple[bytes, bytes]:
+        """(server write key, 4-byte fixed IV) of the key block (lib/picotls.c:5308-5335)."""
+        key, iv = bytearray(key_size), bytearray(4)
+        if self.lib.ref_tls12_server_keys(key_size, _ptr(master_secret), _ptr(randoms), _ptr(key), _ptr(iv)) != 0:
+            raise RuntimeError("ptls_tls12_phash failed")
+        return bytes(key), bytes(iv)
+
+    def send(self, key_size: int, master_secret: bytes, randoms: bytes, record_iv: int, data: bytes) -> bytes:
+        """The server's wire records for `data` (sequence numbers from 1, explicit nonces from record_iv)."""
+        cap = len(data) + (len(data) // 16384 + 1) * 64
+        out = bytearray(cap)
+        n = self.lib.ref_tls12_send(key_size, _ptr(master_secret), _ptr(randoms), record_iv, _ptr(bytes(data)) if data else None,
+                                    len(data), _ptr(out), cap)
+        if n == 0:
+            raise RuntimeError("ptls_send failed")
+        return bytes(out[:n])
+
+    def receive(self, key_size: int, master_secret: bytes, randoms: bytes, wire: bytes):
+        """Plaintext of the server's records as the client decrypts them, or a negative picotls error code."""
+        out = bytearray(len(wire) + 1)
+        r = self.lib.ref_tls12_receive(key_size, _ptr(master_secret), _ptr(randoms), _ptr(bytes(wire)), len(wire), _ptr(out),
+                                       len(out))
+        return bytes(out[:r]) if r >= 0 else r

@@ -43,6 +43,8 @@ ABI_FUNCTIONS = (
     "ptls_mi355x_open_batch",
     "ptls_mi355x_seal_tls_records",
     "ptls_mi355x_open_tls_records",
+    "ptls_mi355x_seal_tls12_records",
+    "ptls_mi355x_open_tls12_records",
     "ptls_mi355x_ecb_batch",
     "ptls_mi355x_hp_mask_batch",
     "ptls_mi355x_seal_batch_hp",
@@ -89,6 +91,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.ptls_mi355x_hp_mask_batch.argtypes = [vp, vp, sz, vp, vp, vp]
     lib.ptls_mi355x_seal_tls_records.argtypes = [vp, vp, sz, vp, vp, vp]
     lib.ptls_mi355x_open_tls_records.argtypes = [vp, vp, sz, vp, vp, vp, vp, vp]
+    lib.ptls_mi355x_seal_tls12_records.argtypes = [vp, vp, sz, vp, vp, vp]
+    lib.ptls_mi355x_open_tls12_records.argtypes = [vp, vp, sz, vp, vp, vp, vp, vp]
     lib.ptls_mi355x_seal_batch_hp.argtypes = [vp, vp, sz, vp, vp, vp, vp, vp, vp, vp]
     lib.ptls_mi355x_encrypt.argtypes = [vp, sz, vp, vp, sz, u64, vp, sz]
     lib.ptls_mi355x_decrypt.argtypes = [vp, sz, vp, vp, sz, u64, vp, sz]
@@ -202,6 +206,20 @@ def open_tls_records(ks: Keyset, recs_ptr: int, nrecs: int, in_ptr: int, out_ptr
     if load_library().ptls_mi355x_open_tls_records(ks.handle, recs_ptr, nrecs, in_ptr, out_ptr, ok_ptr, results_ptr or None,
                                                    stream or None) != 0:
         raise _err("ptls_mi355x_open_tls_records")
+
+
+def seal_tls12_records(ks: Keyset, recs_ptr: int, nrecs: int, in_ptr: int, out_ptr: int, stream: int = 0) -> None:
+    """TLS 1.2 wire records (header || explicit nonce || ciphertext || tag) from explicit nonce || payload; device pointers."""
+    if load_library().ptls_mi355x_seal_tls12_records(ks.handle, recs_ptr, nrecs, in_ptr, out_ptr, stream or None) != 0:
+        raise _err("ptls_mi355x_seal_tls12_records")
+
+
+def open_tls12_records(ks: Keyset, recs_ptr: int, nrecs: int, in_ptr: int, out_ptr: int, ok_ptr: int, results_ptr: int = 0,
+                       stream: int = 0) -> None:
+    """Opens TLS 1.2 wire records (TLS_RESULT_DTYPE results: content type, length, status); device pointers."""
+    if load_library().ptls_mi355x_open_tls12_records(ks.handle, recs_ptr, nrecs, in_ptr, out_ptr, ok_ptr, results_ptr or None,
+                                                     stream or None) != 0:
+        raise _err("ptls_mi355x_open_tls12_records")
 
 
 def hp_mask_batch(hp_ks: Keyset, hp_ptr: int, n: int, base_ptr: int, masks_ptr: int, stream: int = 0) -> None:

@@ -632,16 +632,36 @@ struct BatchArgs {
 // record's len payload bytes plus the inner content type (flags & 0xff); the wire record at out_off is the 5-byte
 // header {23, 3, 3, BE16(len + 17)} (also the AAD), the ciphertext, the tag. Open: the wire record at in_off is header
 // (the AAD, as received), len ciphertext bytes (inner type and padding included), tag; the plaintext goes to out_off.
+//
+// TLS 1.2 AES-GCM record framing (FRAME = 2; buffer_push_encrypted_records lib/picotls.c:779-799, handle_input_tls12
+// :6019-6060, build_tls12_aad :753-762). The wire record is header {type, 3, 3, BE16(8 + len + 16)} || explicit nonce
+// (8 bytes, big endian: the record IV, tls12.record_iv_size) || ciphertext || tag. GCM nonce = static IV ^ (0^32 ||
+// explicit nonce), i.e. ptls_aead_encrypt(..., seq = record IV), and the 13-byte AAD is BE64(seq) || type || 3 || 3 ||
+// BE16(len) with seq the record sequence number. Seal: in_off holds the explicit nonce followed by the len payload
+// bytes; the type is flags & 0xff. Open: the wire record is at in_off; the AAD takes the header's type.
 #define TLS_HEADER_SIZE 5
+#define TLS12_RECORD_IV_SIZE 8
+#define TLS12_AAD_SIZE 13
 template <bool OPEN, int FRAME>
 __device__ __forceinline__ u32 gcm_text_len(const ptls_mi355x_record_t &r)
 {
-    return FRAME && !OPEN ? r.len + 1 : r.len;
+    return FRAME == 1 && !OPEN ? r.len + 1 : r.len;
 }
 template <bool OPEN, int FRAME>
 __device__ __forceinline__ u32 gcm_aad_len(const ptls_mi355x_record_t &r)
 {
-    return FRAME ? (u32)TLS_HEADER_SIZE : (u32)r.aad_len;
+    return FRAME == 1 ? (u32)TLS_HEADER_SIZE : FRAME == 2 ? (u32)TLS12_AAD_SIZE : (u32)r.aad_len;
+}
+// bytes in front of the GCM text in the input / output record
+template <bool OPEN, int FRAME>
+__device__ __forceinline__ constexpr u32 frame_in_skip()
+{
+    return FRAME == 1 ? (OPEN ? TLS_HEADER_SIZE : 0) : FRAME == 2 ? (OPEN ? TLS_HEADER_SIZE : 0) + TLS12_RECORD_IV_SIZE : 0;
+}
+template <bool OPEN, int FRAME>
+__device__ __forceinline__ constexpr u32 frame_out_skip()
+{
+    return FRAME && !OPEN ? TLS_HEADER_SIZE + (FRAME == 2 ? TLS12_RECORD_IV_SIZE : 0) : 0;
 }
 // G-lane steps of a record's GHASH stream [pad | AAD | text | length]
 template <bool OPEN, int FRAME>
@@ -663,7 +683,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                                             u32x4 &ek0, bool finish, u64 rec)
 {
     constexpr int G = ENGINE_G;
-    constexpr bool SEAL_FRAME = FRAME && !OPEN, OPEN_FRAME = FRAME && OPEN;
+    constexpr bool SEAL_FRAME = FRAME == 1 && !OPEN, OPEN_FRAME = FRAME == 1 && OPEN, TLS12 = FRAME == 2;
     const u32 L = gcm_text_len<OPEN, FRAME>(r), A = gcm_aad_len<OPEN, FRAME>(r);
     // bytes of text readable at src (a framed seal reads len payload bytes; its last text byte is the content type)
     const u32 Lsrc = SEAL_FRAME ? L - 1 : L;
@@ -677,11 +697,19 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     for (int off = 32; off >= 1; off >>= 1)
         Smax = max(Smax, (u32)__shfl_xor((int)Smax, off, 64));
 
+    // nonce = iv ^ (0^32 || BE64(seq)) (lib/picotls.c:6587-6601); TLS 1.2 takes the explicit nonce of the record in
+    // place of seq, read as stored (big endian), so its two words need no swap
+    u32 nw1 = bswap32((u32)(r.seq >> 32)), nw2 = bswap32((u32)r.seq);
+    if (TLS12) {
+        const uint8_t *e = args.in + r.in_off + (OPEN ? TLS_HEADER_SIZE : 0);
+        nw1 = *(const u32 __attribute__((aligned(1))) *)e;
+        nw2 = *(const u32 __attribute__((aligned(1))) *)(e + 4);
+    }
     const u32 n0 = iv0 ^ rk[0][0];
-    const u32 n1 = iv1 ^ bswap32((u32)(r.seq >> 32)) ^ rk[0][1];
-    const u32 n2 = iv2 ^ bswap32((u32)r.seq) ^ rk[0][2];
-    const uint8_t *src = args.in + r.in_off + (OPEN_FRAME ? TLS_HEADER_SIZE : 0);
-    uint8_t *dst = args.out + r.out_off + (SEAL_FRAME ? TLS_HEADER_SIZE : 0);
+    const u32 n1 = iv1 ^ nw1 ^ rk[0][1];
+    const u32 n2 = iv2 ^ nw2 ^ rk[0][2];
+    const uint8_t *src = args.in + r.in_off + frame_in_skip<OPEN, FRAME>();
+    uint8_t *dst = args.out + r.out_off + frame_out_skip<OPEN, FRAME>();
     const uint8_t *aadp = OPEN_FRAME ? args.in + r.in_off : args.aad + r.aad_off;
 
     acc = u32x4{0, 0, 0, 0};
@@ -779,6 +807,16 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                     const u32 wl = L + 16;
                     X = u32x4{0x00030317u | ((wl >> 8) & 0xffu) << 24, wl & 0xffu, 0, 0};
                     store_partial(args.out + r.out_off, X, TLS_HEADER_SIZE);
+                } else if (TLS12) {  // AAD = BE64(seq) || type || 3 || 3 || BE16(len) (build_tls12_aad)
+                    const u32 type = OPEN ? (u32)args.in[r.in_off] : (r.flags & 0xffu);
+                    X = u32x4{bswap32((u32)(r.seq >> 32)), bswap32((u32)r.seq), type | 0x030300u | ((L >> 8) & 0xffu) << 24,
+                              L & 0xffu};
+                    if (!OPEN) {  // the wire header and the explicit nonce
+                        const u32 wl = TLS12_RECORD_IV_SIZE + L + 16;
+                        const u32x4 h = {type | 0x030300u | ((wl >> 8) & 0xffu) << 24, (wl & 0xffu) | nw1 << 8,
+                                         nw1 >> 24 | nw2 << 8, nw2 >> 24};
+                        store_partial(args.out + r.out_off, h, TLS_HEADER_SIZE + TLS12_RECORD_IV_SIZE);
+                    }
                 } else {
                     const u32 rem = A - 16u * (u32)logical;
                     const uint8_t *ap = aadp + 16u * (u32)logical;
@@ -1184,12 +1222,12 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                     const u32x4 tag = g ^ s_ek0[ri];
                     if (j != G - 1) {
                     } else if (OPEN) {
-                        const u32x4 rt = *(const u32x4_u *)(args.in + r.in_off + (FRAME ? TLS_HEADER_SIZE : 0) +
+                        const u32x4 rt = *(const u32x4_u *)(args.in + r.in_off + frame_in_skip<OPEN, FRAME>() +
                                                             gcm_text_len<OPEN, FRAME>(r));
                         const u32x4 d = rt ^ tag;
                         args.ok[pos + ri] = (d[0] | d[1] | d[2] | d[3]) == 0;
                     } else {
-                        *(u32x4_u *)(args.out + r.out_off + (FRAME ? TLS_HEADER_SIZE : 0) + gcm_text_len<OPEN, FRAME>(r)) = tag;
+                        *(u32x4_u *)(args.out + r.out_off + frame_out_skip<OPEN, FRAME>() + gcm_text_len<OPEN, FRAME>(r)) = tag;
                     }
                 }
             }
@@ -1378,6 +1416,28 @@ __global__ __launch_bounds__(256) void tls_unpad_kernel(const ptls_mi355x_record
     }
 }
 
+// After opening TLS 1.2 records: the record header must be {type, 3, 3, BE16(8 + len + 16)} (parse_record /
+// handle_input_tls12, lib/picotls.c:6019-6045); TLS 1.2 has no inner content type or padding, so the content is the
+// whole plaintext and the type is the (authenticated) outer one. ok[i] becomes 1 only for status 0.
+__global__ __launch_bounds__(256) void tls12_check_kernel(const ptls_mi355x_record_t *recs, u64 n, const uint8_t *in, uint8_t *ok,
+                                                          ptls_mi355x_tls_result_t *res)
+{
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        const ptls_mi355x_record_t r = recs[i];
+        ptls_mi355x_tls_result_t o = {0, 0, 0, 0};
+        const uint8_t *h = in + r.in_off;
+        if (!ok[i])
+            o.status = PTLS_MI355X_TLS_BAD_MAC;
+        else if (h[1] != 3 || h[2] != 3 || ((u32)h[3] << 8 | h[4]) != r.len + TLS12_RECORD_IV_SIZE + 16)
+            o.status = PTLS_MI355X_TLS_BAD_HEADER;
+        o.content_type = h[0];
+        o.plain_len = o.status == 0 ? r.len : 0;
+        ok[i] = o.status == 0;
+        if (res != nullptr)
+            res[i] = o;
+    }
+}
+
 // ------------------------------------------------------------------------------------------------ host side
 
 static thread_local char g_err[256];
@@ -1424,6 +1484,10 @@ static int engine_init_attrs(void)
     CHUNKED_ATTR(10, true, 1);
     CHUNKED_ATTR(14, false, 1);
     CHUNKED_ATTR(14, true, 1);
+    CHUNKED_ATTR(10, false, 2);
+    CHUNKED_ATTR(10, true, 2);
+    CHUNKED_ATTR(14, false, 2);
+    CHUNKED_ATTR(14, true, 2);
 #undef CHUNKED_ATTR
     HIP_TRY(hipFuncSetAttribute((const void *)ecb_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
     HIP_TRY(hipFuncSetAttribute((const void *)ecb_kernel<14>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
@@ -1567,7 +1631,7 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
         grid = 1;
     hipStream_t s = (hipStream_t)stream;
 #define CHUNKED_LAUNCH(nr, op, frame) gcm_chunked_kernel<nr, op, frame><<<(unsigned)grid, ENGINE_WG, CLDS_ALLOC, s>>>(a)
-    if (frame) {
+    if (frame == 1) {
         if (ks->nr == 10) {
             if (open)
                 CHUNKED_LAUNCH(10, true, 1);
@@ -1578,6 +1642,18 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
                 CHUNKED_LAUNCH(14, true, 1);
             else
                 CHUNKED_LAUNCH(14, false, 1);
+        }
+    } else if (frame == 2) {
+        if (ks->nr == 10) {
+            if (open)
+                CHUNKED_LAUNCH(10, true, 2);
+            else
+                CHUNKED_LAUNCH(10, false, 2);
+        } else {
+            if (open)
+                CHUNKED_LAUNCH(14, true, 2);
+            else
+                CHUNKED_LAUNCH(14, false, 2);
         }
     } else if (use_chunked(ks)) {
         if (ks->nr == 10) {
@@ -1657,6 +1733,27 @@ int ptls_mi355x_open_tls_records(ptls_mi355x_keyset_t *ks, const ptls_mi355x_rec
         grid = (u64)ks->ncu * 4;
     tls_unpad_kernel<<<(unsigned)grid, 256, 0, (hipStream_t)stream>>>(recs, nrecs, (const uint8_t *)in, (const uint8_t *)out,
                                                                        ok, results);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int ptls_mi355x_seal_tls12_records(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
+                                   void *out, void *stream)
+{
+    return launch_batch(ks, false, recs, nrecs, in, NULL, out, NULL, stream, 2);
+}
+
+int ptls_mi355x_open_tls12_records(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
+                                   void *out, uint8_t *ok, ptls_mi355x_tls_result_t *results, void *stream)
+{
+    if (launch_batch(ks, true, recs, nrecs, in, NULL, out, ok, stream, 2) != 0)
+        return -1;
+    if (nrecs == 0)
+        return 0;
+    u64 grid = (nrecs + 255) / 256;
+    if (grid > (u64)ks->ncu * 4)
+        grid = (u64)ks->ncu * 4;
+    tls12_check_kernel<<<(unsigned)grid, 256, 0, (hipStream_t)stream>>>(recs, nrecs, (const uint8_t *)in, ok, results);
     HIP_TRY(hipGetLastError());
     return 0;
 }

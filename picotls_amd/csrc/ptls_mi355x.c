@@ -259,3 +259,35 @@ ptls_aead_algorithm_t ptls_mi355x_aes256gcm = {"AES256-GCM",
                                                0,
                                                sizeof(struct mi355x_aead_context),
                                                aes256gcm_setup};
+
+/* The TLS-1.2-capable objects, counterparts of ptls_non_temporal_aes{128,256}gcm (lib/fusion.c:2159-2184): same GCM
+ * callbacks, record IV sizes {4, 8} so that picotls' TLS 1.2 record layer (lib/picotls.c:779-799, :6019-6060) can use
+ * them, non_temporal = 1 and 64-byte buffer alignment as fusion declares (on the GPU these are hints only: records are
+ * staged through device memory either way). Unlike fusion's, both directions are available on every context. */
+#define MI355X_CACHE_LINE_ALIGN_BITS 6
+ptls_aead_algorithm_t ptls_mi355x_non_temporal_aes128gcm = {"AES128-GCM",
+                                                            PTLS_AESGCM_CONFIDENTIALITY_LIMIT,
+                                                            PTLS_AESGCM_INTEGRITY_LIMIT,
+                                                            &ptls_mi355x_aes128ctr,
+                                                            NULL,
+                                                            PTLS_AES128_KEY_SIZE,
+                                                            PTLS_AESGCM_IV_SIZE,
+                                                            PTLS_AESGCM_TAG_SIZE,
+                                                            {PTLS_TLS12_AESGCM_FIXED_IV_SIZE, PTLS_TLS12_AESGCM_RECORD_IV_SIZE},
+                                                            1,
+                                                            MI355X_CACHE_LINE_ALIGN_BITS,
+                                                            sizeof(struct mi355x_aead_context),
+                                                            aes128gcm_setup};
+ptls_aead_algorithm_t ptls_mi355x_non_temporal_aes256gcm = {"AES256-GCM",
+                                                            PTLS_AESGCM_CONFIDENTIALITY_LIMIT,
+                                                            PTLS_AESGCM_INTEGRITY_LIMIT,
+                                                            &ptls_mi355x_aes256ctr,
+                                                            NULL,
+                                                            PTLS_AES256_KEY_SIZE,
+                                                            PTLS_AESGCM_IV_SIZE,
+                                                            PTLS_AESGCM_TAG_SIZE,
+                                                            {PTLS_TLS12_AESGCM_FIXED_IV_SIZE, PTLS_TLS12_AESGCM_RECORD_IV_SIZE},
+                                                            1,
+                                                            MI355X_CACHE_LINE_ALIGN_BITS,
+                                                            sizeof(struct mi355x_aead_context),
+                                                            aes256gcm_setup};

@@ -9,6 +9,7 @@
 #include <string.h>
 #include "picotls.h"
 #include "picotls/fusion.h"
+#include "picotls/openssl.h"
 #include "picotls/mi355x_picotls.h"
 
 static int nfail, ntest;
@@ -189,6 +190,85 @@ static void quiclb_test(void)
     }
 }
 
+/* picotls' own TLS 1.2 record layer (ptls_build_tls12_export_params -> ptls_import -> ptls_send / ptls_receive,
+ * lib/picotls.c:779-799, :6019-6060) over the MI355X non-temporal objects vs fusion's (lib/fusion.c:2159-2184) */
+static ptls_t *tls12_import(ptls_cipher_suite_t *suite, int is_server, const uint8_t *ms, const uint8_t *randoms,
+                            ptls_context_t *ctx, ptls_cipher_suite_t **suites)
+{
+    suites[0] = suite;
+    suites[1] = NULL;
+    memset(ctx, 0, sizeof(*ctx));
+    ctx->random_bytes = ptls_openssl_random_bytes;
+    ctx->get_time = &ptls_get_time;
+    ctx->tls12_cipher_suites = suites;
+    ptls_buffer_t params;
+    ptls_buffer_init(&params, "", 0);
+    ptls_t *tls = NULL;
+    if (ptls_build_tls12_export_params(ctx, &params, is_server, 0, suite, ms, randoms, 0x1122334455667788, NULL,
+                                       ptls_iovec_init(NULL, 0)) == 0)
+        ptls_import(ctx, &tls, ptls_iovec_init(params.base, params.off));
+    ptls_buffer_dispose(&params);
+    return tls;
+}
+
+static void tls12_send(ptls_aead_algorithm_t *aead, ptls_hash_algorithm_t *hash, const uint8_t *ms, const uint8_t *randoms,
+                       const uint8_t *data, size_t len, ptls_buffer_t *out)
+{
+    ptls_context_t ctx;
+    ptls_cipher_suite_t suite = {hash == &ptls_openssl_sha384 ? 0xc030 : 0xc02f, aead, hash, "tls12"}, *suites[2];
+    ptls_t *tls = tls12_import(&suite, 1, ms, randoms, &ctx, suites);
+    OK(tls != NULL && ptls_send(tls, out, data, len) == 0, "tls12 send");
+    if (tls != NULL)
+        ptls_free(tls);
+}
+
+static int tls12_receive(ptls_aead_algorithm_t *aead, ptls_hash_algorithm_t *hash, const uint8_t *ms, const uint8_t *randoms,
+                         const uint8_t *wire, size_t len, ptls_buffer_t *out)
+{
+    ptls_context_t ctx;
+    ptls_cipher_suite_t suite = {hash == &ptls_openssl_sha384 ? 0xc030 : 0xc02f, aead, hash, "tls12"}, *suites[2];
+    ptls_t *tls = tls12_import(&suite, 0, ms, randoms, &ctx, suites);
+    int ret = tls == NULL ? -1 : 0;
+    size_t off = 0;
+    while (ret == 0 && off < len) {
+        size_t consumed = len - off;
+        ret = ptls_receive(tls, out, wire + off, &consumed);
+        off += consumed;
+    }
+    if (tls != NULL)
+        ptls_free(tls);
+    return ret;
+}
+
+static void tls12_test(ptls_aead_algorithm_t *ours, ptls_aead_algorithm_t *ref, ptls_hash_algorithm_t *hash, const char *what)
+{
+    static uint8_t data[40000];
+    uint8_t ms[48], randoms[64];
+    rnd(ms, sizeof(ms));
+    rnd(randoms, sizeof(randoms));
+    rnd(data, sizeof(data));
+    OK(ours->tls12.fixed_iv_size == ref->tls12.fixed_iv_size && ours->tls12.record_iv_size == ref->tls12.record_iv_size &&
+           ours->non_temporal == ref->non_temporal && ours->align_bits == ref->align_bits && ours->key_size == ref->key_size,
+       "non-temporal object fields match fusion");
+    ptls_buffer_t a, b, pa, pb;
+    ptls_buffer_init(&a, "", 0);
+    ptls_buffer_init(&b, "", 0);
+    ptls_buffer_init(&pa, "", 0);
+    ptls_buffer_init(&pb, "", 0);
+    tls12_send(ours, hash, ms, randoms, data, sizeof(data), &a);
+    tls12_send(ref, hash, ms, randoms, data, sizeof(data), &b);
+    OK(a.off == b.off && memcmp(a.base, b.base, a.off) == 0, "%s", what);
+    OK(tls12_receive(ours, hash, ms, randoms, b.base, b.off, &pa) == 0 && pa.off == sizeof(data) &&
+           memcmp(pa.base, data, sizeof(data)) == 0,
+       "tls12 receive (mi355x) of fusion's records");
+    b.base[100] ^= 1;
+    OK(tls12_receive(ours, hash, ms, randoms, b.base, b.off, &pb) == PTLS_ALERT_BAD_RECORD_MAC, "tls12 tampered record rejected");
+    ptls_buffer_dispose(&a);
+    ptls_buffer_dispose(&b);
+    ptls_buffer_dispose(&pa);
+    ptls_buffer_dispose(&pb);
+}
+
 int main(void)
 {
     if (!ptls_fusion_is_supported_by_cpu()) {
@@ -210,6 +290,8 @@ int main(void)
     supp_test(&ptls_mi355x_aes128gcm, &ptls_mi355x_aes128ctr, &ptls_fusion_aes128gcm, &ptls_fusion_aes128ctr);
     supp_test(&ptls_mi355x_aes256gcm, &ptls_mi355x_aes256ctr, &ptls_fusion_aes256gcm, &ptls_fusion_aes256ctr);
     quiclb_test();
+    tls12_test(&ptls_mi355x_non_temporal_aes128gcm, &ptls_non_temporal_aes128gcm, &ptls_openssl_sha256, "tls12 aes128gcm wire == fusion");
+    tls12_test(&ptls_mi355x_non_temporal_aes256gcm, &ptls_non_temporal_aes256gcm, &ptls_openssl_sha384, "tls12 aes256gcm wire == fusion");
     printf("1..%d\n# %d failed\n", ntest, nfail);
     return nfail == 0 ? 0 : 1;
 }

@@ -193,3 +193,49 @@ def test_quiclb_oracle_vs_fusion_random(oracle):
         data = rng.bytes(ln)
         for enc in (True, False):
             assert oracle.quiclb(key, data, enc) == ref.quiclb(key, data, enc), (ln, enc)
+
+
+# ------------------------------------------------------------------------------------------------ TLS 1.2 framing
+
+HAVE_TLS12_REF = os.path.exists(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
+                                             "libtls12_ref.so"))
+
+
+def parse_tls12_records(wire: bytes):
+    """(type, explicit nonce, ciphertext||tag) per record: header {type, 3, 3, BE16(n)} || nonce (8) || body."""
+    out, off = [], 0
+    while off < len(wire):
+        t, v0, v1, n = wire[off], wire[off + 1], wire[off + 2], int.from_bytes(wire[off + 3:off + 5], "big")
+        assert (v0, v1) == (3, 3)
+        out.append((t, int.from_bytes(wire[off + 5:off + 13], "big"), wire[off + 13:off + 5 + n]))
+        off += 5 + n
+    return out
+
+
+@pytest.mark.skipif(not HAVE_TLS12_REF, reason="oracle/_ref/libtls12_ref.so not built")
+@pytest.mark.parametrize("key_size", [16, 32])
+def test_tls12_record_layer_matches_oracle_framing(oracle, key_size):
+    # picotls' own TLS 1.2 send path (lib/picotls.c:779-799) decoded with the framing the engine implements:
+    # nonce = fixed IV || explicit nonce, AAD = BE64(seq) || type || 3 || 3 || BE16(len) (build_tls12_aad :753-762)
+    from oracle import Tls12Ref
+
+    t = Tls12Ref()
+    rng = np.random.default_rng(key_size)
+    ms, randoms = rng.bytes(48), rng.bytes(64)
+    key, fixed = t.server_keys(key_size, ms, randoms)
+    data = rng.bytes(40000)  # three records: 16384, 16384, 7232
+    rec_iv = 0x0102030405060708
+    wire = t.send(key_size, ms, randoms, rec_iv, data)
+    recs = parse_tls12_records(wire)
+    assert [len(b) - 16 for _, _, b in recs] == [16384, 16384, 40000 - 32768]
+    pos = 0
+    for i, (typ, nonce, body) in enumerate(recs):
+        assert typ == 23 and nonce == rec_iv + i
+        ln = len(body) - 16
+        aad = (1 + i).to_bytes(8, "big") + bytes([typ, 3, 3]) + ln.to_bytes(2, "big")
+        assert oracle.open(key, fixed + bytes(8), nonce, aad, body) == data[pos:pos + ln]
+        pos += ln
+    assert t.receive(key_size, ms, randoms, wire) == data
+    bad = bytearray(wire)
+    bad[20] ^= 1
+    assert t.receive(key_size, ms, randoms, bytes(bad)) == -20  # PTLS_ALERT_BAD_RECORD_MAC
