@@ -1462,7 +1462,50 @@ struct st_ptls_mi355x_keyset_t {
     KeyEntry *d_keys;
     int ncu;
     int schedule;
+    // staging for the synchronous host-buffer helpers (the per-record picotls path): one pinned host buffer and one
+    // device buffer, grown on demand, and a stream of their own, so a call is one H2D copy, one launch, one D2H copy
+    uint8_t *d_stage, *h_stage;
+    size_t stage_cap;
+    hipStream_t stream;
 };
+
+static int stage_reserve(ptls_mi355x_keyset_t *ks, size_t bytes)
+{
+    if (bytes <= ks->stage_cap)
+        return 0;
+    size_t cap = ks->stage_cap * 2 > bytes ? ks->stage_cap * 2 : bytes;
+    cap = cap < 4096 ? 4096 : (cap + 4095) & ~(size_t)4095;
+    if (ks->stream == NULL)
+        HIP_TRY(hipStreamCreateWithFlags(&ks->stream, hipStreamNonBlocking));
+    if (ks->d_stage != NULL) {
+        HIP_TRY(hipStreamSynchronize(ks->stream));
+        hipFree(ks->d_stage);
+        hipHostFree(ks->h_stage);
+        ks->d_stage = ks->h_stage = NULL;
+        ks->stage_cap = 0;
+    }
+    HIP_TRY(hipMalloc((void **)&ks->d_stage, cap));
+    if (hipHostMalloc((void **)&ks->h_stage, cap, hipHostMallocDefault) != hipSuccess) {
+        hipFree(ks->d_stage);
+        ks->d_stage = NULL;
+        return fail("%s", "stage: pinned host allocation failed");
+    }
+    ks->stage_cap = cap;
+    return 0;
+}
+
+// H2D of the first `up` staged bytes, the launch (run by the caller's lambda), D2H of [down_off, down_off + down),
+// then wait: the synchronous round trip of the host-buffer helpers
+template <typename Launch>
+static int stage_roundtrip(ptls_mi355x_keyset_t *ks, size_t up, size_t down_off, size_t down, Launch launch)
+{
+    HIP_TRY(hipMemcpyAsync(ks->d_stage, ks->h_stage, up, hipMemcpyHostToDevice, ks->stream));
+    if (launch() != 0)
+        return -1;
+    HIP_TRY(hipMemcpyAsync(ks->h_stage + down_off, ks->d_stage + down_off, down, hipMemcpyDeviceToHost, ks->stream));
+    HIP_TRY(hipStreamSynchronize(ks->stream));
+    return 0;
+}
 
 static int engine_init_attrs(void)
 {
@@ -1559,6 +1602,15 @@ void ptls_mi355x_keyset_free(ptls_mi355x_keyset_t *ks)
     hipMemset(ks->d_keys, 0, ks->nkeys * sizeof(KeyEntry));
     hipDeviceSynchronize();
     hipFree(ks->d_keys);
+    if (ks->d_stage != NULL) {
+        hipMemset(ks->d_stage, 0, ks->stage_cap);
+        memset(ks->h_stage, 0, ks->stage_cap);  // staged plaintext and keystream-derived bytes
+        hipDeviceSynchronize();
+        hipFree(ks->d_stage);
+        hipHostFree(ks->h_stage);
+    }
+    if (ks->stream != NULL)
+        hipStreamDestroy(ks->stream);
     free(ks);
 }
 
@@ -1813,71 +1865,72 @@ int ptls_mi355x_quiclb_transform(ptls_mi355x_keyset_t *ks, size_t key_idx, void 
     if (ks == NULL || key_idx >= ks->nkeys || output == NULL || input == NULL || len < PTLS_MI355X_QUICLB_MIN_LEN ||
         len > PTLS_MI355X_QUICLB_MAX_LEN)
         return fail("%s", "quiclb_transform: invalid arguments");
-    uint8_t *d = NULL;
-    HIP_TRY(hipMalloc((void **)&d, 96));
-    const ptls_mi355x_cid_t c = {0, 32, (uint32_t)key_idx, (uint8_t)len, (uint8_t)(encrypt != 0), 0};
-    int ret = -1;
-    if (hipMemcpy(d, input, len, hipMemcpyHostToDevice) == hipSuccess && hipMemcpy(d + 64, &c, sizeof(c), hipMemcpyHostToDevice) == hipSuccess &&
-        ptls_mi355x_quiclb_batch(ks, (const ptls_mi355x_cid_t *)(d + 64), 1, d, d, NULL) == 0 &&
-        hipMemcpy(output, d + 32, len, hipMemcpyDeviceToHost) == hipSuccess)
-        ret = 0;
-    hipFree(d);
-    return ret;
+    if (stage_reserve(ks, 96) != 0)
+        return -1;
+    // staging: [0, 32) CID in, [32, 56) descriptor | [64, 96) CID out
+    const ptls_mi355x_cid_t c = {0, 64, (uint32_t)key_idx, (uint8_t)len, (uint8_t)(encrypt != 0), 0};
+    memcpy(ks->h_stage, input, len);
+    memcpy(ks->h_stage + 32, &c, sizeof(c));
+    uint8_t *d = ks->d_stage;
+    if (stage_roundtrip(ks, 64, 64, 32, [&] {
+            return ptls_mi355x_quiclb_batch(ks, (const ptls_mi355x_cid_t *)(d + 32), 1, d, d, ks->stream);
+        }) != 0)
+        return -1;
+    memcpy(output, ks->h_stage + 64, len);
+    return 0;
 }
 
 int ptls_mi355x_encrypt_block(ptls_mi355x_keyset_t *ks, size_t key_idx, void *out, const void *in)
 {
     if (ks == NULL || key_idx >= ks->nkeys || out == NULL || in == NULL)
         return fail("%s", "encrypt_block: invalid arguments");
-    uint8_t *d = NULL;
-    HIP_TRY(hipMalloc((void **)&d, 48));
-    u32 idx = (u32)key_idx;
-    int ret = -1;
-    if (hipMemcpy(d, in, 16, hipMemcpyHostToDevice) == hipSuccess && hipMemcpy(d + 32, &idx, 4, hipMemcpyHostToDevice) == hipSuccess &&
-        ptls_mi355x_ecb_batch(ks, (const uint32_t *)(d + 32), d, d + 16, 1, NULL) == 0 &&
-        hipMemcpy(out, d + 16, 16, hipMemcpyDeviceToHost) == hipSuccess)
-        ret = 0;
-    hipFree(d);
-    return ret;
+    if (stage_reserve(ks, 64) != 0)
+        return -1;
+    // staging: [0, 16) block in, [16, 20) key index | [32, 48) block out
+    const u32 idx = (u32)key_idx;
+    memcpy(ks->h_stage, in, 16);
+    memcpy(ks->h_stage + 16, &idx, 4);
+    uint8_t *d = ks->d_stage;
+    if (stage_roundtrip(ks, 32, 32, 16, [&] {
+            return ptls_mi355x_ecb_batch(ks, (const uint32_t *)(d + 16), d, d + 32, 1, ks->stream);
+        }) != 0)
+        return -1;
+    memcpy(out, ks->h_stage + 32, 16);
+    return 0;
 }
 
-// single record on host buffers: a batch of one
+// single record on host buffers: a batch of one through the keyset's staging buffers
 static int single(ptls_mi355x_keyset_t *ks, size_t key_idx, bool open, void *output, const void *input, size_t len, uint64_t seq,
                   const void *aad, size_t aadlen, int *verified)
 {
     if (ks == NULL || key_idx >= ks->nkeys || aadlen > 0xffff || len > PTLS_MI355X_MAX_RECORD_LEN)
         return fail("%s", "single: invalid arguments");
     const size_t inbytes = len + (open ? 16 : 0), outbytes = len + (open ? 0 : 16);
-    uint8_t *d = NULL;
-    const size_t off_in = 0, off_out = (inbytes + 15) & ~(size_t)15, off_aad = off_out + ((outbytes + 15) & ~(size_t)15),
-                 off_rec = off_aad + ((aadlen + 15) & ~(size_t)15), off_ok = off_rec + 64, total = off_ok + 16;
-    HIP_TRY(hipMalloc((void **)&d, total));
-    ptls_mi355x_record_t r = {0, 0, seq, 0, (u32)len, 0, (uint16_t)aadlen, 0};  // offsets relative to the arenas below
-    int ret = -1;
+    // staging: [in | aad | descriptor] goes up, [out | ok] comes back
+    const size_t off_in = 0, off_aad = (inbytes + 15) & ~(size_t)15, off_rec = off_aad + ((aadlen + 15) & ~(size_t)15),
+                 off_out = off_rec + 64, off_ok = off_out + ((outbytes + 15) & ~(size_t)15), total = off_ok + 16;
+    if (stage_reserve(ks, total) != 0)
+        return -1;
+    const ptls_mi355x_record_t r = {0, 0, seq, 0, (u32)len, 0, (uint16_t)aadlen, 0};  // offsets relative to the arenas below
     ptls_mi355x_keyset_t view = *ks;
     view.d_keys = ks->d_keys + key_idx;
     view.nkeys = 1;
-    if (hipMemcpy(d + off_in, input, inbytes, hipMemcpyHostToDevice) != hipSuccess ||
-        (aadlen != 0 && hipMemcpy(d + off_aad, aad, aadlen, hipMemcpyHostToDevice) != hipSuccess) ||
-        hipMemcpy(d + off_rec, &r, sizeof(r), hipMemcpyHostToDevice) != hipSuccess)
-        goto Exit;
-    if (launch_batch(&view, open, (const ptls_mi355x_record_t *)(d + off_rec), 1, d + off_in, d + off_aad, d + off_out,
-                     d + off_ok, NULL) != 0)
-        goto Exit;
-    if (hipMemcpy(output, d + off_out, outbytes, hipMemcpyDeviceToHost) != hipSuccess)
-        goto Exit;
-    if (open) {
-        uint8_t okb = 0;
-        if (hipMemcpy(&okb, d + off_ok, 1, hipMemcpyDeviceToHost) != hipSuccess)
-            goto Exit;
-        *verified = okb;
-    }
-    ret = 0;
-Exit:
-    if (ret != 0 && g_err[0] == '\0')
-        fail("%s", "single: device copy failed");
-    hipFree(d);
-    return ret;
+    uint8_t *h = ks->h_stage, *d = ks->d_stage;
+    if (inbytes != 0)
+        memcpy(h + off_in, input, inbytes);
+    if (aadlen != 0)
+        memcpy(h + off_aad, aad, aadlen);
+    memcpy(h + off_rec, &r, sizeof(r));
+    if (stage_roundtrip(ks, off_out, off_out, total - off_out, [&] {
+            return launch_batch(&view, open, (const ptls_mi355x_record_t *)(d + off_rec), 1, d + off_in, d + off_aad,
+                                d + off_out, d + off_ok, ks->stream);
+        }) != 0)
+        return -1;
+    if (outbytes != 0)
+        memcpy(output, h + off_out, outbytes);
+    if (open)
+        *verified = h[off_ok];
+    return 0;
 }
 
 int ptls_mi355x_encrypt(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const void *input, size_t inlen, uint64_t seq,
