@@ -116,6 +116,7 @@ static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 #define CRUN_UNITS 1024      // units per run
 #define WHOLE_RUN_RECS 4096  // records per run when a one-key run is uniform (every record one unit)
 #define UNIFORM_SLACK 2      // a run is uniform when its records' step counts differ by at most this
+#define WHOLE_MIN_RECS (ENGINE_WG / ENGINE_G)  // whole-record mode needs at least one record per 8-lane group
 #define CLDS_CTL (LDS_BYTES + GHASH_TABLE_BYTES)                // 128 control words
 #define CLDS_UBASE (CLDS_CTL + 512)                             // u32[CRUN_RECS + 1]: first unit of each record
 #define CLDS_DONE (CLDS_UBASE + 4 * (CRUN_RECS + 16))           // u32[CRUN_RECS]: finished units per record
@@ -1076,8 +1077,10 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             smin = min(smin, s_ctl[16 + w]);
             smax = max(smax, s_ctl[20 + w]);
         }
-        // uniform run: every record is one unit (no partials), and a one-key batch may take a much longer run
-        const bool whole = smax <= smin + UNIFORM_SLACK;
+        // uniform run: every record is one unit (no partials), and a one-key batch may take a much longer run. A
+        // workgroup with fewer records left than it has groups cuts them into units instead, so that a small batch
+        // (the per-record picotls path is a batch of one) spreads over the workgroup's waves.
+        const bool whole = smax <= smin + UNIFORM_SLACK && end - pos >= WHOLE_MIN_RECS;
         if (whole && !args.multi_key)
             run_n = (u32)min(end - pos, (u64)WHOLE_RUN_RECS);
         if (!whole && wave < SCAN_WAVES) {
