@@ -39,6 +39,7 @@ typedef uint32_t u32;
 typedef uint64_t u64;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 __attribute__((aligned(1))) u32x4_u;
+typedef u32 __attribute__((aligned(1))) u32_u;
 
 static_assert(sizeof(ptls_mi355x_record_t) == PTLS_MI355X_RECORD_SIZE, "record descriptor must be 40 bytes");
 static_assert(sizeof(ptls_mi355x_cid_t) == 24, "CID descriptor must be 24 bytes");
@@ -89,9 +90,6 @@ static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 
 #ifndef ENGINE_FAST_STEP
 #define ENGINE_FAST_STEP 1         // wave-uniform fast path for steps where every lane holds a full text block
-#endif
-#ifndef GHASH_BATCH
-#define GHASH_BATCH 0      // 1: issue GHASH table lookups in batches of 8
 #endif
 
 #define ENGINE_G 8                 // lanes per record
@@ -337,96 +335,11 @@ __device__ __forceinline__ void check_lds_base(const void *smem)
 __device__ __forceinline__ u32 te0(const lds_u8 *, u32 w, int r, u32 laneoff) { return lds_load32(TE_ADDR(w, r, laneoff)); }
 __device__ __forceinline__ u32 te2(const lds_u8 *, u32 w, int r, u32 laneoff) { return lds_load32(TE_ADDR(w, r, laneoff) + 128); }
 
-// Explicitly scheduled lookups (ENGINE_ASM_ROUNDS): the reads are issued from inline asm, so the compiler neither
-// reorders them nor inserts waits for them; lgkm_wait<N>() waits until at most N LDS/SMEM operations are outstanding
-// and, through its in/out operands, orders every use of the named values after that wait. LDS returns in order, so
-// waiting for <= N outstanding guarantees every read issued more than N reads ago has landed (other outstanding ops only
-// make the wait stricter).
-#ifndef ENGINE_ASM_ROUNDS
-#define ENGINE_ASM_ROUNDS 0
-#endif
-__device__ __forceinline__ u32 te0_issue(u32 w, int r, u32 laneoff)
-{
-    u32 v;
-    asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(TE_ADDR(w, r, laneoff)));
-    return v;
-}
-__device__ __forceinline__ u32 te2_issue(u32 w, int r, u32 laneoff)
-{
-    u32 v;
-    asm volatile("ds_read_b32 %0, %1 offset:128" : "=v"(v) : "v"(TE_ADDR(w, r, laneoff)));
-    return v;
-}
-template <int N>
-__device__ __forceinline__ void lgkm_wait(u32 &a, u32 &b)
-{
-    asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N));
-}
-template <int N>
-__device__ __forceinline__ void lgkm_wait(u32 &a, u32 &b, u32 &c, u32 &d)
-{
-    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : "i"(N));
-}
-
-// One full T-table round with all 16 lookups issued back to back (column-major) and the columns combined as their
-// four reads land.
-__device__ __forceinline__ void aes_round_asm(u32 (&s)[4], const u32 (&rk)[4], u32 laneoff)
-{
-    u32 e[4][4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        e[c][0] = te0_issue(s[c], 0, laneoff);
-        e[c][1] = te2_issue(s[(c + 2) & 3], 2, laneoff);
-        e[c][2] = te0_issue(s[(c + 1) & 3], 1, laneoff);
-        e[c][3] = te2_issue(s[(c + 3) & 3], 3, laneoff);
-    }
-    lgkm_wait<12>(e[0][0], e[0][1], e[0][2], e[0][3]);
-    s[0] = xor3(e[0][0], e[0][1], rk[0]) ^ rotl8(e[0][2] ^ e[0][3]);
-    lgkm_wait<8>(e[1][0], e[1][1], e[1][2], e[1][3]);
-    s[1] = xor3(e[1][0], e[1][1], rk[1]) ^ rotl8(e[1][2] ^ e[1][3]);
-    lgkm_wait<4>(e[2][0], e[2][1], e[2][2], e[2][3]);
-    s[2] = xor3(e[2][0], e[2][1], rk[2]) ^ rotl8(e[2][2] ^ e[2][3]);
-    lgkm_wait<0>(e[3][0], e[3][1], e[3][2], e[3][3]);
-    s[3] = xor3(e[3][0], e[3][1], rk[3]) ^ rotl8(e[3][2] ^ e[3][3]);
-}
-
-__device__ __forceinline__ void aes_last_round_asm(u32 (&s)[4], const u32 (&rk)[4], u32 laneoff)
-{
-    u32 e[4][4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        e[c][0] = te2_issue(s[c], 0, laneoff);
-        e[c][1] = te0_issue(s[(c + 1) & 3], 1, laneoff);
-        e[c][2] = te0_issue(s[(c + 2) & 3], 2, laneoff);
-        e[c][3] = te2_issue(s[(c + 3) & 3], 3, laneoff);
-    }
-    u32 o[4];
-#define LAST_COL(c, N)                                                                                                 \
-    lgkm_wait<N>(e[c][0], e[c][1], e[c][2], e[c][3]);                                                                  \
-    o[c] = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_perm(e[c][1], e[c][0], 0x0c0c0500u),                          \
-                                       __builtin_amdgcn_perm(e[c][3], e[c][2], 0x07020c0cu), rk[c], 0x56)
-    LAST_COL(0, 12);
-    LAST_COL(1, 8);
-    LAST_COL(2, 4);
-    LAST_COL(3, 0);
-#undef LAST_COL
-    s[0] = o[0], s[1] = o[1], s[2] = o[2], s[3] = o[3];
-}
-
 // rounds FIRST .. NR of AES (T-table rounds, then the final SubBytes/ShiftRows/AddRoundKey) on NB independent
 // LE-column states; the NB blocks advance in lockstep so each round has 16*NB independent LDS lookups in flight.
 template <int NR, int FIRST, int NB>
 __device__ __forceinline__ void aes_rounds_n(const lds_u8 *lds, u32 laneoff, const u32 (*rk)[4], u32 (&s)[NB][4])
 {
-#if ENGINE_ASM_ROUNDS
-    if constexpr (NB == 1) {
-#pragma unroll
-        for (int r = FIRST; r < NR; ++r)
-            aes_round_asm(s[0], rk[r], laneoff);
-        aes_last_round_asm(s[0], rk[NR], laneoff);
-        return;
-    }
-#endif
 #pragma unroll
     for (int r = FIRST; r < NR; ++r) {
 #pragma unroll
@@ -518,8 +431,8 @@ __device__ __forceinline__ void aes_ctr_cached1(const lds_u8 *lds, u32 laneoff, 
 // ------------------------------------------------------------------------------------------------ GHASH (tables)
 
 // returns a * (table t's power), where tsel = 0x10000 + t * 8192: table base for the lane (t < 8: H^(t+1)).
-// The 32 window lookups are independent; they are issued in four batches of 8 (32 VGPRs in flight) and folded with
-// 3-input XORs, so one multiply costs a few overlapped LDS round trips rather than a chain of 16.
+// The 32 window lookups are independent and folded pairwise with 3-input XORs as they land, so one multiply costs a few
+// overlapped LDS round trips rather than a chain of 32 (the compiler keeps ~10 reads in flight).
 __device__ __forceinline__ u32x4 gmul_tab(const lds_u8 *, u32x4 a, u32 tsel)
 {
     u32x4 acc = {0, 0, 0, 0};
@@ -527,21 +440,6 @@ __device__ __forceinline__ u32x4 gmul_tab(const lds_u8 *, u32x4 a, u32 tsel)
     for (int q = 0; q < 4; ++q) {
         const u32 w = a[q];
         const u32 hi = w & 0xf0f0f0f0u, lo = (w << 4) & 0xf0f0f0f0u;
-#if GHASH_BATCH
-        u32x4 e[8];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const u32 sel = 0x0c020100u | (4u + k);
-            e[2 * k] = lds_load128(__builtin_amdgcn_perm(hi, tsel, sel) + (8 * q + 2 * k) * 256);
-            e[2 * k + 1] = lds_load128(__builtin_amdgcn_perm(lo, tsel, sel) + (8 * q + 2 * k + 1) * 256);
-        }
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            u32 x0 = xor3(e[0][c], e[1][c], e[2][c]), x1 = xor3(e[3][c], e[4][c], e[5][c]);
-            acc[c] = xor3(acc[c], xor3(x0, x1, e[6][c]), e[7][c]);
-        }
-        __builtin_amdgcn_sched_barrier(0);  // at most 8 entries (32 VGPRs) in flight
-#else
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const u32 sel = 0x0c020100u | (4u + k);
@@ -551,7 +449,6 @@ __device__ __forceinline__ u32x4 gmul_tab(const lds_u8 *, u32x4 a, u32 tsel)
             for (int c = 0; c < 4; ++c)
                 acc[c] = xor3(acc[c], e0[c], e1[c]);
         }
-#endif
     }
     return acc;
 }
@@ -703,8 +600,8 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     u32 nw1 = bswap32((u32)(r.seq >> 32)), nw2 = bswap32((u32)r.seq);
     if (TLS12) {
         const uint8_t *e = args.in + r.in_off + (OPEN ? TLS_HEADER_SIZE : 0);
-        nw1 = *(const u32 __attribute__((aligned(1))) *)e;
-        nw2 = *(const u32 __attribute__((aligned(1))) *)(e + 4);
+        nw1 = *(const u32_u *)e;
+        nw2 = *(const u32_u *)(e + 4);
     }
     const u32 n0 = iv0 ^ rk[0][0];
     const u32 n1 = iv1 ^ nw1 ^ rk[0][1];
