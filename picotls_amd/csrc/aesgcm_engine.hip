@@ -632,110 +632,112 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             nxt[i] = *(const u32x4_u *)(src + 16u * (u32)b);
     }
 
-    for (u32 s0 = 0; s0 < Smax; s0 += NB) {
-        const u32 m0 = m_lo + s0;
-        u32x4 cur[NB];
-        u32 st[NB][4];
-#pragma unroll
-        for (int i = 0; i < NB; ++i) {
-            cur[i] = nxt[i];
-            int bn;
-            if (full_block(m0 + NB + i, bn))
-                nxt[i] = *(const u32x4_u *)(src + 16u * (u32)bn);
-            // AES-CTR input: data positions encrypt counter 2+b, all others J0 (kept by the length lane as E(K, J0))
-            const int logical = (int)(j + G * (m0 + i)) - P;
-            const int b = logical - (int)na;
-            const bool is_data = m0 + i < m_hi && logical >= (int)na && b < (int)nb;
-            st[i][0] = n0, st[i][1] = n1, st[i][2] = n2;
-            const u32 ctr = is_data ? (u32)(b + 2) : 1u;
-            st[i][3] = bswap32(ctr) ^ rk[0][3];
-            if ((ctr >> 8) != cc1_key) {  // entering a new 256-counter window (divergent; skipped when no lane does)
-                cc1 = ctr_cache1_init<NR>(lds, laneoff, rk, n0, n1, n2, st[i][3]);
-                cc1_key = ctr >> 8;
-            }
+    // step m, part 1: the next step's input prefetch and this step's counter block (refreshing the counter cache when
+    // the lane enters a new 256-counter window)
+    u32x4 cur;
+    auto setup_step = [&](u32 m0, u32 (&st)[1][4]) {
+        cur = nxt[0];
+        int bn;
+        if (full_block(m0 + 1, bn))
+            nxt[0] = *(const u32x4_u *)(src + 16u * (u32)bn);
+        // AES-CTR input: data positions encrypt counter 2+b, all others J0 (kept by the length lane as E(K, J0))
+        const int logical = (int)(j + G * m0) - P;
+        const int b = logical - (int)na;
+        const bool is_data = m0 < m_hi && logical >= (int)na && b < (int)nb;
+        st[0][0] = n0, st[0][1] = n1, st[0][2] = n2;
+        const u32 ctr = is_data ? (u32)(b + 2) : 1u;
+        st[0][3] = bswap32(ctr) ^ rk[0][3];
+        if ((ctr >> 8) != cc1_key) {  // entering a new 256-counter window (divergent; skipped when no lane does)
+            cc1 = ctr_cache1_init<NR>(lds, laneoff, rk, n0, n1, n2, st[0][3]);
+            cc1_key = ctr >> 8;
         }
+    };
+    // step m, part 2: with the keystream block ks, write the output and return the GHASH input block X of position
+    // j + G*m
+    auto finish_step = [&](u32 m, const u32x4 &ks) -> u32x4 {
+        const bool act = m < m_hi;
+        const int logical = (int)(j + G * m) - P;
+        const int b = logical - (int)na;
+        const bool is_data = act && logical >= (int)na && b < (int)nb;
+        const bool is_aad = act && logical >= 0 && logical < (int)na;
+        const bool is_len = act && logical == (int)(na + nb);
+        u32x4 X = {0, 0, 0, 0};
+#if ENGINE_FAST_STEP
+        // steady state: every active lane of the wave holds a full 16-byte text block (one uniform branch, no
+        // per-case dispatch)
+        const bool full = is_data && Lsrc - 16u * (u32)b >= 16;
+        if (__all(!act || full)) {
+            const u32x4 o = cur ^ ks;
+            if (act)
+                *(u32x4_u *)(dst + 16u * (u32)b) = o;
+            return OPEN ? cur : o;
+        }
+#endif
+        if (is_data) {
+            const u32 rem = L - 16u * (u32)b;
+            uint8_t *op = dst + 16u * (u32)b;
+            if (rem >= 16 && (!SEAL_FRAME || Lsrc - 16u * (u32)b >= 16)) {
+                const u32x4 v = cur;
+                const u32x4 o = v ^ ks;
+                *(u32x4_u *)op = o;
+                X = OPEN ? v : o;
+            } else {
+                const u32 srem = Lsrc - 16u * (u32)b;
+                u32x4 v = load_partial(src + 16u * (u32)b, srem);
+                if (SEAL_FRAME)  // the inner content type follows the payload
+                    v[srem >> 2] |= (u32)(r.flags & 0xffu) << (8 * (srem & 3));
+                const u32x4 o = rem >= 16 ? v ^ ks : mask_tail(v ^ ks, rem);
+                if (rem >= 16)
+                    *(u32x4_u *)op = o;
+                else
+                    store_partial(op, o, rem);
+                X = OPEN ? v : o;
+            }
+        } else if (is_aad) {
+            if (SEAL_FRAME) {  // the record header: built here, written to the wire, and authenticated
+                const u32 wl = L + 16;
+                X = u32x4{0x00030317u | ((wl >> 8) & 0xffu) << 24, wl & 0xffu, 0, 0};
+                store_partial(args.out + r.out_off, X, TLS_HEADER_SIZE);
+            } else if (TLS12) {  // AAD = BE64(seq) || type || 3 || 3 || BE16(len) (build_tls12_aad)
+                const u32 type = OPEN ? (u32)args.in[r.in_off] : (r.flags & 0xffu);
+                X = u32x4{bswap32((u32)(r.seq >> 32)), bswap32((u32)r.seq), type | 0x030300u | ((L >> 8) & 0xffu) << 24,
+                          L & 0xffu};
+                if (!OPEN) {  // the wire header and the explicit nonce
+                    const u32 wl = TLS12_RECORD_IV_SIZE + L + 16;
+                    const u32x4 h = {type | 0x030300u | ((wl >> 8) & 0xffu) << 24, (wl & 0xffu) | nw1 << 8,
+                                     nw1 >> 24 | nw2 << 8, nw2 >> 24};
+                    store_partial(args.out + r.out_off, h, TLS_HEADER_SIZE + TLS12_RECORD_IV_SIZE);
+                }
+            } else {
+                const u32 rem = A - 16u * (u32)logical;
+                const uint8_t *ap = aadp + 16u * (u32)logical;
+                X = rem >= 16 ? *(const u32x4_u *)ap : load_partial(ap, rem);
+            }
+        } else if (is_len) {
+            const u64 abits = (u64)A * 8, cbits = (u64)L * 8;
+            X[0] = bswap32((u32)(abits >> 32));
+            X[1] = bswap32((u32)abits);
+            X[2] = bswap32((u32)(cbits >> 32));
+            X[3] = bswap32((u32)cbits);
+            ek0 = ks;
+        }
+        return X;
+    };
+
+    for (u32 s0 = 0; s0 < Smax; ++s0) {
+        const u32 m0 = m_lo + s0;
+        u32 st[1][4];
+        setup_step(m0, st);
         aes_ctr_cached1<NR>(lds, laneoff, rk, cc1, st);
         __builtin_amdgcn_sched_barrier(0);
-
-#pragma unroll
-        for (int i = 0; i < NB; ++i) {
-            const u32 m = m0 + i;
-            const bool act = m < m_hi;
-            const int logical = (int)(j + G * m) - P;
-            const int b = logical - (int)na;
-            const bool is_data = act && logical >= (int)na && b < (int)nb;
-            const bool is_aad = act && logical >= 0 && logical < (int)na;
-            const bool is_len = act && logical == (int)(na + nb);
-            const u32x4 ks = {st[i][0], st[i][1], st[i][2], st[i][3]};
-
-            u32x4 X = {0, 0, 0, 0};
-#if ENGINE_FAST_STEP
-            // steady state: every active lane of the wave holds a full 16-byte text block (one uniform branch, no
-            // per-case dispatch)
-            const bool full = is_data && Lsrc - 16u * (u32)b >= 16;
-            if (__all(!act || full)) {
-                const u32x4 o = cur[i] ^ ks;
-                if (act)
-                    *(u32x4_u *)(dst + 16u * (u32)b) = o;
-                X = OPEN ? cur[i] : o;
-            } else
-#endif
-            if (is_data) {
-                const u32 rem = L - 16u * (u32)b;
-                uint8_t *op = dst + 16u * (u32)b;
-                if (rem >= 16 && (!SEAL_FRAME || Lsrc - 16u * (u32)b >= 16)) {
-                    const u32x4 v = cur[i];
-                    const u32x4 o = v ^ ks;
-                    *(u32x4_u *)op = o;
-                    X = OPEN ? v : o;
-                } else {
-                    const u32 srem = Lsrc - 16u * (u32)b;
-                    u32x4 v = load_partial(src + 16u * (u32)b, srem);
-                    if (SEAL_FRAME)  // the inner content type follows the payload
-                        v[srem >> 2] |= (u32)(r.flags & 0xffu) << (8 * (srem & 3));
-                    const u32x4 o = rem >= 16 ? v ^ ks : mask_tail(v ^ ks, rem);
-                    if (rem >= 16)
-                        *(u32x4_u *)op = o;
-                    else
-                        store_partial(op, o, rem);
-                    X = OPEN ? v : o;
-                }
-            } else if (is_aad) {
-                if (SEAL_FRAME) {  // the record header: built here, written to the wire, and authenticated
-                    const u32 wl = L + 16;
-                    X = u32x4{0x00030317u | ((wl >> 8) & 0xffu) << 24, wl & 0xffu, 0, 0};
-                    store_partial(args.out + r.out_off, X, TLS_HEADER_SIZE);
-                } else if (TLS12) {  // AAD = BE64(seq) || type || 3 || 3 || BE16(len) (build_tls12_aad)
-                    const u32 type = OPEN ? (u32)args.in[r.in_off] : (r.flags & 0xffu);
-                    X = u32x4{bswap32((u32)(r.seq >> 32)), bswap32((u32)r.seq), type | 0x030300u | ((L >> 8) & 0xffu) << 24,
-                              L & 0xffu};
-                    if (!OPEN) {  // the wire header and the explicit nonce
-                        const u32 wl = TLS12_RECORD_IV_SIZE + L + 16;
-                        const u32x4 h = {type | 0x030300u | ((wl >> 8) & 0xffu) << 24, (wl & 0xffu) | nw1 << 8,
-                                         nw1 >> 24 | nw2 << 8, nw2 >> 24};
-                        store_partial(args.out + r.out_off, h, TLS_HEADER_SIZE + TLS12_RECORD_IV_SIZE);
-                    }
-                } else {
-                    const u32 rem = A - 16u * (u32)logical;
-                    const uint8_t *ap = aadp + 16u * (u32)logical;
-                    X = rem >= 16 ? *(const u32x4_u *)ap : load_partial(ap, rem);
-                }
-            } else if (is_len) {
-                const u64 abits = (u64)A * 8, cbits = (u64)L * 8;
-                X[0] = bswap32((u32)(abits >> 32));
-                X[1] = bswap32((u32)abits);
-                X[2] = bswap32((u32)(cbits >> 32));
-                X[3] = bswap32((u32)cbits);
-                ek0 = ks;
-            }
-            // scheduling fence: keeps the 32 table loads of this fold from being hoisted next to the other blocks'
-            // work (that hoisting spills them to scratch)
-            __builtin_amdgcn_sched_barrier(0);
-            const u32x4 prod = gmul_tab(lds, acc ^ X, m + 1 == m_hi ? tsel_last : tsel_horner);
-            if (act)
-                acc = prod;
-            __builtin_amdgcn_sched_barrier(0);
-        }
+        const u32x4 X = finish_step(m0, u32x4{st[0][0], st[0][1], st[0][2], st[0][3]});
+        // scheduling fence: keeps the 32 table loads of this fold from being hoisted next to the other work (that
+        // hoisting spills them to scratch)
+        __builtin_amdgcn_sched_barrier(0);
+        const u32x4 prod = gmul_tab(lds, acc ^ X, m0 + 1 == m_hi ? tsel_last : tsel_horner);
+        if (m0 < m_hi)
+            acc = prod;
+        __builtin_amdgcn_sched_barrier(0);
     }
 
     // XOR over the G lanes of the group
