@@ -37,8 +37,13 @@ def test_picotls_backend_exports_algorithms():
     if not os.path.exists(pa.PICOTLS_LIB_PATH):
         pytest.skip("picotls headers were not available at build time")
     syms = exported(pa.PICOTLS_LIB_PATH)
-    for s in ("ptls_mi355x_aes128gcm", "ptls_mi355x_aes256gcm", "ptls_mi355x_aes128ctr", "ptls_mi355x_aes256ctr"):
-        assert s in syms
+    text = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "picotls", "mi355x_picotls.h")).read(), flags=re.S)
+    objects = set()
+    for decl in re.findall(r"extern\s+ptls_\w+_algorithm_t\s+([^;]+);", text):
+        objects |= {n.strip() for n in decl.split(",")}
+    assert objects == {"ptls_mi355x_aes128ctr", "ptls_mi355x_aes256ctr", "ptls_mi355x_quiclb", "ptls_mi355x_aes128gcm",
+                       "ptls_mi355x_aes256gcm", "ptls_mi355x_non_temporal_aes128gcm", "ptls_mi355x_non_temporal_aes256gcm"}
+    assert objects <= syms
     assert declared("mi355x_picotls.h") <= syms
 
 
@@ -60,6 +65,15 @@ def test_record_descriptor_layout_matches_header():
     import oracle
 
     assert oracle.RECORD_DTYPE == pa.RECORD_DTYPE
+
+
+def test_side_descriptor_layouts_match_header():
+    text = open(os.path.join(ROOT, "include", "picotls", "mi355x.h")).read()
+    # ptls_mi355x_cid_t (QUIC-LB), ptls_mi355x_hp_t (header protection), ptls_mi355x_tls_result_t
+    assert re.search(r"uint64_t in_off;\s*uint64_t out_off;\s*uint32_t key_idx;\s*uint8_t len;\s*uint8_t encrypt;", text)
+    assert list(pa.CID_DTYPE.names) == ["in_off", "out_off", "key_idx", "len", "encrypt", "reserved"]
+    assert pa.CID_DTYPE.itemsize == 24 and pa.HP_DTYPE.itemsize == 16 and pa.TLS_RESULT_DTYPE.itemsize == 8
+    assert "#define PTLS_MI355X_QUICLB_MIN_LEN 7" in text and "#define PTLS_MI355X_QUICLB_MAX_LEN 19" in text
 
 
 def test_no_cpu_fallback_when_library_missing(tmp_path):
