@@ -94,7 +94,7 @@ int ptls_mi355x_keyset_set_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, const vo
  *   AUTO      = CHUNKED (the default)
  *   LOCKSTEP  one whole record per 8-lane group, records assigned statically; kept for comparison
  *   CHUNKED   waves pull work units from a per-run queue. Runs of uniform record lengths use whole records as units;
- *             other runs cut records into 1 KiB GHASH units recombined with H^64, which balances mixed lengths and
+ *             other runs cut records into 2 KiB GHASH units recombined with H^128, which balances mixed lengths and
  *             short per-connection key runs
  * Returns 0, or -1 for an unknown schedule.
  */

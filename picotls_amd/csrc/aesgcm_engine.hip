@@ -107,16 +107,22 @@ static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 
 // Chunked schedule (many-key batches): records are cut into units of at most CHUNK_BLOCKS GHASH-stream blocks, and
 // the per-unit GHASH partials are recombined with H^CHUNK_BLOCKS (one more 8 KiB table, LDS table slot 8).
-#define CHUNK_BLOCKS 64
+#ifndef CHUNK_BLOCKS
+#define CHUNK_BLOCKS 128  // 2 KiB units: 64K-key mixed +3 %, one-key mixed +7 % over 1 KiB units (interleaved A/B); 256: +1 % / +10 %
+#endif
 #define CHUNK_STEPS (CHUNK_BLOCKS / ENGINE_G)
-#define CHUNK_MAX_UNITS 64   // records longer than CHUNK_MAX_UNITS units (> ~64 KiB) are processed as one unit
+#define CHUNK_MAX_UNITS (4096 / CHUNK_BLOCKS)  // records longer than this many units (> ~64 KiB) run as one unit
+#define BKT_STRIDE (CHUNK_STEPS + 1)             // per-wave front-unit bucket counters in s_ctl
 #define CRUN_RECS 256        // records per run (one key)
+#ifndef CRUN_UNITS
 #define CRUN_UNITS 1024      // units per run
+#endif
 #define WHOLE_RUN_RECS 4096  // records per run when a one-key run is uniform (every record one unit)
 #define UNIFORM_SLACK 2      // a run is uniform when its records' step counts differ by at most this
 #define WHOLE_MIN_RECS (ENGINE_WG / ENGINE_G)  // whole-record mode needs at least one record per 8-lane group
-#define CLDS_CTL (LDS_BYTES + GHASH_TABLE_BYTES)                // 128 control words
-#define CLDS_UBASE (CLDS_CTL + 512)                             // u32[CRUN_RECS + 1]: first unit of each record
+#define CLDS_CTL_WORDS ((32 + (CRUN_RECS / 64) * BKT_STRIDE + 127) / 128 * 128)
+#define CLDS_CTL (LDS_BYTES + GHASH_TABLE_BYTES)                // CLDS_CTL_WORDS control words
+#define CLDS_UBASE (CLDS_CTL + 4 * CLDS_CTL_WORDS)              // u32[CRUN_RECS + 1]: first unit of each record
 #define CLDS_DONE (CLDS_UBASE + 4 * (CRUN_RECS + 16))           // u32[CRUN_RECS]: finished units per record
 #define CLDS_EK0 (CLDS_DONE + 4 * CRUN_RECS)                    // 16 B per record: E(K, J0)
 #define CLDS_PART (CLDS_EK0 + 16 * CRUN_RECS)                   // 16 B per unit: GHASH partial
@@ -124,6 +130,7 @@ static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 #define CLDS_ALLOC (CLDS_FRONT + 4 * CRUN_RECS)
 static_assert(CLDS_ALLOC <= 160 * 1024, "chunked schedule LDS budget");
 static_assert(CHUNK_BLOCKS % ENGINE_G == 0, "units are whole steps");
+
 
 // ------------------------------------------------------------------------------------------------ small helpers
 
@@ -1009,7 +1016,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 for (u32 b = 0; b <= CHUNK_STEPS; ++b) {
                     const u64 m = __ballot(in && bkt == b);
                     if (lane == 0)
-                        s_ctl[32 + 16 * wave + b] = (u32)__popcll(m);
+                        s_ctl[32 + BKT_STRIDE * wave + b] = (u32)__popcll(m);
                     if (in && bkt == b)
                         rank = (u32)__popcll(m & ((1ull << lane) - 1));
                 }
@@ -1020,14 +1027,14 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 for (u32 b = 0; b < bkt; ++b)
 #pragma unroll
                     for (u32 w = 0; w < SCAN_WAVES; ++w)
-                        base += s_ctl[32 + 16 * w + b];
+                        base += s_ctl[32 + BKT_STRIDE * w + b];
                 for (u32 w = 0; w < wave; ++w)
-                    base += s_ctl[32 + 16 * w + bkt];
+                    base += s_ctl[32 + BKT_STRIDE * w + bkt];
                 s_front[base] = threadIdx.x;
             }
 #pragma unroll
             for (u32 w = 0; w < SCAN_WAVES; ++w)
-                nhuge += s_ctl[32 + 16 * w];
+                nhuge += s_ctl[32 + BKT_STRIDE * w];
             __syncthreads();
         }
         const u32 total_units = whole ? run_n : s_ubase[run_n];
