@@ -111,7 +111,9 @@ static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 #define CHUNK_BLOCKS 128  // 2 KiB units: 64K-key mixed +3 %, one-key mixed +7 % over 1 KiB units (interleaved A/B); 256: +1 % / +10 %
 #endif
 #define CHUNK_STEPS (CHUNK_BLOCKS / ENGINE_G)
-#define CHUNK_MAX_UNITS (4096 / CHUNK_BLOCKS)  // records longer than this many units (> ~64 KiB) run as one unit
+#ifndef CHUNK_MAX_UNITS
+#define CHUNK_MAX_UNITS CRUN_UNITS  // records longer than this many units (> ~2 MiB) run as one unit
+#endif
 #define BKT_STRIDE (CHUNK_STEPS + 1)             // per-wave front-unit bucket counters in s_ctl
 #define CRUN_RECS 256        // records per run (one key)
 #ifndef CRUN_UNITS
