@@ -489,9 +489,27 @@ __device__ __forceinline__ u32x4 gmul_group(const lds_u8 *, u32x4 a, u32 tsel, u
 
 // ------------------------------------------------------------------------------------------------ byte-exact I/O
 
-// loads n (< 16) bytes, zero padded
+// zero bytes n..15
+__device__ __forceinline__ u32x4 mask_tail(u32x4 v, u32 n)
+{
+    u32x4 r;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        int nb = (int)n - 4 * c;
+        u32 m = nb >= 4 ? 0xffffffffu : nb <= 0 ? 0u : (0xffffffffu >> (32 - 8 * nb));
+        r[c] = v[c] & m;
+    }
+    return r;
+}
+
+// loads n (< 16) bytes, zero padded. As fusion's loadn128 (lib/fusion.c:355-368): when the 16 bytes at p stay inside
+// p's 4 KiB page (which holds valid data, so it is mapped) one unaligned 16-byte load plus a mask replaces n byte loads;
+// only a tail within 15 bytes of a page end is read byte by byte. Bytes past n are never used. n = 0 reads nothing (p
+// may then be one past the end of a buffer).
 __device__ __forceinline__ u32x4 load_partial(const uint8_t *p, u32 n)
 {
+    if (n != 0 && ((uintptr_t)p & 4095u) <= 4096u - 16u)
+        return mask_tail(*(const u32x4_u *)p, n);
     u32x4 v = {0, 0, 0, 0};
 #pragma unroll
     for (u32 i = 0; i < 15; ++i)
@@ -504,19 +522,6 @@ __device__ __forceinline__ void store_partial(uint8_t *p, u32x4 v, u32 n)
 {
     for (u32 i = 0; i < n; ++i)
         p[i] = (uint8_t)(v[i >> 2] >> (8 * (i & 3)));
-}
-
-// zero bytes n..15
-__device__ __forceinline__ u32x4 mask_tail(u32x4 v, u32 n)
-{
-    u32x4 r;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        int nb = (int)n - 4 * c;
-        u32 m = nb >= 4 ? 0xffffffffu : nb <= 0 ? 0u : (0xffffffffu >> (32 - 8 * nb));
-        r[c] = v[c] & m;
-    }
-    return r;
 }
 
 // ------------------------------------------------------------------------------------------------ main kernel
