@@ -140,6 +140,26 @@ __device__ __forceinline__ u32 bswap32(u32 x) { return __builtin_bswap32(x); }
 __device__ __forceinline__ u32 rotl8(u32 x) { return __builtin_amdgcn_alignbit(x, x, 24); }
 __device__ __forceinline__ u32 xor3(u32 a, u32 b, u32 c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
 
+// Cross-lane steps on the VALU (DPP) instead of the LDS crossbar (__shfl lowers to ds_bpermute, which competes with the
+// table lookups for the LDS): XOR over each aligned group of 8 lanes (quad_perm [1,0,3,2], [2,3,0,1], then
+// row_half_mirror pairs the two quads), result in all 8 lanes.
+__device__ __forceinline__ u32 dpp_xor8(u32 v)
+{
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+    return v;
+}
+// maximum over the wave of a value that is uniform within each 8-lane group
+__device__ __forceinline__ u32 wave_max_per8(u32 v)
+{
+    u32 m = (u32)__builtin_amdgcn_readlane((int)v, 0);
+#pragma unroll
+    for (int g = 1; g < 8; ++g)
+        m = max(m, (u32)__builtin_amdgcn_readlane((int)v, 8 * g));
+    return m;
+}
+
 // GF(2^128) * x on a GHASH element held as big-endian words (b0 most significant; bit 127 of the integer is x^0)
 __device__ __forceinline__ void gf_mulx_be(u32 &b0, u32 &b1, u32 &b2, u32 &b3)
 {
@@ -480,10 +500,8 @@ __device__ __forceinline__ u32x4 gmul_group(const lds_u8 *, u32x4 a, u32 tsel, u
     for (int c = 0; c < 4; ++c)
         r[c] = xor3(e0[c], e1[c], e2[c]) ^ e3[c];
 #pragma unroll
-    for (int off = 1; off < 8; off <<= 1)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-            r[c] ^= (u32)__shfl_xor((int)r[c], off, 64);
+    for (int c = 0; c < 4; ++c)
+        r[c] = dpp_xor8(r[c]);
     return r;
 }
 
@@ -604,10 +622,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     const u32 K = (total + G - 1) / G;
     const int P = (int)(K * G) - (int)total;
 
-    u32 Smax = m_hi - m_lo;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1)
-        Smax = max(Smax, (u32)__shfl_xor((int)Smax, off, 64));
+    const u32 Smax = wave_max_per8(m_hi - m_lo);  // m_lo, m_hi are uniform within a group
 
     // nonce = iv ^ (0^32 || BE64(seq)) (lib/picotls.c:6587-6601); TLS 1.2 takes the explicit nonce of the record in
     // place of seq, read as stored (big endian), so its two words need no swap
@@ -755,13 +770,10 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     }
 
     // XOR over the G lanes of the group
+    static_assert(G == 8, "dpp_xor8 reduces groups of 8 lanes");
 #pragma unroll
-    for (int off = 1; off < G; off <<= 1) {
-        acc[0] ^= (u32)__shfl_xor((int)acc[0], off, 64);
-        acc[1] ^= (u32)__shfl_xor((int)acc[1], off, 64);
-        acc[2] ^= (u32)__shfl_xor((int)acc[2], off, 64);
-        acc[3] ^= (u32)__shfl_xor((int)acc[3], off, 64);
-    }
+    for (int c = 0; c < 4; ++c)
+        acc[c] = dpp_xor8(acc[c]);
     // whole record (finish): tag = GHASH ^ E(K, J0), written after the ciphertext (seal) or compared with the
     // received one (open)
     if (finish && valid && j == G - 1) {
