@@ -150,6 +150,13 @@ __device__ __forceinline__ u32 dpp_xor8(u32 v)
     v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
     return v;
 }
+// lane 7 of each aligned 8-lane group, to all 8 lanes (quad_perm [3,3,3,3], then row_half_mirror for lanes 0-3)
+__device__ __forceinline__ u32 dpp_bcast7(u32 v, u32 lane)
+{
+    const u32 t = (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0xFF, 0xF, 0xF, false);
+    const u32 u = (u32)__builtin_amdgcn_update_dpp(0, (int)t, 0x141, 0xF, 0xF, false);
+    return (lane & 4) ? t : u;
+}
 // maximum over the wave of a value that is uniform within each 8-lane group
 __device__ __forceinline__ u32 wave_max_per8(u32 v)
 {
@@ -1141,7 +1148,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                     __threadfence_block();  // partial and E(K, J0) land before the count that publishes them
                     last = atomicAdd((u32 *)&s_done[ri], 1u) == unc - 1;
                 }
-                last = (u32)__shfl((int)last, (int)(lane | (G - 1)), 64);
+                last = dpp_bcast7(last, lane);
                 if (last) {
                     // last unit of the record: GHASH = Horner over the partials with H^CHUNK_BLOCKS (whole group)
                     u32x4 g = s_part[first];
