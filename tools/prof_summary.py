@@ -8,6 +8,7 @@ import csv
 import collections
 import json
 import os
+import re
 import sys
 
 
@@ -43,7 +44,8 @@ def main(src, dst_prefix, records=None):
             if "GRBM_GUI_ACTIVE" in c:
                 k["effective_clock_GHz"] = c["GRBM_GUI_ACTIVE"] / 8 / (st["avg_ns"])
         out["kernels"][name] = k
-    seal = next((v for n, v in out["kernels"].items() if "false>" in n), None)
+    # the seal instantiation: gcm_*_kernel<NR, false[, FRAME]>
+    seal = next((v for n, v in out["kernels"].items() if re.search(r"<\d+, false[,>]", n)), None)
     if seal and "hbm_bytes_per_launch" in seal:
         out["seal_hbm_bytes_per_launch"] = seal["hbm_bytes_per_launch"]
     json.dump(out, open(dst_prefix + ".json", "w"), indent=1)
