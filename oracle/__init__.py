@@ -199,9 +199,9 @@ class FusionRef:
 
 
 class Tls12Ref:
-    """ctypes front-end of picotls' own TLS 1.2 record layer over fusion's non-temporal AEADs
-    (oracle/_ref/libtls12_ref.so, oracle/tls12_harness.c): ptls_import of ptls_build_tls12_export_params, then
-    ptls_send (server) / ptls_receive (client)."""
+    """ctypes front-end of picotls' own record layer (oracle/_ref/libtls12_ref.so, oracle/tls12_harness.c): TLS 1.2 over
+    fusion's non-temporal AEADs (ptls_import of ptls_build_tls12_export_params) and TLS 1.3 over the same objects
+    (ptls_import of traffic secrets), then ptls_send (server) / ptls_receive (client)."""
 
     def __init__(self):
         path = os.path.join(REF_DIR, "libtls12_ref.so")
@@ -216,6 +216,11 @@ class Tls12Ref:
         lib.ref_tls12_send.restype = sz
         lib.ref_tls12_receive.argtypes = [sz, vp, vp, vp, sz, vp, sz]
         lib.ref_tls12_receive.restype = ctypes.c_long
+        lib.ref_tls13_traffic_keys.argtypes = [sz, vp, vp, vp]
+        lib.ref_tls13_send.argtypes = [sz, vp, u64, vp, sz, vp, sz]
+        lib.ref_tls13_send.restype = sz
+        lib.ref_tls13_receive.argtypes = [sz, vp, u64, vp, sz, vp, sz]
+        lib.ref_tls13_receive.restype = ctypes.c_long
         self.lib = lib
 
     def server_keys(self, key_size: int, master_secret: bytes, randoms: bytes) -> tuple[bytes, bytes]:
@@ -240,4 +245,25 @@ class Tls12Ref:
         out = bytearray(len(wire) + 1)
         r = self.lib.ref_tls12_receive(key_size, _ptr(master_secret), _ptr(randoms), _ptr(bytes(wire)), len(wire), _ptr(out),
                                        len(out))
+        return bytes(out[:r]) if r >= 0 else r
+
+    # TLS 1.3 (ptls_import of traffic secrets, ptls_send / ptls_receive over ptls_non_temporal_aes{128,256}gcm)
+    def tls13_keys(self, key_size: int, secret: bytes) -> tuple[bytes, bytes]:
+        """(key, static IV) that setup_traffic_protection derives from a TLS 1.3 traffic secret (ptls_get_traffic_keys)."""
+        key, iv = bytearray(key_size), bytearray(12)
+        if self.lib.ref_tls13_traffic_keys(key_size, _ptr(secret), _ptr(key), _ptr(iv)) != 0:
+            raise RuntimeError("ptls_import / ptls_get_traffic_keys failed")
+        return bytes(key), bytes(iv)
+
+    def tls13_send(self, key_size: int, secret: bytes, seq: int, data: bytes) -> bytes:
+        cap = len(data) + (len(data) // 16384 + 1) * 64
+        out = bytearray(cap)
+        n = self.lib.ref_tls13_send(key_size, _ptr(secret), seq, _ptr(bytes(data)) if data else None, len(data), _ptr(out), cap)
+        if n == 0:
+            raise RuntimeError("ptls_send failed")
+        return bytes(out[:n])
+
+    def tls13_receive(self, key_size: int, secret: bytes, seq: int, wire: bytes):
+        out = bytearray(len(wire) + 1)
+        r = self.lib.ref_tls13_receive(key_size, _ptr(secret), seq, _ptr(bytes(wire)), len(wire), _ptr(out), len(out))
         return bytes(out[:r]) if r >= 0 else r

@@ -115,3 +115,129 @@ long ref_tls12_receive(size_t key_size, const uint8_t *master_secret, const uint
     ptls_free(tls);
     return ret;
 }
+
+/* ---------------------------------------------------------------- TLS 1.3 record layer
+ * ptls_import of TLS 1.3 traffic secrets in the serialization of ptls_export (export_tls_params, lib/picotls.c:5262-5282,
+ * TLS 1.3 block :5359-5365), then ptls_send (aead_encrypt / buffer_push_encrypted_records :728-738, :770-817) and
+ * ptls_receive (:5952-5974) over fusion's ptls_non_temporal_aes{128,256}gcm: the TLS 1.3 sender seals with
+ * ptls_aead_encrypt_v (payload || content type), which ptls_fusion_aes{128,256}gcm leave unimplemented
+ * (aead_do_encrypt_v asserts "FIXME", lib/fusion.c:1148-1152) and the non-temporal objects implement
+ * (non_temporal_encrypt_v128/256, :1345-2112). The traffic key and IV come from ptls_get_traffic_keys (the
+ * HKDF-Expand-Label of setup_traffic_protection). */
+static ptls_cipher_suite_t tls13_128 = {PTLS_CIPHER_SUITE_AES_128_GCM_SHA256, &ptls_non_temporal_aes128gcm, &ptls_openssl_sha256,
+                                        "TLS_AES_128_GCM_SHA256"},
+                           tls13_256 = {PTLS_CIPHER_SUITE_AES_256_GCM_SHA384, &ptls_non_temporal_aes256gcm, &ptls_openssl_sha384,
+                                        "TLS_AES_256_GCM_SHA384"};
+
+static ptls_t *import13(size_t key_size, int is_server, const uint8_t *enc_secret, uint64_t enc_seq, const uint8_t *dec_secret,
+                        uint64_t dec_seq, ptls_context_t *ctx, ptls_cipher_suite_t **suites)
+{
+    ptls_cipher_suite_t *suite = key_size == 32 ? &tls13_256 : &tls13_128;
+    const size_t dsz = suite->hash->digest_size;
+    static const uint8_t client_random[PTLS_HELLO_RANDOM_SIZE] = {0};
+    suites[0] = suite;
+    suites[1] = NULL;
+    memset(ctx, 0, sizeof(*ctx));
+    ctx->random_bytes = ptls_openssl_random_bytes;
+    ctx->get_time = &ptls_get_time;
+    ctx->cipher_suites = suites;
+    ptls_buffer_t p;
+    ptls_buffer_init(&p, "", 0);
+    ptls_t *tls = NULL;
+    int ret;
+    ptls_buffer_push_block(&p, 2, {
+        ptls_buffer_push(&p, (uint8_t)is_server);
+        ptls_buffer_push(&p, 0);
+        ptls_buffer_push16(&p, PTLS_PROTOCOL_VERSION_TLS13);
+        ptls_buffer_push16(&p, suite->id);
+        ptls_buffer_pushv(&p, client_random, PTLS_HELLO_RANDOM_SIZE);
+        ptls_buffer_push_block(&p, 2, {});
+        ptls_buffer_push_block(&p, 2, {});
+        ptls_buffer_push_block(&p, 2, {
+            ptls_buffer_pushv(&p, enc_secret, dsz);
+            ptls_buffer_push64(&p, enc_seq);
+            ptls_buffer_pushv(&p, dec_secret, dsz);
+            ptls_buffer_push64(&p, dec_seq);
+        });
+        ptls_buffer_push_block(&p, 2, {});
+    });
+    ret = ptls_import(ctx, &tls, ptls_iovec_init(p.base, p.off));
+    if (ret != 0)
+        tls = NULL;
+Exit:
+    ptls_buffer_dispose(&p);
+    return tls;
+}
+
+/* key and IV of the send direction of a server holding traffic secret `secret` (32 / 48 bytes) */
+int ref_tls13_traffic_keys(size_t key_size, const uint8_t *secret, uint8_t *key, uint8_t *iv)
+{
+    ptls_context_t ctx;
+    ptls_cipher_suite_t *suites[2];
+    uint8_t other[64] = {0};
+    ptls_t *tls = import13(key_size, 1, secret, 0, other, 0, &ctx, suites);
+    uint64_t seq;
+    if (tls == NULL)
+        return -1;
+    int ret = ptls_get_traffic_keys(tls, 1, key, iv, &seq);
+    ptls_free(tls);
+    return ret;
+}
+
+/* server sends `inlen` application-data bytes with traffic secret `secret`, first record sequence number `seq` */
+size_t ref_tls13_send(size_t key_size, const uint8_t *secret, uint64_t seq, const uint8_t *input, size_t inlen, uint8_t *out,
+                      size_t outcap)
+{
+    ptls_context_t ctx;
+    ptls_cipher_suite_t *suites[2];
+    uint8_t other[64] = {0};
+    ptls_t *tls = import13(key_size, 1, secret, seq, other, 0, &ctx, suites);
+    size_t n = 0;
+    if (tls == NULL)
+        return 0;
+    ptls_buffer_t buf;
+    ptls_buffer_init(&buf, "", 0);
+    if (ptls_send(tls, &buf, input, inlen) == 0 && buf.off <= outcap) {
+        memcpy(out, buf.base, buf.off);
+        n = buf.off;
+    }
+    ptls_buffer_dispose(&buf);
+    ptls_free(tls);
+    return n;
+}
+
+/* client receives the server's records (its decrypt secret = the server's `secret`); plaintext length or -(error) */
+long ref_tls13_receive(size_t key_size, const uint8_t *secret, uint64_t seq, const uint8_t *input, size_t inlen, uint8_t *out,
+                       size_t outcap)
+{
+    ptls_context_t ctx;
+    ptls_cipher_suite_t *suites[2];
+    uint8_t other[64] = {0};
+    ptls_t *tls = import13(key_size, 0, other, 0, secret, seq, &ctx, suites);
+    if (tls == NULL)
+        return -1;
+    ptls_buffer_t buf;
+    ptls_buffer_init(&buf, "", 0);
+    long ret = 0;
+    size_t off = 0;
+    while (off < inlen) {
+        size_t consumed = inlen - off;
+        int r = ptls_receive(tls, &buf, input + off, &consumed);
+        if (r != 0) {
+            ret = -(long)r;
+            break;
+        }
+        off += consumed;
+    }
+    if (ret == 0) {
+        if (buf.off <= outcap) {
+            memcpy(out, buf.base, buf.off);
+            ret = (long)buf.off;
+        } else {
+            ret = -1;
+        }
+    }
+    ptls_buffer_dispose(&buf);
+    ptls_free(tls);
+    return ret;
+}

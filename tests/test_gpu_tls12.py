@@ -1,7 +1,8 @@
-"""TLS 1.2 AES-GCM record protection on the GPU (ptls_mi355x_seal_tls12_records / _open_tls12_records) against
-picotls' own TLS 1.2 record layer over fusion's non-temporal AEADs (oracle/_ref/libtls12_ref.so: ptls_import +
-ptls_send / ptls_receive, lib/picotls.c:779-799, :6019-6060) and, for arbitrary descriptors, lib/fusion.c's
-ptls_aead_encrypt with the record-layer nonce and AAD. Bit-exact.
+"""Record framing on the GPU against picotls' own record layer (oracle/_ref/libtls12_ref.so: ptls_import + ptls_send /
+ptls_receive over fusion's non-temporal AEADs). TLS 1.2 (ptls_mi355x_seal_tls12_records / _open_tls12_records,
+lib/picotls.c:779-799, :6019-6060), and, for arbitrary descriptors, lib/fusion.c's ptls_aead_encrypt with the
+record-layer nonce and AAD; TLS 1.3 (ptls_mi355x_seal_tls_records / _open_tls_records, :728-738, :5952-5974) against
+ptls_send after ptls_import of a traffic secret. Bit-exact.
 """
 import os
 
@@ -179,4 +180,48 @@ def test_tls12_empty_batch():
     ks = pa.Keyset(bytes(16), bytes(12), 16)
     pa.seal_tls12_records(ks, 0, 0, 0, 0)
     pa.open_tls12_records(ks, 0, 0, 0, 0, 0)
+    ks.free()
+
+
+@pytest.mark.parametrize("key_size", [16, 32])
+def test_tls13_seal_equals_picotls_send_and_open_its_records(tls12ref, key_size):
+    # TLS 1.3: picotls' own ptls_send (aead_encrypt, lib/picotls.c:728-738) after ptls_import of a traffic secret; the
+    # batch (ptls_mi355x_seal_tls_records) with the key / IV of ptls_get_traffic_keys must give the same wire bytes,
+    # open_tls_records must recover the data from picotls' records, and ptls_receive must accept the engine's
+    rng = np.random.default_rng(500 + key_size)
+    secret = rng.bytes(32 if key_size == 16 else 48)
+    key, iv = tls12ref.tls13_keys(key_size, secret)
+    data = rng.bytes(70000)
+    # below 2^24: from there ptls_send first emits a KeyUpdate and rekeys (lib/picotls.c:6220-6232)
+    seq0 = int(rng.integers(0, 2**24 - 16))
+    wire = tls12ref.tls13_send(key_size, secret, seq0, data)
+    chunks = [data[o:o + 16384] for o in range(0, len(data), 16384)]
+    n = len(chunks)
+    recs = np.zeros(n, dtype=pa.RECORD_DTYPE)
+    pin = pout = 0
+    for i, c in enumerate(chunks):
+        recs[i]["in_off"], recs[i]["out_off"], recs[i]["len"] = pin, pout, len(c)
+        recs[i]["seq"], recs[i]["flags"] = seq0 + i, 23
+        pin += len(c)
+        pout += 5 + len(c) + 1 + 16
+    ks = pa.Keyset(key, iv, key_size)
+    d_recs, d_in, d_out = dev(recs), dev(np.frombuffer(data, np.uint8)), empty(pout, 0xEE)
+    pa.seal_tls_records(ks, d_recs.data_ptr(), n, d_in.data_ptr(), d_out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy().tobytes()
+    assert out == wire
+    orecs = np.zeros(n, dtype=pa.RECORD_DTYPE)
+    orecs["in_off"] = recs["out_off"]
+    orecs["out_off"] = np.cumsum([0] + [len(c) + 1 for c in chunks[:-1]])
+    orecs["len"] = [len(c) + 1 for c in chunks]
+    orecs["seq"] = recs["seq"]
+    d_recs2, d_wire, d_plain = dev(orecs), dev(np.frombuffer(wire, np.uint8)), empty(len(data) + n + 1)
+    d_ok, d_res = empty(n, 0x77), empty(8 * n, 0x77)
+    pa.open_tls_records(ks, d_recs2.data_ptr(), n, d_wire.data_ptr(), d_plain.data_ptr(), d_ok.data_ptr(), d_res.data_ptr(),
+                        torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ok, res, plain = d_ok.cpu().numpy(), d_res.cpu().numpy().view(pa.TLS_RESULT_DTYPE), d_plain.cpu().numpy()
+    assert ok.all() and (res["status"] == pa.TLS_OK).all() and (res["content_type"] == 23).all()
+    assert b"".join(plain[int(o):int(o) + int(r["plain_len"])].tobytes() for o, r in zip(orecs["out_off"], res)) == data
+    assert tls12ref.tls13_receive(key_size, secret, seq0, out) == data
     ks.free()

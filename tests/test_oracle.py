@@ -239,3 +239,39 @@ def test_tls12_record_layer_matches_oracle_framing(oracle, key_size):
     bad = bytearray(wire)
     bad[20] ^= 1
     assert t.receive(key_size, ms, randoms, bytes(bad)) == -20  # PTLS_ALERT_BAD_RECORD_MAC
+
+
+def parse_tls13_records(wire: bytes):
+    """(header, ciphertext||tag) per record: header {23, 3, 3, BE16(n)}."""
+    out, off = [], 0
+    while off < len(wire):
+        n = int.from_bytes(wire[off + 3:off + 5], "big")
+        assert wire[off:off + 3] == bytes([23, 3, 3])
+        out.append((wire[off:off + 5], wire[off + 5:off + 5 + n]))
+        off += 5 + n
+    return out
+
+
+@pytest.mark.skipif(not HAVE_TLS12_REF, reason="oracle/_ref/libtls12_ref.so not built")
+@pytest.mark.parametrize("key_size", [16, 32])
+def test_tls13_record_layer_matches_oracle_framing(oracle, key_size):
+    # picotls' own TLS 1.3 send path (aead_encrypt lib/picotls.c:728-738) decoded with the framing the engine
+    # implements: AAD = the 5-byte header, plaintext = payload || inner type (23), nonce = iv ^ seq
+    from oracle import Tls12Ref
+
+    t = Tls12Ref()
+    rng = np.random.default_rng(300 + key_size)
+    secret = rng.bytes(32 if key_size == 16 else 48)
+    key, iv = t.tls13_keys(key_size, secret)
+    data = rng.bytes(40000)
+    seq0 = 12345
+    wire = t.tls13_send(key_size, secret, seq0, data)
+    recs = parse_tls13_records(wire)
+    assert [len(b) - 17 for _, b in recs] == [16384, 16384, 40000 - 32768]
+    pos = 0
+    for i, (hdr, body) in enumerate(recs):
+        inner = oracle.open(key, iv, seq0 + i, hdr, body)
+        ln = len(body) - 17
+        assert inner == data[pos:pos + ln] + bytes([23])
+        pos += ln
+    assert t.tls13_receive(key_size, secret, seq0, wire) == data
