@@ -83,6 +83,14 @@ void ptls_mi355x_keyset_free(ptls_mi355x_keyset_t *ks);
 size_t ptls_mi355x_keyset_size(const ptls_mi355x_keyset_t *ks);
 size_t ptls_mi355x_keyset_key_size(const ptls_mi355x_keyset_t *ks);
 /**
+ * Replaces the key and static IV of the n entries key_idx[0..n) (host arrays: n * key_size key bytes, n * 12 IV bytes),
+ * deriving their schedules and H powers on the device: the rekey of some connections of a many-connection keyset, e.g.
+ * after a TLS 1.3 KeyUpdate (picotls rekeys a sender once its record sequence number reaches 2^24,
+ * lib/picotls.c:6220-6232, update_send_key -> setup_traffic_protection). Synchronous: waits for work in flight.
+ * Returns 0, or -1 on invalid arguments / out-of-range or repeated indices (nothing changed) or device failure.
+ */
+int ptls_mi355x_keyset_update(ptls_mi355x_keyset_t *ks, const uint32_t *key_idx, const void *keys, const void *ivs, size_t n);
+/**
  * Static IV accessors (do_get_iv / do_set_iv, include/picotls.h:475-481). Return 0 on success.
  */
 int ptls_mi355x_keyset_get_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, void *iv);

@@ -221,6 +221,8 @@ class Tls12Ref:
         lib.ref_tls13_send.restype = sz
         lib.ref_tls13_receive.argtypes = [sz, vp, u64, vp, sz, vp, sz]
         lib.ref_tls13_receive.restype = ctypes.c_long
+        lib.ref_tls13_send_rekeyed.argtypes = [sz, vp, u64, vp, sz, vp, sz, vp, vp, vp]
+        lib.ref_tls13_send_rekeyed.restype = sz
         self.lib = lib
 
     def server_keys(self, key_size: int, master_secret: bytes, randoms: bytes) -> tuple[bytes, bytes]:
@@ -262,6 +264,17 @@ class Tls12Ref:
         if n == 0:
             raise RuntimeError("ptls_send failed")
         return bytes(out[:n])
+
+    def tls13_send_rekeyed(self, key_size: int, secret: bytes, seq: int, data: bytes):
+        """(wire, key, IV, next seq) of the send direction after ptls_send: from seq >= 2^24 the wire starts with a
+        KeyUpdate record under the old key and the data records use the next traffic secret from seq 0."""
+        cap = len(data) + (len(data) // 16384 + 2) * 64
+        out, key, iv, nseq = bytearray(cap), bytearray(key_size), bytearray(12), ctypes.c_uint64()
+        n = self.lib.ref_tls13_send_rekeyed(key_size, _ptr(secret), seq, _ptr(bytes(data)) if data else None, len(data),
+                                            _ptr(out), cap, _ptr(key), _ptr(iv), ctypes.byref(nseq))
+        if n == 0:
+            raise RuntimeError("ptls_send failed")
+        return bytes(out[:n]), bytes(key), bytes(iv), nseq.value
 
     def tls13_receive(self, key_size: int, secret: bytes, seq: int, wire: bytes):
         out = bytearray(len(wire) + 1)

@@ -241,3 +241,28 @@ long ref_tls13_receive(size_t key_size, const uint8_t *secret, uint64_t seq, con
     ptls_free(tls);
     return ret;
 }
+
+/* as ref_tls13_send, then the send direction's key, IV and next sequence number afterwards (ptls_get_traffic_keys): from
+ * seq >= 2^24 ptls_send first emits a KeyUpdate under the old key and moves to the next traffic secret
+ * (lib/picotls.c:6220-6232, update_send_key :6193-6211) */
+size_t ref_tls13_send_rekeyed(size_t key_size, const uint8_t *secret, uint64_t seq, const uint8_t *input, size_t inlen,
+                              uint8_t *out, size_t outcap, uint8_t *key_after, uint8_t *iv_after, uint64_t *seq_after)
+{
+    ptls_context_t ctx;
+    ptls_cipher_suite_t *suites[2];
+    uint8_t other[64] = {0};
+    ptls_t *tls = import13(key_size, 1, secret, seq, other, 0, &ctx, suites);
+    size_t n = 0;
+    if (tls == NULL)
+        return 0;
+    ptls_buffer_t buf;
+    ptls_buffer_init(&buf, "", 0);
+    if (ptls_send(tls, &buf, input, inlen) == 0 && buf.off <= outcap &&
+        ptls_get_traffic_keys(tls, 1, key_after, iv_after, seq_after) == 0) {
+        memcpy(out, buf.base, buf.off);
+        n = buf.off;
+    }
+    ptls_buffer_dispose(&buf);
+    ptls_free(tls);
+    return n;
+}

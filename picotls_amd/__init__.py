@@ -38,6 +38,7 @@ ABI_FUNCTIONS = (
     "ptls_mi355x_keyset_key_size",
     "ptls_mi355x_keyset_get_iv",
     "ptls_mi355x_keyset_set_iv",
+    "ptls_mi355x_keyset_update",
     "ptls_mi355x_keyset_set_schedule",
     "ptls_mi355x_seal_batch",
     "ptls_mi355x_open_batch",
@@ -84,6 +85,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.ptls_mi355x_keyset_key_size.restype = sz
     lib.ptls_mi355x_keyset_get_iv.argtypes = [vp, sz, vp]
     lib.ptls_mi355x_keyset_set_iv.argtypes = [vp, sz, vp]
+    lib.ptls_mi355x_keyset_update.argtypes = [vp, vp, vp, vp, sz]
     lib.ptls_mi355x_keyset_set_schedule.argtypes = [vp, ci]
     lib.ptls_mi355x_seal_batch.argtypes = [vp, vp, sz, vp, vp, vp, vp]
     lib.ptls_mi355x_open_batch.argtypes = [vp, vp, sz, vp, vp, vp, vp, vp]
@@ -165,6 +167,16 @@ class Keyset:
     def set_iv(self, iv: bytes, idx: int = 0) -> None:
         if load_library().ptls_mi355x_keyset_set_iv(self.handle, idx, _buf(bytes(iv))) != 0:
             raise _err("set_iv")
+
+    def update(self, key_idx, keys: bytes, ivs: bytes) -> None:
+        """Rekeys entries key_idx (ptls_mi355x_keyset_update), e.g. after a TLS 1.3 KeyUpdate."""
+        idx = np.ascontiguousarray(key_idx, dtype=np.uint32)
+        k = np.frombuffer(bytes(keys), np.uint8)
+        v = np.frombuffer(bytes(ivs), np.uint8)
+        if k.size != idx.size * self.key_size or v.size != idx.size * 12:
+            raise ValueError("keys must be n*key_size bytes and ivs n*12 bytes")
+        if load_library().ptls_mi355x_keyset_update(self.handle, _buf(idx), _buf(k), _buf(v), idx.size) != 0:
+            raise _err("keyset_update")
 
     SCHEDULES = {"auto": 0, "lockstep": 1, "chunked": 2}
 

@@ -29,6 +29,7 @@
 
 #include <hip/hip_runtime.h>
 #include <type_traits>
+#include <vector>
 #include <stdint.h>
 #include <string.h>
 #include <stdio.h>
@@ -222,8 +223,9 @@ __device__ void aes_plain(const u32 (*rk)[4], int nr, u32 s[4])
 }
 
 // one thread per key: FIPS-197 key expansion, H = E_K(0), H^1..H^16, static IV
+// (slot: entry i goes to out[slot[i]] when slot != nullptr: a rekey of some connections of a keyset)
 __global__ void keyset_setup_kernel(const uint8_t *__restrict__ keys, const uint8_t *__restrict__ ivs, KeyEntry *__restrict__ out,
-                                    u32 nkeys, u32 key_size)
+                                    u32 nkeys, u32 key_size, const u32 *__restrict__ slot = nullptr)
 {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nkeys)
@@ -244,7 +246,7 @@ __global__ void keyset_setup_kernel(const uint8_t *__restrict__ keys, const uint
         }
         w[j] = w[j - nk] ^ t;
     }
-    KeyEntry *e = out + i;
+    KeyEntry *e = out + (slot != nullptr ? slot[i] : i);
     u32 rk[15][4];
     for (int r = 0; r < 15; ++r)
         for (int c = 0; c < 4; ++c)
@@ -1528,6 +1530,40 @@ Fail:
         hipFree(ks->d_keys);
     free(ks);
     return NULL;
+}
+
+int ptls_mi355x_keyset_update(ptls_mi355x_keyset_t *ks, const uint32_t *key_idx, const void *keys, const void *ivs, size_t n)
+{
+    if (ks == NULL || (n != 0 && (key_idx == NULL || keys == NULL || ivs == NULL)))
+        return fail("%s", "keyset_update: invalid arguments");
+    std::vector<bool> seen(n != 0 ? ks->nkeys : 0);
+    for (size_t i = 0; i < n; ++i) {
+        if (key_idx[i] >= ks->nkeys)
+            return fail("%s", "keyset_update: key index out of range");
+        if (seen[key_idx[i]])
+            return fail("%s", "keyset_update: key index listed twice");
+        seen[key_idx[i]] = true;
+    }
+    if (n == 0)
+        return 0;
+    uint8_t *d = NULL;
+    const size_t kb = n * ks->key_size, ib = n * 12, sb = n * 4;
+    HIP_TRY(hipMalloc((void **)&d, kb + ib + sb));
+    int ret = -1;
+    if (hipDeviceSynchronize() == hipSuccess &&  // no launch in flight still reads the old entries
+        hipMemcpy(d, keys, kb, hipMemcpyHostToDevice) == hipSuccess && hipMemcpy(d + kb, ivs, ib, hipMemcpyHostToDevice) == hipSuccess &&
+        hipMemcpy(d + kb + ib, key_idx, sb, hipMemcpyHostToDevice) == hipSuccess) {
+        keyset_setup_kernel<<<(unsigned)((n + 127) / 128), 128>>>(d, d + kb, ks->d_keys, (u32)n, (u32)ks->key_size,
+                                                                 (const u32 *)(d + kb + ib));
+        if (hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess)
+            ret = 0;
+    }
+    hipMemset(d, 0, kb + ib);
+    hipDeviceSynchronize();
+    hipFree(d);
+    if (ret != 0)
+        fail("%s", "keyset_update: device setup failed");
+    return ret;
 }
 
 void ptls_mi355x_keyset_free(ptls_mi355x_keyset_t *ks)

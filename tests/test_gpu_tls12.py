@@ -225,3 +225,81 @@ def test_tls13_seal_equals_picotls_send_and_open_its_records(tls12ref, key_size)
     assert b"".join(plain[int(o):int(o) + int(r["plain_len"])].tobytes() for o, r in zip(orecs["out_off"], res)) == data
     assert tls12ref.tls13_receive(key_size, secret, seq0, out) == data
     ks.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key_size", [16, 32])
+def test_tls13_key_update_via_keyset_update(tls12ref, key_size):
+    # picotls rekeys its send side once enc.seq reaches 2^24 (lib/picotls.c:6220-6232): the KeyUpdate record goes out
+    # under the old key, the data under the next traffic secret from seq 0. The engine does the same with one keyset:
+    # seal the KeyUpdate, ptls_mi355x_keyset_update to the new key / IV, seal the data; the wire bytes must match
+    rng = np.random.default_rng(520 + key_size)
+    secret = rng.bytes(32 if key_size == 16 else 48)
+    key, iv = tls12ref.tls13_keys(key_size, secret)
+    data = rng.bytes(50000)
+    seq0 = 2**24 + int(rng.integers(0, 1000))
+    wire, key2, iv2, seq_after = tls12ref.tls13_send_rekeyed(key_size, secret, seq0, data)
+    stream = torch.cuda.current_stream().cuda_stream
+    ks = pa.Keyset(key, iv, key_size)
+    # the KeyUpdate handshake message (type 24, length 1, request_update 0), content type 22
+    ku = np.zeros(1, dtype=pa.RECORD_DTYPE)
+    ku[0]["len"], ku[0]["seq"], ku[0]["flags"] = 5, seq0, 22
+    d_ku, d_kin, d_kout = dev(ku), dev(np.frombuffer(bytes([24, 0, 0, 1, 0]), np.uint8)), empty(27, 0xEE)
+    pa.seal_tls_records(ks, d_ku.data_ptr(), 1, d_kin.data_ptr(), d_kout.data_ptr(), stream)
+    torch.cuda.synchronize()
+    ks.update([0], key2, iv2)
+    chunks = [data[o:o + 16384] for o in range(0, len(data), 16384)]
+    n = len(chunks)
+    recs = np.zeros(n, dtype=pa.RECORD_DTYPE)
+    recs["in_off"] = np.arange(n) * 16384
+    recs["out_off"] = np.arange(n) * (16384 + 22)
+    recs["len"] = [len(c) for c in chunks]
+    recs["seq"], recs["flags"] = np.arange(n), 23
+    d_recs, d_in, d_out = dev(recs), dev(np.frombuffer(data, np.uint8)), empty(len(data) + 22 * n, 0xEE)
+    pa.seal_tls_records(ks, d_recs.data_ptr(), n, d_in.data_ptr(), d_out.data_ptr(), stream)
+    torch.cuda.synchronize()
+    assert seq_after == n
+    assert d_kout.cpu().numpy().tobytes() + d_out.cpu().numpy().tobytes() == wire
+    ks.free()
+
+
+@pytest.mark.gpu
+def test_keyset_update_rekeys_only_the_named_entries(ref):
+    # rekey entries 2 and 5 of a 7-key keyset (key schedule + H powers rebuilt on the GPU); every record of a batch
+    # over all keys must then equal fusion under the current key of its entry
+    rng = np.random.default_rng(530)
+    nkeys, n = 7, 70
+    keys = [rng.bytes(16) for _ in range(nkeys)]
+    ivs = [rng.bytes(12) for _ in range(nkeys)]
+    ks = pa.Keyset(b"".join(keys), b"".join(ivs), 16)
+    new = {2: (rng.bytes(16), rng.bytes(12)), 5: (rng.bytes(16), rng.bytes(12))}
+    ks.update([5, 2], new[5][0] + new[2][0], new[5][1] + new[2][1])
+    for i, (k, v) in new.items():
+        keys[i], ivs[i] = k, v
+    lens = rng.integers(0, 3000, n)
+    recs = np.zeros(n, dtype=pa.RECORD_DTYPE)
+    recs["in_off"] = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    recs["out_off"] = recs["in_off"] + 16 * np.arange(n)
+    recs["len"], recs["seq"] = lens, rng.integers(0, 2**48, n)
+    recs["key_idx"] = np.sort(rng.integers(0, nkeys, n))
+    recs["aad_off"], recs["aad_len"] = 0, 13
+    pt = rng.bytes(int(lens.sum()))
+    aad = rng.bytes(13)
+    d_recs, d_in, d_aad, d_out = dev(recs), dev(np.frombuffer(pt, np.uint8)), dev(np.frombuffer(aad, np.uint8)), \
+        empty(int(lens.sum()) + 16 * n, 0xEE)
+    pa.seal_batch(ks, d_recs.data_ptr(), n, d_in.data_ptr(), d_aad.data_ptr(), d_out.data_ptr(),
+                  torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy().tobytes()
+    for r in recs:
+        o, ln, k = int(r["out_off"]), int(r["len"]), int(r["key_idx"])
+        want = ref.seal(keys[k], ivs[k], int(r["seq"]), aad, pt[int(r["in_off"]):int(r["in_off"]) + ln])
+        assert out[o:o + ln + 16] == want, (k, ln)
+    # an index outside the keyset is refused and leaves the keyset usable
+    with pytest.raises(pa.EngineError):
+        ks.update([7], rng.bytes(16), rng.bytes(12))
+    with pytest.raises(pa.EngineError):
+        ks.update([3, 3], rng.bytes(32), rng.bytes(24))
+    with pytest.raises(ValueError):
+        ks.update([1], rng.bytes(32), rng.bytes(12))
+    ks.free()

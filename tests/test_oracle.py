@@ -275,3 +275,28 @@ def test_tls13_record_layer_matches_oracle_framing(oracle, key_size):
         assert inner == data[pos:pos + ln] + bytes([23])
         pos += ln
     assert t.tls13_receive(key_size, secret, seq0, wire) == data
+
+
+@pytest.mark.skipif(not HAVE_TLS12_REF, reason="oracle/_ref/libtls12_ref.so not built")
+@pytest.mark.parametrize("key_size", [16, 32])
+def test_tls13_key_update_at_2_24_records(oracle, key_size):
+    # from enc.seq >= 2^24 ptls_send emits a KeyUpdate (handshake 24, request_update 0) under the old key at that seq,
+    # then seals the data under the next traffic secret from seq 0 (lib/picotls.c:6220-6232, :6193-6211)
+    from oracle import Tls12Ref
+
+    t = Tls12Ref()
+    rng = np.random.default_rng(310 + key_size)
+    secret = rng.bytes(32 if key_size == 16 else 48)
+    key, iv = t.tls13_keys(key_size, secret)
+    data = rng.bytes(20000)
+    seq0 = 2**24 + 7
+    wire, key2, iv2, seq_after = t.tls13_send_rekeyed(key_size, secret, seq0, data)
+    assert (key2, iv2) != (key, iv) and seq_after == 2
+    recs = parse_tls13_records(wire)
+    assert len(recs) == 3
+    assert oracle.open(key, iv, seq0, *recs[0]) == bytes([24, 0, 0, 1, 0, 22])
+    assert oracle.open(key2, iv2, 0, *recs[1]) + oracle.open(key2, iv2, 1, *recs[2]) == data[:16384] + b"\x17" + data[16384:] + b"\x17"
+    assert t.tls13_receive(key_size, secret, seq0, wire) == data
+    # below 2^24 nothing changes
+    w, k, v, s = t.tls13_send_rekeyed(key_size, secret, 2**24 - 1, data)
+    assert (k, v, s) == (key, iv, 2**24 + 1) and len(parse_tls13_records(w)) == 2
