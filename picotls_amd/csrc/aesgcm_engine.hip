@@ -85,7 +85,8 @@ __constant__ SboxTable c_sbox = make_sbox();
 struct KeyEntry {
     u32 rk[15][4];  // round keys, LE column words
     u32 iv[4];      // static IV as LE words (word 3 = 0)
-    u32 h[16][4];   // GHASH elements (LE words): [0..7] = H^1..H^8, [8] = H^CHUNK_BLOCKS, [9..15] = 0
+    u32 h[16][4];   // GHASH elements (LE words): [0..7] = H^1..H^8, [8] = H^CHUNK_BLOCKS, [9..11] = H^16, H^32, H^64
+                    // (the combine powers of smaller units), [12..15] = 0
 };
 static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 
@@ -112,10 +113,11 @@ static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 #define CHUNK_BLOCKS 128  // 2 KiB units: 64K-key mixed +3 %, one-key mixed +7 % over 1 KiB units (interleaved A/B); 256: +1 % / +10 %
 #endif
 #define CHUNK_STEPS (CHUNK_BLOCKS / ENGINE_G)
+#define CHUNK_LOG2 (__builtin_ctz(CHUNK_STEPS))
 #ifndef CHUNK_MAX_UNITS
 #define CHUNK_MAX_UNITS CRUN_UNITS  // records longer than this many units (> ~2 MiB) run as one unit
 #endif
-#define BKT_STRIDE (CHUNK_STEPS + 1)             // per-wave front-unit bucket counters in s_ctl
+#define BKT_STRIDE (CHUNK_STEPS + 1)             // per-wave front-unit bucket counters in s_ctl (<= 32)
 #define CRUN_RECS 256        // records per run (one key)
 #ifndef CRUN_UNITS
 #define CRUN_UNITS 1024      // units per run
@@ -133,6 +135,7 @@ static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 #define CLDS_ALLOC (CLDS_FRONT + 4 * CRUN_RECS)
 static_assert(CLDS_ALLOC <= 160 * 1024, "chunked schedule LDS budget");
 static_assert(CHUNK_BLOCKS % ENGINE_G == 0, "units are whole steps");
+static_assert((CHUNK_STEPS & (CHUNK_STEPS - 1)) == 0 && CHUNK_STEPS <= 16, "unit lengths are powers of two up to 16 steps");
 
 
 // ------------------------------------------------------------------------------------------------ small helpers
@@ -265,16 +268,18 @@ __global__ void keyset_setup_kernel(const uint8_t *__restrict__ keys, const uint
     const u32 h0 = bswap32(s[0]), h1 = bswap32(s[1]), h2 = bswap32(s[2]), h3 = bswap32(s[3]);
     const u32 hb[4] = {h0, h1, h2, h3};
     u32 p[4] = {h0, h1, h2, h3};  // current power, big-endian words
-    for (int n = 1; n <= CHUNK_BLOCKS; ++n) {
+    for (int n = 1; n <= (CHUNK_BLOCKS > 64 ? CHUNK_BLOCKS : 64); ++n) {
         if (n <= 8)
             for (int c = 0; c < 4; ++c)
                 e->h[n - 1][c] = bswap32(p[c]);
-        if (n == CHUNK_BLOCKS)
+        if (n == CHUNK_BLOCKS || n == 16 || n == 32 || n == 64) {
+            const int slot = n == CHUNK_BLOCKS ? 8 : n == 16 ? 9 : n == 32 ? 10 : 11;
             for (int c = 0; c < 4; ++c)
-                e->h[8][c] = bswap32(p[c]);
+                e->h[slot][c] = bswap32(p[c]);
+        }
         gf_mul_be(p, hb);
     }
-    for (int n = 9; n < 16; ++n)
+    for (int n = 12; n < 16; ++n)
         for (int c = 0; c < 4; ++c)
             e->h[n][c] = 0;
 }
@@ -289,63 +294,83 @@ typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 __device__ void build_aes_tables(lds_u8 *lds)
 {
     lds_u32 *t = (lds_u32 *)lds;
-    for (u32 idx = threadIdx.x; idx < 256 * 64; idx += blockDim.x) {
-        u32 n = idx >> 6, slot = idx & 63;
-        u32 s = c_sbox.v[n];
-        u32 s2 = ((s << 1) ^ ((s & 0x80) ? 0x1b : 0)) & 0xff;
-        u32 te0 = s2 | s << 8 | s << 16 | (s2 ^ s) << 24;
-        t[idx] = slot < 32 ? te0 : ((te0 << 16) | (te0 >> 16));
+    // entry n = idx >> 6 is wave-uniform (blockDim.x is a multiple of 64): scalar S-box loads, 16 in flight per batch,
+    // so a launch pays one memory latency here instead of one per loop trip (the per-record path is a launch of one)
+    for (u32 base = 0; base < 256 * 64; base += 16 * blockDim.x) {
+        u32 sv[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            sv[k] = c_sbox.v[__builtin_amdgcn_readfirstlane((base + threadIdx.x + k * blockDim.x) >> 6) & 255u];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const u32 idx = base + threadIdx.x + k * blockDim.x, slot = idx & 63;
+            const u32 s = sv[k];
+            const u32 s2 = ((s << 1) ^ ((s & 0x80) ? 0x1b : 0)) & 0xff;
+            const u32 te0 = s2 | s << 8 | s << 16 | (s2 ^ s) << 24;
+            if (idx < 256 * 64)
+                t[idx] = slot < 32 ? te0 : ((te0 << 16) | (te0 >> 16));
+        }
     }
 }
 
-// (b0..b3) *= x^8 in GF(2^128), big-endian words: the 8 bits shifted out of b3 each inject the reduction 0xE1 << 120,
-// shifted by the steps left after them; those never reach b3 within 8 steps, so one pass suffices.
-__device__ __forceinline__ void gf_mulx8_be(u32 &b0, u32 &b1, u32 &b2, u32 &b3)
+// (b0..b3) *= x^s in GF(2^128), big-endian words (GCM bit order: the MSB of b0 is x^0), 1 <= s <= 32, in closed form:
+// bit i of the s bits shifted out of b3 is x^(127 - i) and comes back as x^(s - 1 - i) * (1 + x + x^2 + x^7), i.e. the
+// shifted-out bits land at the top of b0 ("1") and again 1, 2 and 7 bits further down, the last spilling into b1
+__device__ __forceinline__ void gf_mulxs_be(u32 &b0, u32 &b1, u32 &b2, u32 &b3, u32 s)
 {
-    const u32 n = b3 & 0xffu;
-    b3 = __builtin_amdgcn_alignbit(b2, b3, 8);
-    b2 = __builtin_amdgcn_alignbit(b1, b2, 8);
-    b1 = __builtin_amdgcn_alignbit(b0, b1, 8);
-    b0 >>= 8;
-    u32 r = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-        r ^= ((n >> k) & 1u) ? (0xE1000000u >> (7 - k)) : 0u;
-    b0 ^= r;
+    const u32 top = s == 32 ? b3 : b3 << (32 - s);
+    if (s == 32) {
+        b3 = b2, b2 = b1, b1 = b0, b0 = 0;
+    } else {
+        b3 = __builtin_amdgcn_alignbit(b2, b3, s);
+        b2 = __builtin_amdgcn_alignbit(b1, b2, s);
+        b1 = __builtin_amdgcn_alignbit(b0, b1, s);
+        b0 >>= s;
+    }
+    const u64 v = (u64)top << 32;
+    const u64 r = v ^ (v >> 1) ^ (v >> 2) ^ (v >> 7);
+    b0 ^= (u32)(r >> 32);
+    b1 ^= (u32)r;
 }
 
 // GHASH window tables of one key: table t (element key->h[t]), window p (x^(4p)..x^(4p+3)), entry n (4-bit value,
 // MSB = coefficient of x^(4p)) = sum over set bits of n of x^(4p+q) * h[t]. Thread (t, p) derives V_0 = x^(4p) h[t]
-// with byte steps (x^8) and at most one nibble step, V_1..V_3 by single steps, and writes the window's 16 entries
-// (rotated by p so the threads of a wave spread over the banks).
-__device__ void build_ghash_tables(lds_u8 *lds, const KeyEntry *__restrict__ key, u32 ntables = ENGINE_G)
+// with at most three 32-bit steps and one step of 4 (p mod 8) bits, V_1..V_3 by single steps, and writes the window's
+// 16 entries. Entries are GF(2)-linear in n, so the XOR combinations are formed after the byte swap back to memory
+// order, and entry n ^ c = e(n) ^ e(c): at store n a lane writes slot n ^ (p mod 16), spreading a wave's 16-byte stores
+// over the bank groups. A few hundred VALU operations per thread: the build is a small part of a launch of one record.
+__device__ void build_ghash_tables(lds_u8 *lds, const KeyEntry *__restrict__ key, u32 ntables = ENGINE_G, u32 src8 = 8)
 {
     for (u32 idx = threadIdx.x; idx < ntables * 32; idx += blockDim.x) {
         const u32 t = idx >> 5, p = idx & 31;
-        u32 v[4][4];
-        u32 b0 = bswap32(key->h[t][0]), b1 = bswap32(key->h[t][1]), b2 = bswap32(key->h[t][2]), b3 = bswap32(key->h[t][3]);
-        for (u32 k = 0; k < (p >> 1); ++k)
-            gf_mulx8_be(b0, b1, b2, b3);
-        if (p & 1)
-            for (int k = 0; k < 4; ++k)
-                gf_mulx_be(b0, b1, b2, b3);
+        const u32 *h = key->h[t == 8 ? src8 : t];  // table 8: the unit combine power (chunked kernel)
+        u32 b0 = bswap32(h[0]), b1 = bswap32(h[1]), b2 = bswap32(h[2]), b3 = bswap32(h[3]);
+        for (u32 k = 0; k < (p >> 3); ++k)
+            gf_mulxs_be(b0, b1, b2, b3, 32);
+        if (p & 7)
+            gf_mulxs_be(b0, b1, b2, b3, 4 * (p & 7));
+        u32x4 v[4];
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
-            v[m][0] = b0, v[m][1] = b1, v[m][2] = b2, v[m][3] = b3;
-            gf_mulx_be(b0, b1, b2, b3);
+            v[m] = u32x4{bswap32(b0), bswap32(b1), bswap32(b2), bswap32(b3)};
+            if (m < 3)
+                gf_mulxs_be(b0, b1, b2, b3, 1);
         }
+        const u32 c = p & 15;
+        u32x4 ec = {0, 0, 0, 0};
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            if ((c >> (3 - m)) & 1u)
+                ec ^= v[m];
         lds_u32x4 *row = (lds_u32x4 *)(lds + LDS_AES_BYTES + t * GHASH_TABLE_BYTES + p * 256);
 #pragma unroll
-        for (u32 i = 0; i < 16; ++i) {
-            const u32 n = (i + p) & 15;
-            u32 e0 = 0, e1 = 0, e2 = 0, e3 = 0;
+        for (u32 n = 0; n < 16; ++n) {
+            u32x4 e = ec;
 #pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const u32 msk = 0u - ((n >> (3 - m)) & 1u);
-                e0 ^= v[m][0] & msk, e1 ^= v[m][1] & msk, e2 ^= v[m][2] & msk, e3 ^= v[m][3] & msk;
-            }
-            const u32x4 ent = {bswap32(e0), bswap32(e1), bswap32(e2), bswap32(e3)};
-            row[n] = ent;
+            for (int m = 0; m < 4; ++m)
+                if ((n >> (3 - m)) & 1u)
+                    e ^= v[m];
+            row[n ^ c] = e;
         }
     }
 }
@@ -563,6 +588,7 @@ struct BatchArgs {
     uint8_t *ok;
     u32 multi_key;  // 0: every record uses key 0 (no key-run scan)
     u32 nkeys;      // records whose key_idx >= nkeys are skipped (open: ok = 0)
+    u32 unit_log2;  // chunked kernel: units of 2^unit_log2 steps (<= CHUNK_STEPS; smaller for a launch of one record)
 };
 
 #define RUN_SCAN_CAP 256  // records examined per key-run scan (multi-key batches)
@@ -892,7 +918,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
 }
 
 // Diagnostic build only (-DENGINE_PROFILE=1): s_memtime stamps of the chunked kernel's phases, summed over runs and
-// workgroups: [0] run setup, [1] GHASH table build, [2] unit loop, [3] -, [4] wave idle at the unit-loop barrier,
+// workgroups: [0] run setup, [1] GHASH table build, [2] unit loop, [3] kernel prologue (AES tables), [4] wave idle at the unit-loop barrier,
 // [5] units, [6] runs, [7] table builds.
 #ifndef ENGINE_PROFILE
 #define ENGINE_PROFILE 0
@@ -929,6 +955,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     lds_u8 *lds = (lds_u8 *)smem;
     check_lds_base(smem);
+    PROF_STAMP(tk);
     // s_ctl: [1] next unit, [4..7] per-wave unit totals, [8..11] per-wave key boundary, [12..15] per-wave unit cut,
     // [16..19] / [20..23] per-wave min / max steps, [32 + 16 w + b] per-wave count of front-unit bucket b
     lds_u32 *s_front = (lds_u32 *)(lds + CLDS_FRONT);
@@ -941,8 +968,6 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     constexpr int RPW = 64 / G;
     constexpr u32 SCAN_WAVES = CRUN_RECS / 64;
 
-    build_aes_tables(lds);
-
     const u32 lane = threadIdx.x & 63;
     const u32 j = lane % G;
     const u32 slot = lane / G;
@@ -951,10 +976,15 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     const u32 tsel_horner = 0x10000u + (u32)(G - 1) * GHASH_TABLE_BYTES;
     const u32 tsel_last = 0x10000u + (u32)(G - 1 - j) * GHASH_TABLE_BYTES;
     const u32 tsel_chunk = 0x10000u + 8u * GHASH_TABLE_BYTES;
+    // unit length in steps (a power of two <= CHUNK_STEPS) and the key element of its combine power H^(G * ustep)
+    const u32 ustep = 1u << args.unit_log2;
+    const u32 usrc = ustep == CHUNK_STEPS ? 8u : args.unit_log2 == 0 ? 7u : 8u + args.unit_log2;
 
     const u64 n = args.nrecs;
     const u64 beg = n * blockIdx.x / gridDim.x, end = n * (blockIdx.x + 1) / gridDim.x;
     u32 loaded_key = 0xffffffffu;
+
+    build_aes_tables(lds);
 
     for (u64 pos = beg; pos < end;) {
         PROF_STAMP(t0);
@@ -970,10 +1000,10 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             if (t < lim) {
                 const ptls_mi355x_record_t r = args.recs[pos + t];
                 const u32 steps = gcm_steps<OPEN, FRAME>(r);
-                nc = (steps + CHUNK_STEPS - 1) / CHUNK_STEPS;
-                // front-unit size bucket: 0 = very long record run whole (nc forced to 1), else CHUNK_STEPS + 1 -
-                // size of the record's first unit (1 = a full unit, CHUNK_STEPS = one step)
-                bkt = CHUNK_STEPS + 1 - (steps - (nc - 1) * CHUNK_STEPS);
+                nc = (steps + ustep - 1) >> args.unit_log2;
+                // front-unit size bucket: 0 = very long record run whole (nc forced to 1), else ustep + 1 - size of
+                // the record's first unit (1 = a full unit, ustep = one step)
+                bkt = ustep + 1 - (steps - (nc - 1) * ustep);
                 if (nc > CHUNK_MAX_UNITS)
                     nc = 1, bkt = 0;
                 other_key = args.multi_key && r.key_idx != key_idx;
@@ -1050,15 +1080,27 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 }
             }
             __syncthreads();
-            if (wave < SCAN_WAVES && threadIdx.x < run_n) {
-                u32 base = rank;
-                for (u32 b = 0; b < bkt; ++b)
+            if (wave < SCAN_WAVES) {
+                // lane b: first slot of this wave's bucket-b records = all records of earlier buckets (prefix over
+                // lanes) + bucket b of earlier waves; a record then takes lane bkt's value (no serial walk)
+                u32 tot = 0, mine = 0;
 #pragma unroll
-                    for (u32 w = 0; w < SCAN_WAVES; ++w)
-                        base += s_ctl[32 + BKT_STRIDE * w + b];
-                for (u32 w = 0; w < wave; ++w)
-                    base += s_ctl[32 + BKT_STRIDE * w + bkt];
-                s_front[base] = threadIdx.x;
+                for (u32 w = 0; w < SCAN_WAVES; ++w) {
+                    const u32 c = lane < BKT_STRIDE ? s_ctl[32 + BKT_STRIDE * w + lane] : 0u;
+                    tot += c;
+                    mine += w < wave ? c : 0u;
+                }
+                u32 before = tot;
+#pragma unroll
+                for (int off = 1; off < 32; off <<= 1) {
+                    const u32 y = (u32)__shfl_up((int)before, off, 64);
+                    if (lane >= (u32)off)
+                        before += y;
+                }
+                const u32 first_slot = before - tot + mine;
+                const u32 base = (u32)__shfl((int)first_slot, (int)bkt, 64);
+                if (threadIdx.x < run_n)
+                    s_front[base + rank] = threadIdx.x;
             }
 #pragma unroll
             for (u32 w = 0; w < SCAN_WAVES; ++w)
@@ -1079,7 +1121,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             continue;
         }
         if (key_idx != loaded_key) {
-            build_ghash_tables(lds, args.keys + key_idx, 9);  // H^1..H^8 and H^CHUNK_BLOCKS
+            build_ghash_tables(lds, args.keys + key_idx, 9, usrc);  // H^1..H^8 and the unit combine power
             __syncthreads();
             loaded_key = key_idx;
             if (threadIdx.x == 0)
@@ -1134,8 +1176,8 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             if (valid)
                 r = args.recs[pos + ri];
             const u32 steps = gcm_steps<OPEN, FRAME>(r);
-            u32 m_hi = steps - k_back * CHUNK_STEPS;
-            u32 m_lo = k_back + 1 == unc ? 0u : m_hi - CHUNK_STEPS;
+            u32 m_hi = steps - k_back * ustep;
+            u32 m_lo = k_back + 1 == unc ? 0u : m_hi - ustep;
             if (!valid)
                 m_lo = m_hi = 0;
             u32x4 acc, ek0;
@@ -1152,7 +1194,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 }
                 last = dpp_bcast7(last, lane);
                 if (last) {
-                    // last unit of the record: GHASH = Horner over the partials with H^CHUNK_BLOCKS (whole group)
+                    // last unit of the record: GHASH = Horner over the partials with H^(G * ustep) (whole group)
                     u32x4 g = s_part[first];
                     for (u32 i = 1; i < unc; ++i)
                         g = gmul_group(lds, g, tsel_chunk, j) ^ s_part[first + i];
@@ -1181,6 +1223,8 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             PROF_ADD(2, t3 - t2);
             PROF_ADD(5, total_units);
             PROF_ADD(6, 1);
+            if (pos == beg)
+                PROF_ADD(3, t0 - tk);
         }
 #endif
         pos = run_end;
@@ -1635,14 +1679,14 @@ int ptls_mi355x_keyset_set_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, const vo
 static bool use_chunked(const ptls_mi355x_keyset_t *ks) { return ks->schedule != PTLS_MI355X_SCHEDULE_LOCKSTEP; }
 
 static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
-                        const void *aad, void *out, uint8_t *ok, void *stream, int frame = 0)
+                        const void *aad, void *out, uint8_t *ok, void *stream, int frame = 0, u32 unit_log2 = CHUNK_LOG2)
 {
     if (ks == NULL || (nrecs != 0 && (recs == NULL || in == NULL || out == NULL || (open && ok == NULL))))
         return fail("%s", "batch: invalid arguments");
     if (nrecs == 0)
         return 0;
     BatchArgs a = {ks->d_keys, recs, (u64)nrecs, (const uint8_t *)in, (const uint8_t *)aad, (uint8_t *)out, ok,
-                   ks->nkeys > 1 ? 1u : 0u, (u32)ks->nkeys};
+                   ks->nkeys > 1 ? 1u : 0u, (u32)ks->nkeys, unit_log2};
     if (a.aad == NULL)
         a.aad = a.in;
     const u64 groups = (nrecs + (64 / ENGINE_G) - 1) / (64 / ENGINE_G);
@@ -1892,9 +1936,13 @@ static int single(ptls_mi355x_keyset_t *ks, size_t key_idx, bool open, void *out
     if (aadlen != 0)
         memcpy(h + off_aad, aad, aadlen);
     memcpy(h + off_rec, &r, sizeof(r));
+    // one record on one workgroup: shorter units put more of its waves to work (a unit step costs a lone wave ~2 us of
+    // latency, a unit combine ~0.15 us); steps / 2^k units balance the two
+    const size_t steps = ((aadlen + 15) / 16 + (len + 15) / 16 + 1 + ENGINE_G - 1) / ENGINE_G;
+    const u32 unit_log2 = steps <= 24 ? 0 : steps <= 96 ? 1 : steps <= 400 ? 2 : steps <= 1600 ? 3 : CHUNK_LOG2;
     if (stage_roundtrip(ks, off_out, off_out, total - off_out, [&] {
             return launch_batch(&view, open, (const ptls_mi355x_record_t *)(d + off_rec), 1, d + off_in, d + off_aad,
-                                d + off_out, d + off_ok, ks->stream);
+                                d + off_out, d + off_ok, ks->stream, 0, unit_log2 < CHUNK_LOG2 ? unit_log2 : CHUNK_LOG2);
         }) != 0)
         return -1;
     if (outbytes != 0)

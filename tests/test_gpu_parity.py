@@ -584,3 +584,27 @@ def test_picotls_vtable_pairs():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     assert "not ok" not in r.stdout
+
+
+@pytest.mark.parametrize("key_size", [16, 32])
+def test_per_record_path_every_unit_size_vs_fusion(ref, key_size):
+    # the per-record path (ptls_aead_encrypt / decrypt through the vtable = a launch of one record) cuts the record into
+    # units of 1, 2, 4, 8 or 16 steps by its length, each recombined with its own power H^(8 * steps); lengths across
+    # every choice and its boundaries, against fusion, plus a tampered tag
+    rng = np.random.default_rng(600 + key_size)
+    key, iv = rng.bytes(key_size), rng.bytes(12)
+    alg = pa.aes128gcm if key_size == 16 else pa.aes256gcm
+    enc = pa.aead_new_direct(alg, True, key, iv)
+    dec = pa.aead_new_direct(alg, False, key, iv)
+    # steps = ceil((ceil(A/16) + ceil(L/16) + 1) / 8) with A = 13: switch points 24 / 96 / 400 / 1600 steps
+    lens = [0, 1, 100, 1200, 2900, 2950, 3000, 12000, 12300, 16384, 16640, 51000, 51300, 60000, 204700, 204900, 300000,
+            1 << 20]
+    for ln in lens:
+        pt, aad, seq = rng.bytes(ln), rng.bytes(13), int(rng.integers(0, 2**48))
+        want = ref.seal(key, iv, seq, aad, pt)
+        got = enc.encrypt(pt, seq, aad)
+        assert got == want, ln
+        assert dec.decrypt(want, seq, aad) == pt, ln
+        bad = bytearray(want)
+        bad[-1] ^= 0x40
+        assert dec.decrypt(bytes(bad), seq, aad) is None, ln

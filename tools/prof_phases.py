@@ -54,7 +54,7 @@ def main():
     tot = p[0] + p[1] + p[2] + p[3]
     print(f"{a.workload} n={a.records} schedule={a.schedule}: seal {ms:.3f} ms, runs/launch {p[6] / a.reps:.0f}, "
           f"units/run {p[5] / runs:.1f}, table builds/launch {p[7] / a.reps:.0f}")
-    for i, name in enumerate(["run setup", "table build", "unit loop", "combine"]):
+    for i, name in enumerate(["run setup", "table build", "unit loop", "prologue"]):
         print(f"  {name:12s} {p[i] / runs:10.0f} cycles/run  {100 * p[i] / max(tot, 1):5.1f} %")
     waves = 16
     print(f"  wave idle at unit-loop barrier: {p[4] / runs / waves:.0f} cycles/run/wave "
