@@ -823,6 +823,10 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     }
 }
 
+// Descriptors whose len exceeds PTLS_MI355X_MAX_RECORD_LEN are rejected as a whole: nothing is written for them and an
+// open reports ok = 0, so a corrupt length cannot make the kernel address memory far past the record's offsets.
+__device__ __forceinline__ bool record_len_ok(const ptls_mi355x_record_t &r) { return r.len <= PTLS_MI355X_MAX_RECORD_LEN; }
+
 // Seals / opens one whole record per G-lane group.
 template <int NR, bool OPEN, int NB>
 __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u8 *lds, const u32 (&rk)[NR + 1][4], u32 iv0,
@@ -833,6 +837,11 @@ __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u
     ptls_mi355x_record_t r = {};
     if (valid)
         r = args.recs[rec];
+    if (valid && !record_len_ok(r)) {
+        if (OPEN && j == 0)
+            args.ok[rec] = 0;
+        valid = false;
+    }
     const u32 K = valid ? gcm_steps<OPEN, 0>(r) : 0;
     u32x4 acc, ek0;
     gcm_segment<NR, OPEN, NB>(args, lds, rk, iv0, iv1, iv2, r, valid, 0, K, j, laneoff, tsel_horner, tsel_last, acc, ek0,
@@ -998,7 +1007,9 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             bool other_key = false;
             u32 smin = 0xffffffffu, smax = 0;
             if (t < lim) {
-                const ptls_mi355x_record_t r = args.recs[pos + t];
+                ptls_mi355x_record_t r = args.recs[pos + t];
+                if (!record_len_ok(r))  // rejected: one empty unit (see the unit loop)
+                    r.len = 0, r.aad_len = 0;
                 const u32 steps = gcm_steps<OPEN, FRAME>(r);
                 nc = (steps + ustep - 1) >> args.unit_log2;
                 // front-unit size bucket: 0 = very long record run whole (nc forced to 1), else ustep + 1 - size of
@@ -1175,15 +1186,21 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             ptls_mi355x_record_t r = {};
             if (valid)
                 r = args.recs[pos + ri];
+            const bool live = valid && record_len_ok(r);
+            if (valid && !live) {  // rejected length: the scan gave it one unit; nothing is written
+                r.len = 0, r.aad_len = 0;
+                if (OPEN && j == 0)
+                    args.ok[pos + ri] = 0;
+            }
             const u32 steps = gcm_steps<OPEN, FRAME>(r);
             u32 m_hi = steps - k_back * ustep;
             u32 m_lo = k_back + 1 == unc ? 0u : m_hi - ustep;
-            if (!valid)
+            if (!live)
                 m_lo = m_hi = 0;
             u32x4 acc, ek0;
-            gcm_segment<NR, OPEN, 1, FRAME>(args, lds, rk, iv0, iv1, iv2, r, valid, m_lo, m_hi, j, laneoff, tsel_horner,
+            gcm_segment<NR, OPEN, 1, FRAME>(args, lds, rk, iv0, iv1, iv2, r, live, m_lo, m_hi, j, laneoff, tsel_horner,
                                      tsel_last, acc, ek0, unc == 1, pos + ri);
-            if (valid && unc > 1) {  // uniform over the group
+            if (live && unc > 1) {  // uniform over the group
                 u32 last = 0;
                 if (j == G - 1) {
                     s_part[first + unc - 1 - k_back] = acc;  // stream order: the front unit first

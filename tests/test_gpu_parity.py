@@ -608,3 +608,37 @@ def test_per_record_path_every_unit_size_vs_fusion(ref, key_size):
         bad = bytearray(want)
         bad[-1] ^= 0x40
         assert dec.decrypt(bytes(bad), seq, aad) is None, ln
+
+
+@pytest.mark.parametrize("schedule", ["lockstep", "chunked"])
+def test_over_long_descriptor_rejected(ref, schedule):
+    # a descriptor whose len exceeds PTLS_MI355X_MAX_RECORD_LEN (corrupt, or up to 2^32 - 1) is rejected as a whole:
+    # nothing is written for it, open reports ok = 0, and the other records of the batch are unaffected
+    rng = np.random.default_rng(610)
+    n = 40
+    lens = rng.integers(0, 3000, n)
+    b = RecordBatch.build(lens, rng.integers(0, 30, n), seqs=rng.integers(0, 2**40, n, dtype=np.uint64))
+    keys, ivs = np.frombuffer(rng.bytes(16), np.uint8), np.frombuffer(rng.bytes(12), np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(b.aad_bytes), np.uint8)
+    expect = np.zeros(b.sealed_bytes, np.uint8)
+    ref.run_batch(True, keys, ivs, 16, b.seal, pt, aad, expect, nthreads=2)
+    bad = [3, 17, 39]
+    seal, opn = b.seal.copy(), b.open.copy()
+    for i, v in zip(bad, [(1 << 24) + 1, 0xFFFFFFFF, 0xFFFFFFF0]):
+        seal[i]["len"] = opn[i]["len"] = v
+    ks = pa.Keyset(keys, ivs, 16)
+    ks.set_schedule(schedule)
+    sealed = gpu_seal(ks, seal, pt, aad, b.sealed_bytes, out_fill=0xEE)
+    for i, r in enumerate(b.seal):
+        o, ln = int(r["out_off"]), int(r["len"]) + 16
+        if i in bad:
+            assert (sealed[o:o + ln] == 0xEE).all(), i
+        else:
+            assert np.array_equal(sealed[o:o + ln], expect[o:o + ln]), i
+    plain, ok = gpu_open(ks, opn, expect, aad, b.pt_bytes, out_fill=0x55)
+    assert [int(x) for x in ok] == [0 if i in bad else 1 for i in range(n)]
+    for i, r in enumerate(b.open):
+        o, ln = int(r["out_off"]), int(r["len"])
+        want = np.full(ln, 0x55, np.uint8) if i in bad else pt[int(b.seal[i]["in_off"]):int(b.seal[i]["in_off"]) + ln]
+        assert np.array_equal(plain[o:o + ln], want), i
