@@ -48,8 +48,9 @@ extern "C" {
  *         writes out[out_off .. out_off+len)         plaintext            (out may alias in)
  *   aad:  aad[aad_off .. aad_off+aad_len)
  *   nonce = static_iv(key_idx) ^ (0^32 || seq big-endian)        (lib/picotls.c:6587-6601, lib/fusion.c:1127-1134)
- * len is at most PTLS_MI355X_MAX_RECORD_LEN: a record with a larger len is rejected (nothing is written for it; open
- * reports ok = 0), so a corrupt descriptor cannot address memory beyond the offsets it names.
+ * len is at most PTLS_MI355X_MAX_RECORD_LEN and key_idx is below the keyset size: a record with a larger len or key_idx
+ * is rejected (nothing is written for it; open reports ok = 0), so a corrupt descriptor cannot address memory beyond
+ * the offsets it names.
  */
 typedef struct st_ptls_mi355x_record_t {
     uint64_t in_off;

@@ -823,9 +823,13 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     }
 }
 
-// Descriptors whose len exceeds PTLS_MI355X_MAX_RECORD_LEN are rejected as a whole: nothing is written for them and an
-// open reports ok = 0, so a corrupt length cannot make the kernel address memory far past the record's offsets.
-__device__ __forceinline__ bool record_len_ok(const ptls_mi355x_record_t &r) { return r.len <= PTLS_MI355X_MAX_RECORD_LEN; }
+// Descriptors whose len exceeds PTLS_MI355X_MAX_RECORD_LEN or whose key_idx is not below the keyset size are rejected
+// as a whole: nothing is written for them and an open reports ok = 0, so a corrupt length cannot make the kernel address
+// memory far past the record's offsets. (Multi-key batches also reject invalid keys per key run, before any table build.)
+__device__ __forceinline__ bool record_ok(const BatchArgs &args, const ptls_mi355x_record_t &r)
+{
+    return r.len <= PTLS_MI355X_MAX_RECORD_LEN && r.key_idx < args.nkeys;
+}
 
 // Seals / opens one whole record per G-lane group.
 template <int NR, bool OPEN, int NB>
@@ -837,7 +841,7 @@ __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u
     ptls_mi355x_record_t r = {};
     if (valid)
         r = args.recs[rec];
-    if (valid && !record_len_ok(r)) {
+    if (valid && !record_ok(args, r)) {
         if (OPEN && j == 0)
             args.ok[rec] = 0;
         valid = false;
@@ -1008,7 +1012,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             u32 smin = 0xffffffffu, smax = 0;
             if (t < lim) {
                 ptls_mi355x_record_t r = args.recs[pos + t];
-                if (!record_len_ok(r))  // rejected: one empty unit (see the unit loop)
+                if (!record_ok(args, r))  // rejected: one empty unit (see the unit loop)
                     r.len = 0, r.aad_len = 0;
                 const u32 steps = gcm_steps<OPEN, FRAME>(r);
                 nc = (steps + ustep - 1) >> args.unit_log2;
@@ -1186,8 +1190,8 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             ptls_mi355x_record_t r = {};
             if (valid)
                 r = args.recs[pos + ri];
-            const bool live = valid && record_len_ok(r);
-            if (valid && !live) {  // rejected length: the scan gave it one unit; nothing is written
+            const bool live = valid && record_ok(args, r);
+            if (valid && !live) {  // rejected descriptor: the scan gave it one unit; nothing is written
                 r.len = 0, r.aad_len = 0;
                 if (OPEN && j == 0)
                     args.ok[pos + ri] = 0;

@@ -611,9 +611,10 @@ def test_per_record_path_every_unit_size_vs_fusion(ref, key_size):
 
 
 @pytest.mark.parametrize("schedule", ["lockstep", "chunked"])
-def test_over_long_descriptor_rejected(ref, schedule):
-    # a descriptor whose len exceeds PTLS_MI355X_MAX_RECORD_LEN (corrupt, or up to 2^32 - 1) is rejected as a whole:
-    # nothing is written for it, open reports ok = 0, and the other records of the batch are unaffected
+def test_invalid_descriptor_rejected(ref, schedule):
+    # a descriptor whose len exceeds PTLS_MI355X_MAX_RECORD_LEN (corrupt, or up to 2^32 - 1) or whose key_idx is not in
+    # the keyset is rejected as a whole: nothing is written for it, open reports ok = 0, and the other records of the
+    # batch are unaffected
     rng = np.random.default_rng(610)
     n = 40
     lens = rng.integers(0, 3000, n)
@@ -623,10 +624,11 @@ def test_over_long_descriptor_rejected(ref, schedule):
     aad = np.frombuffer(rng.bytes(b.aad_bytes), np.uint8)
     expect = np.zeros(b.sealed_bytes, np.uint8)
     ref.run_batch(True, keys, ivs, 16, b.seal, pt, aad, expect, nthreads=2)
-    bad = [3, 17, 39]
+    bad = [3, 17, 39, 25]
     seal, opn = b.seal.copy(), b.open.copy()
     for i, v in zip(bad, [(1 << 24) + 1, 0xFFFFFFFF, 0xFFFFFFF0]):
         seal[i]["len"] = opn[i]["len"] = v
+    seal[25]["key_idx"] = opn[25]["key_idx"] = 5  # a one-key keyset: key 5 does not exist
     ks = pa.Keyset(keys, ivs, 16)
     ks.set_schedule(schedule)
     sealed = gpu_seal(ks, seal, pt, aad, b.sealed_bytes, out_fill=0xEE)
