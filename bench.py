@@ -235,6 +235,17 @@ def cpu_baseline(wl, seconds: float):
         if time.perf_counter() - start > seconds or reps >= 50:
             break
     gib = 2 * b.payload_bytes * reps / 2**30
+    # one core (1 thread and all cores), on a 1/8 slice of the same sample for ~3 s
+    n1 = max(1, b.n // 8)
+    b1 = wl.descriptors(0, n1)
+    t1, reps1, start1 = 0.0, 0, time.perf_counter()
+    while reps1 < 50 and (reps1 == 0 or time.perf_counter() - start1 < 3.0):
+        ts, _ = ref.run_batch(True, keys, ivs, wl.key_size, b1.seal, pt, aad, sealed, nthreads=1, cpus=cpus[:1])
+        to, fails = ref.run_batch(False, keys, ivs, wl.key_size, b1.open, sealed, aad, back, ok=ok, nthreads=1,
+                                  cpus=cpus[:1])
+        assert fails == 0
+        t1 += ts + to
+        reps1 += 1
     model = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -248,7 +259,8 @@ def cpu_baseline(wl, seconds: float):
                       f"seal+open x{reps}, ptls_fusion_aes{8 * wl.key_size}gcm via ptls_aead_encrypt/decrypt, "
                       f"{nthreads} pinned threads, CLOCK_MONOTONIC; CPU: {model}",
             "seal_GiBps": round(b.payload_bytes * reps / 2**30 / t_seal, 3),
-            "open_GiBps": round(b.payload_bytes * reps / 2**30 / t_open, 3)}
+            "open_GiBps": round(b.payload_bytes * reps / 2**30 / t_open, 3),
+            "single_thread_GiBps": round(2 * b1.payload_bytes * reps1 / 2**30 / t1, 3)}
 
 
 def run_e2e(R, wl, nchunks: int = 16, reps: int = 3, schedule: str = "auto"):
