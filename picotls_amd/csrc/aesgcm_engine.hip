@@ -115,7 +115,7 @@ static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 #define CHUNK_STEPS (CHUNK_BLOCKS / ENGINE_G)
 #define CHUNK_LOG2 (__builtin_ctz(CHUNK_STEPS))
 #ifndef CHUNK_MAX_UNITS
-#define CHUNK_MAX_UNITS CRUN_UNITS  // records longer than this many units (> ~2 MiB) run as one unit
+#define CHUNK_MAX_UNITS CRUN_UNITS  // records longer than this many units (> ~2 MiB) use units of a multiple length
 #endif
 #define BKT_STRIDE (CHUNK_STEPS + 1)             // per-wave front-unit bucket counters in s_ctl (<= 32)
 #define CRUN_RECS 256        // records per run (one key)
@@ -823,6 +823,15 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     }
 }
 
+// Unit length multiplier of a record of `steps` steps: 1, or for a record that would need more than CHUNK_MAX_UNITS units
+// of 2^log2 steps the least factor that fits it in CHUNK_MAX_UNITS (its partials are then combined with the unit power
+// applied mul times). Records up to PTLS_MI355X_MAX_RECORD_LEN thus always spread over the workgroup.
+__device__ __forceinline__ u32 unit_mul(u32 steps, u32 log2)
+{
+    const u32 nc = (steps + (1u << log2) - 1) >> log2;
+    return nc > CHUNK_MAX_UNITS ? (nc + CHUNK_MAX_UNITS - 1) / CHUNK_MAX_UNITS : 1u;
+}
+
 // Descriptors whose len exceeds PTLS_MI355X_MAX_RECORD_LEN or whose key_idx is not below the keyset size are rejected
 // as a whole: nothing is written for them and an open reports ok = 0, so a corrupt length cannot make the kernel address
 // memory far past the record's offsets. (Multi-key batches also reject invalid keys per key run, before any table build.)
@@ -1015,12 +1024,12 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 if (!record_ok(args, r))  // rejected: one empty unit (see the unit loop)
                     r.len = 0, r.aad_len = 0;
                 const u32 steps = gcm_steps<OPEN, FRAME>(r);
-                nc = (steps + ustep - 1) >> args.unit_log2;
-                // front-unit size bucket: 0 = very long record run whole (nc forced to 1), else ustep + 1 - size of
-                // the record's first unit (1 = a full unit, ustep = one step)
-                bkt = ustep + 1 - (steps - (nc - 1) * ustep);
-                if (nc > CHUNK_MAX_UNITS)
-                    nc = 1, bkt = 0;
+                // front-unit size bucket: 0 = a record too long for CHUNK_MAX_UNITS units (it takes units of a
+                // multiple length, unit_mul), else ustep + 1 - size of the record's first unit (1 = a full unit, ustep =
+                // one step)
+                const u32 mul = unit_mul(steps, args.unit_log2);
+                nc = (steps + mul * ustep - 1) / (mul * ustep);
+                bkt = mul > 1 ? 0u : ustep + 1 - (steps - (nc - 1) * ustep);
                 other_key = args.multi_key && r.key_idx != key_idx;
                 if (!other_key)
                     smin = smax = steps;
@@ -1197,8 +1206,9 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                     args.ok[pos + ri] = 0;
             }
             const u32 steps = gcm_steps<OPEN, FRAME>(r);
-            u32 m_hi = steps - k_back * ustep;
-            u32 m_lo = k_back + 1 == unc ? 0u : m_hi - ustep;
+            const u32 mul = unit_mul(steps, args.unit_log2), ulen = mul * ustep;
+            u32 m_hi = steps - k_back * ulen;
+            u32 m_lo = k_back + 1 == unc ? 0u : m_hi - ulen;
             if (!live)
                 m_lo = m_hi = 0;
             u32x4 acc, ek0;
@@ -1215,10 +1225,14 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 }
                 last = dpp_bcast7(last, lane);
                 if (last) {
-                    // last unit of the record: GHASH = Horner over the partials with H^(G * ustep) (whole group)
+                    // last unit of the record: GHASH = Horner over the partials with H^(G * ulen) = (H^(G * ustep))^mul
+                    // (whole group)
                     u32x4 g = s_part[first];
-                    for (u32 i = 1; i < unc; ++i)
-                        g = gmul_group(lds, g, tsel_chunk, j) ^ s_part[first + i];
+                    for (u32 i = 1; i < unc; ++i) {
+                        for (u32 t = 0; t < mul; ++t)
+                            g = gmul_group(lds, g, tsel_chunk, j);
+                        g ^= s_part[first + i];
+                    }
                     const u32x4 tag = g ^ s_ek0[ri];
                     if (j != G - 1) {
                     } else if (OPEN) {

@@ -644,3 +644,31 @@ def test_invalid_descriptor_rejected(ref, schedule):
         o, ln = int(r["out_off"]), int(r["len"])
         want = np.full(ln, 0x55, np.uint8) if i in bad else pt[int(b.seal[i]["in_off"]):int(b.seal[i]["in_off"]) + ln]
         assert np.array_equal(plain[o:o + ln], want), i
+
+
+def test_records_beyond_1024_units_chunked(ref):
+    # records needing more than 1024 units of 2 KiB (> 2 MiB) take units of a multiple length (their partials combined
+    # with the unit power applied that many times) instead of running whole on one group; up to
+    # PTLS_MI355X_MAX_RECORD_LEN, next to ordinary records in the same run, sealed and opened (one tampered)
+    rng = np.random.default_rng(620)
+    lens = [3 << 20, 16384, (5 << 20) + 7, (2 << 20) + 1, 1 << 24, 1200, (2 << 20) - 40]
+    n = len(lens)
+    b = RecordBatch.build(lens, [13] * n, seqs=rng.integers(0, 2**40, n, dtype=np.uint64))
+    keys, ivs = np.frombuffer(rng.bytes(32), np.uint8), np.frombuffer(rng.bytes(12), np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(b.aad_bytes), np.uint8)
+    ks = pa.Keyset(keys, ivs, 32)
+    ks.set_schedule("chunked")
+    sealed = gpu_seal(ks, b.seal, pt, aad, b.sealed_bytes)
+    expect = np.zeros(b.sealed_bytes, np.uint8)
+    ref.run_batch(True, keys, ivs, 32, b.seal, pt, aad, expect, nthreads=4)
+    assert np.array_equal(sealed, expect)
+    bad = expect.copy()
+    bad[int(b.seal[4]["out_off"]) + 12345] ^= 1
+    plain, ok = gpu_open(ks, b.open, bad, aad, b.pt_bytes)
+    assert [int(x) for x in ok] == [1, 1, 1, 1, 0, 1, 1]
+    want = pt.copy()
+    want[int(b.seal[4]["in_off"]) + 12345] ^= 1  # plaintext is written regardless, like fusion (CTR: the flipped bit)
+    for r in b.open:
+        o, ln = int(r["out_off"]), int(r["len"])
+        assert np.array_equal(plain[o:o + ln], want[o:o + ln]), ln
