@@ -1028,7 +1028,9 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 // multiple length, unit_mul), else ustep + 1 - size of the record's first unit (1 = a full unit, ustep =
                 // one step)
                 const u32 mul = unit_mul(steps, args.unit_log2);
-                nc = (steps + mul * ustep - 1) / (mul * ustep);
+                nc = (steps + ustep - 1) >> args.unit_log2;
+                if (mul > 1)  // rare: the only division
+                    nc = (steps + mul * ustep - 1) / (mul * ustep);
                 bkt = mul > 1 ? 0u : ustep + 1 - (steps - (nc - 1) * ustep);
                 other_key = args.multi_key && r.key_idx != key_idx;
                 if (!other_key)
@@ -1206,9 +1208,14 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                     args.ok[pos + ri] = 0;
             }
             const u32 steps = gcm_steps<OPEN, FRAME>(r);
-            const u32 mul = unit_mul(steps, args.unit_log2), ulen = mul * ustep;
-            u32 m_hi = steps - k_back * ulen;
-            u32 m_lo = k_back + 1 == unc ? 0u : m_hi - ulen;
+            // unit [m_lo, m_hi) of the record's steps (whole mode: the record); huge records take longer units
+            const u32 mul = whole ? 1u : unit_mul(steps, args.unit_log2);
+            u32 m_hi = steps, m_lo = 0;
+            if (!whole) {
+                const u32 ulen = mul * ustep;
+                m_hi = steps - k_back * ulen;
+                m_lo = k_back + 1 == unc ? 0u : m_hi - ulen;
+            }
             if (!live)
                 m_lo = m_hi = 0;
             u32x4 acc, ek0;
@@ -1229,7 +1236,8 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                     // (whole group)
                     u32x4 g = s_part[first];
                     for (u32 i = 1; i < unc; ++i) {
-                        for (u32 t = 0; t < mul; ++t)
+                        g = gmul_group(lds, g, tsel_chunk, j);
+                        for (u32 t = 1; t < mul; ++t)  // huge records only
                             g = gmul_group(lds, g, tsel_chunk, j);
                         g ^= s_part[first + i];
                     }
