@@ -83,7 +83,7 @@ __constant__ SboxTable c_sbox = make_sbox();
 
 // one keyset entry in HBM (512 bytes, 16-byte aligned)
 struct KeyEntry {
-    u32 rk[15][4];  // round keys, LE column words
+    u32 rk[15][4];  // round keys, LE column words; rounds 1..NR-1 stored rotated right by 8 bits (see aes_rounds_n)
     u32 iv[4];      // static IV as LE words (word 3 = 0)
     u32 h[16][4];   // GHASH elements (LE words): [0..7] = H^1..H^8, [8] = H^CHUNK_BLOCKS, [9..11] = H^16, H^32, H^64
                     // (the combine powers of smaller units), [12..15] = 0
@@ -142,6 +142,7 @@ static_assert((CHUNK_STEPS & (CHUNK_STEPS - 1)) == 0 && CHUNK_STEPS <= 16, "unit
 
 __device__ __forceinline__ u32 bswap32(u32 x) { return __builtin_bswap32(x); }
 __device__ __forceinline__ u32 rotl8(u32 x) { return __builtin_amdgcn_alignbit(x, x, 24); }
+__device__ __forceinline__ u32 rotr8(u32 x) { return __builtin_amdgcn_alignbit(x, x, 8); }
 __device__ __forceinline__ u32 xor3(u32 a, u32 b, u32 c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
 
 // Cross-lane steps on the VALU (DPP) instead of the LDS crossbar (__shfl lowers to ds_bpermute, which competes with the
@@ -256,7 +257,7 @@ __global__ void keyset_setup_kernel(const uint8_t *__restrict__ keys, const uint
             rk[r][c] = r <= nr ? w[4 * r + c] : 0;
     for (int r = 0; r < 15; ++r)
         for (int c = 0; c < 4; ++c)
-            e->rk[r][c] = rk[r][c];
+            e->rk[r][c] = r >= 1 && r < nr ? rotr8(rk[r][c]) : rk[r][c];
     const uint8_t *v = ivs + (size_t)i * 12;
     for (int c = 0; c < 3; ++c)
         e->iv[c] = (u32)v[4 * c] | (u32)v[4 * c + 1] << 8 | (u32)v[4 * c + 2] << 16 | (u32)v[4 * c + 3] << 24;
@@ -408,14 +409,16 @@ __device__ __forceinline__ void aes_rounds_n(const lds_u8 *lds, u32 laneoff, con
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
             const u32 s0 = s[i][0], s1 = s[i][1], s2 = s[i][2], s3 = s[i][3];
-            s[i][0] = xor3(te0(lds, s0, 0, laneoff), te2(lds, s2, 2, laneoff), rk[r][0]) ^
-                      rotl8(te0(lds, s1, 1, laneoff) ^ te2(lds, s3, 3, laneoff));
-            s[i][1] = xor3(te0(lds, s1, 0, laneoff), te2(lds, s3, 2, laneoff), rk[r][1]) ^
-                      rotl8(te0(lds, s2, 1, laneoff) ^ te2(lds, s0, 3, laneoff));
-            s[i][2] = xor3(te0(lds, s2, 0, laneoff), te2(lds, s0, 2, laneoff), rk[r][2]) ^
-                      rotl8(te0(lds, s3, 1, laneoff) ^ te2(lds, s1, 3, laneoff));
-            s[i][3] = xor3(te0(lds, s3, 0, laneoff), te2(lds, s1, 2, laneoff), rk[r][3]) ^
-                      rotl8(te0(lds, s0, 1, laneoff) ^ te2(lds, s2, 3, laneoff));
+            // the round key is stored rotated right by 8 (KeyEntry), so it joins the rotated half: three VALU ops a
+            // column (two 3-input XORs and a rotate) instead of four
+            s[i][0] = xor3(te0(lds, s0, 0, laneoff), te2(lds, s2, 2, laneoff),
+                           rotl8(xor3(te0(lds, s1, 1, laneoff), te2(lds, s3, 3, laneoff), rk[r][0])));
+            s[i][1] = xor3(te0(lds, s1, 0, laneoff), te2(lds, s3, 2, laneoff),
+                           rotl8(xor3(te0(lds, s2, 1, laneoff), te2(lds, s0, 3, laneoff), rk[r][1])));
+            s[i][2] = xor3(te0(lds, s2, 0, laneoff), te2(lds, s0, 2, laneoff),
+                           rotl8(xor3(te0(lds, s3, 1, laneoff), te2(lds, s1, 3, laneoff), rk[r][2])));
+            s[i][3] = xor3(te0(lds, s3, 0, laneoff), te2(lds, s1, 2, laneoff),
+                           rotl8(xor3(te0(lds, s0, 1, laneoff), te2(lds, s2, 3, laneoff), rk[r][3])));
         }
     }
     // last round: SubBytes + ShiftRows + AddRoundKey; S(x) is byte 1/2 of Te0[x] and byte 0/3 of Te2[x]
@@ -464,17 +467,18 @@ __device__ __forceinline__ CtrCache1 ctr_cache1_init(const lds_u8 *lds, u32 lane
                                                      u32 s3)
 {
     CtrCache1 c;
-    c.a0 = xor3(te0(lds, n0, 0, laneoff), te2(lds, n2, 2, laneoff), rk[1][0]) ^ rotl8(te0(lds, n1, 1, laneoff));
-    const u32 u1 = xor3(te0(lds, n1, 0, laneoff), te2(lds, s3, 2, laneoff), rk[1][1]) ^
-                   rotl8(te0(lds, n2, 1, laneoff) ^ te2(lds, n0, 3, laneoff));
-    const u32 t2 = xor3(te0(lds, n2, 0, laneoff), te2(lds, n0, 2, laneoff), rk[1][2]) ^
-                   rotl8(te0(lds, s3, 1, laneoff) ^ te2(lds, n1, 3, laneoff));
-    const u32 t3 = xor3(te0(lds, s3, 0, laneoff), te2(lds, n1, 2, laneoff), rk[1][3]) ^
-                   rotl8(te0(lds, n0, 1, laneoff) ^ te2(lds, n2, 3, laneoff));
-    c.b0 = xor3(te2(lds, t2, 2, laneoff), rotl8(te0(lds, u1, 1, laneoff) ^ te2(lds, t3, 3, laneoff)), rk[2][0]);
-    c.b1 = xor3(te0(lds, u1, 0, laneoff), te2(lds, t3, 2, laneoff), rk[2][1]) ^ rotl8(te0(lds, t2, 1, laneoff));
-    c.b2 = xor3(te0(lds, t2, 0, laneoff), rotl8(te0(lds, t3, 1, laneoff) ^ te2(lds, u1, 3, laneoff)), rk[2][2]);
-    c.b3 = xor3(te0(lds, t3, 0, laneoff), te2(lds, u1, 2, laneoff), rk[2][3]) ^ rotl8(te2(lds, t2, 3, laneoff));
+    // rk[1], rk[2] are stored rotated right by 8 (KeyEntry): they join the rotated half of each column
+    c.a0 = xor3(te0(lds, n0, 0, laneoff), te2(lds, n2, 2, laneoff), rotl8(te0(lds, n1, 1, laneoff) ^ rk[1][0]));
+    const u32 u1 = xor3(te0(lds, n1, 0, laneoff), te2(lds, s3, 2, laneoff),
+                        rotl8(xor3(te0(lds, n2, 1, laneoff), te2(lds, n0, 3, laneoff), rk[1][1])));
+    const u32 t2 = xor3(te0(lds, n2, 0, laneoff), te2(lds, n0, 2, laneoff),
+                        rotl8(xor3(te0(lds, s3, 1, laneoff), te2(lds, n1, 3, laneoff), rk[1][2])));
+    const u32 t3 = xor3(te0(lds, s3, 0, laneoff), te2(lds, n1, 2, laneoff),
+                        rotl8(xor3(te0(lds, n0, 1, laneoff), te2(lds, n2, 3, laneoff), rk[1][3])));
+    c.b0 = te2(lds, t2, 2, laneoff) ^ rotl8(xor3(te0(lds, u1, 1, laneoff), te2(lds, t3, 3, laneoff), rk[2][0]));
+    c.b1 = xor3(te0(lds, u1, 0, laneoff), te2(lds, t3, 2, laneoff), rotl8(te0(lds, t2, 1, laneoff) ^ rk[2][1]));
+    c.b2 = te0(lds, t2, 0, laneoff) ^ rotl8(xor3(te0(lds, t3, 1, laneoff), te2(lds, u1, 3, laneoff), rk[2][2]));
+    c.b3 = xor3(te0(lds, t3, 0, laneoff), te2(lds, u1, 2, laneoff), rotl8(te2(lds, t2, 3, laneoff) ^ rk[2][3]));
     return c;
 }
 
