@@ -171,6 +171,23 @@ __device__ __forceinline__ u32 wave_max_per8(u32 v)
         m = max(m, (u32)__builtin_amdgcn_readlane((int)v, 8 * g));
     return m;
 }
+// signed maximum / minimum over the wave of a value that is uniform within each 8-lane group
+__device__ __forceinline__ int wave_smax_per8(int v)
+{
+    int m = __builtin_amdgcn_readlane(v, 0);
+#pragma unroll
+    for (int g = 1; g < 8; ++g)
+        m = max(m, __builtin_amdgcn_readlane(v, 8 * g));
+    return m;
+}
+__device__ __forceinline__ int wave_smin_per8(int v)
+{
+    int m = __builtin_amdgcn_readlane(v, 0);
+#pragma unroll
+    for (int g = 1; g < 8; ++g)
+        m = min(m, __builtin_amdgcn_readlane(v, 8 * g));
+    return m;
+}
 
 // GF(2^128) * x on a GHASH element held as big-endian words (b0 most significant; bit 127 of the integer is x^0)
 __device__ __forceinline__ void gf_mulx_be(u32 &b0, u32 &b1, u32 &b2, u32 &b3)
@@ -792,7 +809,46 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         return X;
     };
 
+    // Steady state: the steps [sa, sb) (relative to m_lo, wave-uniform) in which every lane of every group of the wave
+    // holds a full text block, the next step's block is full too (the prefetch needs no check) and no group is at its
+    // segment's last step (Horner with H^G throughout). They run without the per-lane position logic: the counter,
+    // source and destination just advance by one step, about 30 VALU operations fewer per block.
+    const int D0 = P + (int)na;         // stream position of text block 0
+    const int nbf = (int)(Lsrc >> 4);   // full text blocks
+    const int ms = (D0 + G - 1) / G;    // first step whose 8 positions are all >= D0
+    const int me = nbf + D0 >= G ? (nbf + D0 - G) / G : -1;  // last step whose 8 positions are all full text
+    int sa = max(ms, (int)m_lo) - (int)m_lo;
+    int sb = min(me - 1, (int)m_hi - 2) + 1 - (int)m_lo;
+    if (!valid || m_hi <= m_lo)
+        sa = 1, sb = 0;
+    sa = wave_smax_per8(sa);
+    sb = wave_smin_per8(sb);
+
     for (u32 s0 = 0; s0 < Smax; ++s0) {
+        if ((int)s0 == sa && sb > sa) {
+            const int b0 = (int)(j + G * (m_lo + (u32)sa)) - D0;  // this lane's text block at step sa
+            u32 off = 16u * (u32)b0;                               // its byte offset in the text
+            u32 ctr = (u32)b0 + 2;
+            for (int s = sa; s < sb; ++s) {
+                cur = nxt[0];
+                nxt[0] = *(const u32x4_u *)(src + off + 16 * G);
+                u32 st[1][4] = {{n0, n1, n2, bswap32(ctr) ^ rk[0][3]}};
+                if ((ctr >> 8) != cc1_key) {
+                    cc1 = ctr_cache1_init<NR>(lds, laneoff, rk, n0, n1, n2, st[0][3]);
+                    cc1_key = ctr >> 8;
+                }
+                aes_ctr_cached1<NR>(lds, laneoff, rk, cc1, st);
+                __builtin_amdgcn_sched_barrier(0);
+                const u32x4 o = cur ^ u32x4{st[0][0], st[0][1], st[0][2], st[0][3]};
+                *(u32x4_u *)(dst + off) = o;
+                __builtin_amdgcn_sched_barrier(0);
+                acc = gmul_tab(lds, acc ^ (OPEN ? cur : o), tsel_horner);
+                __builtin_amdgcn_sched_barrier(0);
+                ctr += G;
+                off += 16 * G;
+            }
+            s0 = (u32)sb;
+        }
         const u32 m0 = m_lo + s0;
         u32 st[1][4];
         setup_step(m0, st);
