@@ -116,6 +116,9 @@ int ptls_mi355x_keyset_set_schedule(ptls_mi355x_keyset_t *ks, int schedule);
 
 /**
  * Seals nrecs records in one launch. recs, in, aad, out are DEVICE pointers. Asynchronous on `stream`.
+ * Records may come in any order: with a many-key keyset (up to 2^20 keys) a batch whose key runs would average under
+ * 8 records is grouped by key_idx on the device first (scratch kept in the keyset; batches on different streams that
+ * share the keyset are ordered through it).
  * Returns 0 on success, a negative value on invalid arguments or launch failure.
  */
 int ptls_mi355x_seal_batch(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,

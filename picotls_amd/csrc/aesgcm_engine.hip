@@ -610,6 +610,11 @@ struct BatchArgs {
     u32 multi_key;  // 0: every record uses key 0 (no key-run scan)
     u32 nkeys;      // records whose key_idx >= nkeys are skipped (open: ok = 0)
     u32 unit_log2;  // chunked kernel: units of 2^unit_log2 steps (<= CHUNK_STEPS; smaller for a launch of one record)
+    // chunked kernel, ungrouped many-key batches (key_*_kernel): when *perm_on != 0 the kernel walks `grouped` (the
+    // descriptors in key order) and perm[i] is the batch index of grouped[i] (for the ok bytes)
+    const ptls_mi355x_record_t *grouped;
+    const u32 *perm;
+    const u32 *perm_on;
 };
 
 #define RUN_SCAN_CAP 256  // records examined per key-run scan (multi-key batches)
@@ -1065,6 +1070,13 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     const u64 n = args.nrecs;
     const u64 beg = n * blockIdx.x / gridDim.x, end = n * (blockIdx.x + 1) / gridDim.x;
     u32 loaded_key = 0xffffffffu;
+    // the descriptors in batch order, or (an ungrouped many-key batch) the key-grouped copy built on the device; ok
+    // bytes go to the record's batch index either way
+    const ptls_mi355x_record_t *recs = args.recs;
+    const u32 *perm = nullptr;
+    if (args.perm_on != nullptr && *args.perm_on)
+        recs = args.grouped, perm = args.perm;
+    auto ok_at = [&](u64 i) -> u64 { return perm != nullptr ? (u64)perm[i] : i; };
 
     build_aes_tables(lds);
 
@@ -1072,7 +1084,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         PROF_STAMP(t0);
         // ---- the run: records [pos, pos + run_n) with one key, at most CRUN_RECS records and CRUN_UNITS units.
         // Threads 0..CRUN_RECS-1 read one descriptor each: the key boundary and the unit counts come from one pass.
-        const u32 key_idx = args.multi_key ? args.recs[pos].key_idx : 0u;
+        const u32 key_idx = args.multi_key ? recs[pos].key_idx : 0u;
         const u32 lim = (u32)min(end - pos, (u64)CRUN_RECS);
         u32 nc = 0, incl = 0, bkt = 0;
         if (wave < SCAN_WAVES) {
@@ -1080,7 +1092,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             bool other_key = false;
             u32 smin = 0xffffffffu, smax = 0;
             if (t < lim) {
-                ptls_mi355x_record_t r = args.recs[pos + t];
+                ptls_mi355x_record_t r = recs[pos + t];
                 if (!record_ok(args, r))  // rejected: one empty unit (see the unit loop)
                     r.len = 0, r.aad_len = 0;
                 const u32 steps = gcm_steps<OPEN, FRAME>(r);
@@ -1201,7 +1213,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         if (key_idx >= args.nkeys) {  // invalid key: nothing is written except a failed ok byte
             if (OPEN)
                 for (u64 t = pos + threadIdx.x; t < run_end; t += blockDim.x)
-                    args.ok[t] = 0;
+                    args.ok[ok_at(t)] = 0;
             __syncthreads();
             pos = run_end;
             continue;
@@ -1260,12 +1272,13 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             const u32 ri = lo;
             ptls_mi355x_record_t r = {};
             if (valid)
-                r = args.recs[pos + ri];
+                r = recs[pos + ri];
+            const u64 rid = OPEN && valid ? ok_at(pos + ri) : pos + ri;  // the record's batch index (ok byte)
             const bool live = valid && record_ok(args, r);
             if (valid && !live) {  // rejected descriptor: the scan gave it one unit; nothing is written
                 r.len = 0, r.aad_len = 0;
                 if (OPEN && j == 0)
-                    args.ok[pos + ri] = 0;
+                    args.ok[rid] = 0;
             }
             const u32 steps = gcm_steps<OPEN, FRAME>(r);
             // unit [m_lo, m_hi) of the record's steps (whole mode: the record); huge records take longer units
@@ -1280,7 +1293,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 m_lo = m_hi = 0;
             u32x4 acc, ek0;
             gcm_segment<NR, OPEN, 1, FRAME>(args, lds, rk, iv0, iv1, iv2, r, live, m_lo, m_hi, j, laneoff, tsel_horner,
-                                     tsel_last, acc, ek0, unc == 1, pos + ri);
+                                     tsel_last, acc, ek0, unc == 1, rid);
             if (live && unc > 1) {  // uniform over the group
                 u32 last = 0;
                 if (j == G - 1) {
@@ -1307,7 +1320,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                         const u32x4 rt = *(const u32x4_u *)(args.in + r.in_off + frame_in_skip<OPEN, FRAME>() +
                                                             gcm_text_len<OPEN, FRAME>(r));
                         const u32x4 d = rt ^ tag;
-                        args.ok[pos + ri] = (d[0] | d[1] | d[2] | d[3]) == 0;
+                        args.ok[rid] = (d[0] | d[1] | d[2] | d[3]) == 0;
                     } else {
                         *(u32x4_u *)(args.out + r.out_off + frame_out_skip<OPEN, FRAME>() + gcm_text_len<OPEN, FRAME>(r)) = tag;
                     }
@@ -1331,6 +1344,101 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         }
 #endif
         pos = run_end;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------ key grouping
+// A many-key batch whose records are not grouped by connection would give the chunked kernel one-record key runs, each
+// with its own table build and barrier (15 GiB/s on 4M records over 64K keys in random order against 724 grouped).
+// Small kernels group it on the device first: the number of key changes between neighbours (regroup when runs would
+// average under 8 records; a grouped batch stops here), key counts, their exclusive scan, and a scatter of record
+// indices into key order. The chunked kernel then walks the permutation; descriptors, outputs and ok bytes stay
+// at each record's own index, so the results are those of the batch order. ctl[0] = key changes, ctl[1] = regroup.
+#define KEY_GROUP_MAX_KEYS (1u << 20)
+
+// ctl[0]: key changes between neighbouring records (a wave sum per atomic)
+__global__ __launch_bounds__(256) void key_changes_kernel(const ptls_mi355x_record_t *recs, u64 n, u32 *ctl)
+{
+    u32 changes = 0;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x + 1; i < n; i += (u64)gridDim.x * blockDim.x)
+        changes += recs[i - 1].key_idx != recs[i].key_idx;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+        changes += (u32)__shfl_xor((int)changes, off, 64);
+    if ((threadIdx.x & 63) == 0 && changes != 0)
+        atomicAdd(&ctl[0], changes);
+}
+
+__device__ __forceinline__ bool key_regroup(const u32 *ctl, u64 n) { return (u64)ctl[0] * 8 > n; }
+
+// key counts (only when regrouping): each thread counts a contiguous stretch of records and adds one count per key run
+__global__ __launch_bounds__(256) void key_hist_kernel(const ptls_mi355x_record_t *recs, u64 n, u32 nkeys, u32 *cnt, const u32 *ctl)
+{
+    if (!key_regroup(ctl, n))
+        return;
+    const u64 nthr = (u64)gridDim.x * blockDim.x, t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+    const u64 per = (n + nthr - 1) / nthr, i0 = min(n, t * per), i1 = min(n, i0 + per);
+    u32 run_key = 0xffffffffu, run_len = 0;
+    for (u64 i = i0; i < i1; ++i) {
+        u32 k = recs[i].key_idx;
+        k = k < nkeys ? k : nkeys;  // out-of-range keys share the last bucket
+        if (k != run_key) {
+            if (run_len != 0)
+                atomicAdd(&cnt[run_key], run_len);
+            run_key = k, run_len = 0;
+        }
+        ++run_len;
+    }
+    if (run_len != 0)
+        atomicAdd(&cnt[run_key], run_len);
+}
+
+// exclusive scan of the counts in place (one workgroup), then ctl[1] = regroup
+__global__ __launch_bounds__(1024) void key_scan_kernel(u32 *cnt, u32 nb, u64 n, u32 *ctl)
+{
+    __shared__ u32 wsum[16];
+    const bool regroup = key_regroup(ctl, n);
+    if (threadIdx.x == 0)
+        ctl[1] = regroup;
+    if (!regroup)
+        return;
+    const u32 t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const u32 per = (nb + blockDim.x - 1) / blockDim.x, b0 = min(nb, t * per), b1 = min(nb, b0 + per);
+    u32 sum = 0;
+#pragma unroll 8
+    for (u32 i = b0; i < b1; ++i)
+        sum += cnt[i];
+    u32 incl = sum;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const u32 y = (u32)__shfl_up((int)incl, off, 64);
+        if (lane >= (u32)off)
+            incl += y;
+    }
+    if (lane == 63)
+        wsum[wave] = incl;
+    __syncthreads();
+    u32 run = incl - sum;
+    for (u32 w = 0; w < wave; ++w)
+        run += wsum[w];
+#pragma unroll 8
+    for (u32 i = b0; i < b1; ++i) {
+        const u32 c = cnt[i];
+        cnt[i] = run;
+        run += c;
+    }
+}
+
+__global__ __launch_bounds__(256) void key_scatter_kernel(const ptls_mi355x_record_t *recs, u64 n, u32 nkeys, u32 *cur, u32 *perm,
+                                                          ptls_mi355x_record_t *grouped, const u32 *ctl)
+{
+    if (ctl[1] == 0)
+        return;
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (u64)gridDim.x * blockDim.x) {
+        const ptls_mi355x_record_t r = recs[i];
+        const u32 slot = atomicAdd(&cur[r.key_idx < nkeys ? r.key_idx : nkeys], 1u);
+        perm[slot] = (u32)i;
+        grouped[slot] = r;
     }
 }
 
@@ -1551,6 +1659,11 @@ struct st_ptls_mi355x_keyset_t {
     uint8_t *d_stage, *h_stage;
     size_t stage_cap;
     hipStream_t stream;
+    // key grouping of ungrouped many-key batches (key_group_*): scratch for key counts and the record permutation,
+    // grown on demand; group_ev orders its users when batches on several streams share the keyset
+    u32 *d_group;
+    size_t group_cap;
+    hipEvent_t group_ev;
 };
 
 static int stage_reserve(ptls_mi355x_keyset_t *ks, size_t bytes)
@@ -1729,6 +1842,11 @@ void ptls_mi355x_keyset_free(ptls_mi355x_keyset_t *ks)
     }
     if (ks->stream != NULL)
         hipStreamDestroy(ks->stream);
+    if (ks->group_ev != NULL) {
+        hipEventSynchronize(ks->group_ev);
+        hipEventDestroy(ks->group_ev);
+    }
+    hipFree(ks->d_group);
     free(ks);
 }
 
@@ -1789,7 +1907,7 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
     if (nrecs == 0)
         return 0;
     BatchArgs a = {ks->d_keys, recs, (u64)nrecs, (const uint8_t *)in, (const uint8_t *)aad, (uint8_t *)out, ok,
-                   ks->nkeys > 1 ? 1u : 0u, (u32)ks->nkeys, unit_log2};
+                   ks->nkeys > 1 ? 1u : 0u, (u32)ks->nkeys, unit_log2, nullptr, nullptr, nullptr};
     if (a.aad == NULL)
         a.aad = a.in;
     const u64 groups = (nrecs + (64 / ENGINE_G) - 1) / (64 / ENGINE_G);
@@ -1800,6 +1918,39 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
     if (grid < 1)
         grid = 1;
     hipStream_t s = (hipStream_t)stream;
+    // ungrouped many-key batches: group the records by key on the device first (see key_hist_kernel)
+#ifndef KEY_GROUP_DISABLE
+    const bool group = use_chunked(ks) && ks->nkeys > 1 && ks->nkeys <= KEY_GROUP_MAX_KEYS && nrecs > 1 &&
+                       nrecs <= 0xffffffffu;
+#else
+    const bool group = false;
+#endif
+    if (group) {
+        // scratch: ctl[2] | counts[nkeys + 1] | perm[n] | (8-byte aligned) grouped descriptors[n]
+        const size_t nb = ks->nkeys + 1, words = ((2 + nb + nrecs + 1) & ~(size_t)1) + nrecs * (sizeof(ptls_mi355x_record_t) / 4);
+        if (ks->group_ev == NULL)
+            HIP_TRY(hipEventCreateWithFlags(&ks->group_ev, hipEventDisableTiming));
+        if (words > ks->group_cap) {
+            HIP_TRY(hipEventSynchronize(ks->group_ev));
+            hipFree(ks->d_group);
+            ks->d_group = NULL;
+            ks->group_cap = 0;
+            HIP_TRY(hipMalloc((void **)&ks->d_group, words * 4));
+            ks->group_cap = words;
+        }
+        HIP_TRY(hipStreamWaitEvent(s, ks->group_ev, 0));  // a batch on another stream may still use the scratch
+        u32 *ctl = ks->d_group, *cnt = ctl + 2, *perm = cnt + nb;
+        HIP_TRY(hipMemsetAsync(ctl, 0, (2 + nb) * 4, s));
+        const unsigned gh = (unsigned)min((nrecs + 255) / 256, (size_t)ks->ncu * 8);
+        key_changes_kernel<<<gh, 256, 0, s>>>(recs, nrecs, ctl);
+        key_hist_kernel<<<gh, 256, 0, s>>>(recs, nrecs, (u32)ks->nkeys, cnt, ctl);
+        key_scan_kernel<<<1, 1024, 0, s>>>(cnt, (u32)nb, nrecs, ctl);
+        ptls_mi355x_record_t *grouped = (ptls_mi355x_record_t *)(ctl + ((2 + nb + nrecs + 1) & ~(size_t)1));
+        key_scatter_kernel<<<gh, 256, 0, s>>>(recs, nrecs, (u32)ks->nkeys, cnt, perm, grouped, ctl);
+        a.grouped = grouped;
+        a.perm = perm;
+        a.perm_on = ctl + 1;
+    }
 #define CHUNKED_LAUNCH(nr, op, frame) gcm_chunked_kernel<nr, op, frame><<<(unsigned)grid, ENGINE_WG, CLDS_ALLOC, s>>>(a)
     if (frame == 1) {
         if (ks->nr == 10) {
@@ -1849,6 +2000,8 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
             gcm_batch_kernel<14, false><<<(unsigned)grid, ENGINE_WG, LDS_ALLOC, s>>>(a);
     }
     HIP_TRY(hipGetLastError());
+    if (group)
+        HIP_TRY(hipEventRecord(ks->group_ev, s));
     return 0;
 }
 

@@ -88,6 +88,7 @@ class Workload:
     tls_header_aad: bool = False
     seed: int = 0x5EED
     desc: str = ""
+    key_order: str = "grouped"  # many keys: "grouped" by connection, or "random" (key_idx = splitmix(i) mod nkeys)
 
     def scaled(self, nrecs: int) -> "Workload":
         return replace(self, nrecs=nrecs)
@@ -105,6 +106,16 @@ class Workload:
         i = np.arange(begin, end, dtype=np.uint64)
         if self.nkeys == 1:
             return np.zeros(end - begin, np.uint32), i
+        if self.key_order == "random":
+            # SURVEY §8(d) config 4 as written: key_idx = splitmix(i) mod nkeys over the whole batch, seq counting each
+            # connection's records in batch order
+            allk = (splitmix_words_np(self.seed ^ 0x4B4958, 0, self.nrecs) % np.uint64(self.nkeys)).astype(np.uint32)
+            order = np.argsort(allk, kind="stable")
+            ks = allk[order]
+            starts = np.searchsorted(ks, ks, side="left")
+            seq = np.empty(self.nrecs, np.uint64)
+            seq[order] = (np.arange(self.nrecs) - starts).astype(np.uint64)
+            return allk[begin:end], seq[begin:end]
         key = (i * np.uint64(self.nkeys) // np.uint64(self.nrecs)).astype(np.uint32)
         first = (key.astype(np.uint64) * np.uint64(self.nrecs) + np.uint64(self.nkeys) - np.uint64(1)) // np.uint64(self.nkeys)
         return key, i - first
@@ -141,6 +152,8 @@ WORKLOADS = {
     "quic1200": Workload("quic1200", 4 << 20, 1200, 13, 16, desc="4M x 1200 B QUIC-sized records, AES-128-GCM, single key"),
     "mixed": Workload("mixed", 4 << 20, None, 13, 32, nkeys=65536,
                       desc="4M mixed-length records 64 B-16 KiB, AES-256-GCM, 64K traffic keys"),
+    "mixedrand": Workload("mixedrand", 4 << 20, None, 13, 32, nkeys=65536, key_order="random",
+                          desc="4M mixed-length records 64 B-16 KiB, AES-256-GCM, 64K traffic keys in random order"),
     "shard1200": Workload("shard1200", 32 << 20, 1200, 13, 16,
                           desc="32M x 1200 B records sharded evenly across GPUs, AES-128-GCM"),
     # analysis variants (not BASELINE configs): isolate key switching and length mix from the AES-256 cost

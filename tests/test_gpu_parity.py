@@ -672,3 +672,41 @@ def test_records_beyond_1024_units_chunked(ref):
     for r in b.open:
         o, ln = int(r["out_off"]), int(r["len"])
         assert np.array_equal(plain[o:o + ln], want[o:o + ln]), ln
+
+
+@pytest.mark.parametrize("nkeys,frac_bad", [(300, 0.0), (4096, 0.02)])
+def test_ungrouped_many_key_batch_regrouped_on_device(ref, nkeys, frac_bad):
+    # records of many connections in random order (SURVEY 8(d) config 4 as written) are grouped by key on the device
+    # before the chunked kernel (key_hist / key_scan / key_scatter); results and ok bytes stay at each record's own
+    # index, out-of-range keys are rejected wherever they sit, and a second batch on the same keyset reuses the scratch
+    rng = np.random.default_rng(630 + nkeys)
+    n = 6000
+    lens = rng.integers(0, 5000, n)
+    key_idx = rng.integers(0, nkeys, n)
+    bad = rng.random(n) < frac_bad
+    key_idx[bad] = nkeys + rng.integers(0, 5, int(bad.sum()))
+    b = RecordBatch.build(lens, rng.integers(0, 40, n), seqs=rng.integers(0, 2**48, n, dtype=np.uint64), key_idx=key_idx)
+    keys = np.frombuffer(rng.bytes(nkeys * 32), np.uint8)
+    ivs = np.frombuffer(rng.bytes(nkeys * 12), np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(max(b.aad_bytes, 1)), np.uint8)
+    ks = pa.Keyset(keys, ivs, 32)
+    sealed = gpu_seal(ks, b.seal, pt, aad, b.sealed_bytes)
+    good = np.flatnonzero(~bad)
+    expect = np.zeros(b.sealed_bytes, np.uint8)
+    ref.run_batch(True, keys, ivs, 32, b.seal[good], pt, aad, expect, nthreads=8)
+    for i in range(n):
+        o, ln = int(b.seal[i]["out_off"]), int(b.seal[i]["len"]) + 16
+        if bad[i]:
+            assert not sealed[o:o + ln].any(), i  # nothing written (the arena starts zeroed)
+        else:
+            assert np.array_equal(sealed[o:o + ln], expect[o:o + ln]), i
+    back, ok = gpu_open(ks, b.open, expect, aad, b.pt_bytes)
+    assert np.array_equal(ok.astype(bool), ~bad)
+    for i in good:
+        o, ln = int(b.open[i]["out_off"]), int(b.open[i]["len"])
+        assert np.array_equal(back[o:o + ln], pt[o:o + ln]), i
+    # the same keyset again, grouped order this time (no regrouping needed)
+    order = np.argsort(key_idx, kind="stable")
+    sealed2 = gpu_seal(ks, b.seal[order], pt, aad, b.sealed_bytes)
+    assert np.array_equal(sealed2, sealed)
