@@ -24,6 +24,8 @@ ENGINE_FLAGS = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
 ENGINE_SRCS = [os.path.join(PKG, "csrc", "aesgcm_engine.hip")]
 PICOTLS_SRCS = [os.path.join(PKG, "csrc", "ptls_mi355x.c")]
 HEADERS = [os.path.join(ROOT, "include", "picotls", "mi355x.h"), os.path.join(ROOT, "include", "picotls", "mi355x_picotls.h")]
+ENGINE_PARTS = sorted(os.path.join(PKG, "csrc", "engine", f) for f in os.listdir(os.path.join(PKG, "csrc", "engine"))
+                      if f.endswith(".h"))  # included by aesgcm_engine.hip (one translation unit)
 
 
 def _stale(target: str, deps: list[str]) -> bool:
@@ -35,7 +37,7 @@ def _stale(target: str, deps: list[str]) -> bool:
 
 def build_engine(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(LIB_DIR, exist_ok=True)
-    if force or _stale(ENGINE_SO, ENGINE_SRCS + HEADERS):
+    if force or _stale(ENGINE_SO, ENGINE_SRCS + ENGINE_PARTS + HEADERS):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
                "-Wno-unused-value", *ENGINE_FLAGS, "-I", os.path.join(ROOT, "include"), *ENGINE_SRCS,
                "-o", ENGINE_SO + ".tmp"]

@@ -1,0 +1,169 @@
+// picotls_amd/csrc/engine/common.h -- Types, constants, the S-box, the keyset entry layout and small lane/GF helpers.
+// Part of the single translation unit picotls_amd/csrc/aesgcm_engine.hip (included in order; not standalone).
+#ifndef PTLS_MI355X_ENGINE_COMMON_H
+#define PTLS_MI355X_ENGINE_COMMON_H
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef u32x4 __attribute__((aligned(1))) u32x4_u;
+typedef u32 __attribute__((aligned(1))) u32_u;
+
+static_assert(sizeof(ptls_mi355x_record_t) == PTLS_MI355X_RECORD_SIZE, "record descriptor must be 40 bytes");
+static_assert(sizeof(ptls_mi355x_cid_t) == 24, "CID descriptor must be 24 bytes");
+
+// ------------------------------------------------------------------------------------------------ constants
+
+namespace {
+
+struct SboxTable {
+    uint8_t v[256];
+};
+
+constexpr uint8_t xtime_c(uint8_t a) { return (uint8_t)((a << 1) ^ ((a & 0x80) ? 0x1b : 0)); }
+
+// FIPS-197 S-box derived at compile time: multiplicative inverse via exp/log tables of generator 3, then the
+// affine transform.
+constexpr SboxTable make_sbox()
+{
+    uint8_t exp_t[256] = {}, log_t[256] = {};
+    uint8_t x = 1;
+    for (int i = 0; i < 255; ++i) {
+        exp_t[i] = x;
+        log_t[x] = (uint8_t)i;
+        x = (uint8_t)(x ^ xtime_c(x));  // x * 3
+    }
+    SboxTable t = {};
+    for (int v = 0; v < 256; ++v) {
+        uint8_t inv = v == 0 ? 0 : exp_t[(255 - log_t[v]) % 255];
+        uint8_t s = inv;
+        for (int k = 1; k <= 4; ++k)
+            s ^= (uint8_t)((inv << k) | (inv >> (8 - k)));
+        t.v[v] = (uint8_t)(s ^ 0x63);
+    }
+    return t;
+}
+
+}  // namespace
+
+__constant__ SboxTable c_sbox = make_sbox();
+
+// one keyset entry in HBM (512 bytes, 16-byte aligned)
+struct KeyEntry {
+    u32 rk[15][4];  // round keys, LE column words; rounds 1..NR-1 stored rotated right by 8 bits (see aes_rounds_n)
+    u32 iv[4];      // static IV as LE words (word 3 = 0)
+    u32 h[16][4];   // GHASH elements (LE words): [0..7] = H^1..H^8, [8] = H^CHUNK_BLOCKS, [9..11] = H^16, H^32, H^64
+                    // (the combine powers of smaller units), [12..15] = 0
+};
+static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
+
+#ifndef ENGINE_FAST_STEP
+#define ENGINE_FAST_STEP 1         // wave-uniform fast path for steps where every lane holds a full text block
+#endif
+
+#define ENGINE_G 8                 // lanes per record
+#ifndef ENGINE_NB
+#define ENGINE_NB 1                // AES-CTR blocks per lane per step (independent chains in flight)
+#endif
+#ifndef ENGINE_WG
+#define ENGINE_WG 1024             // threads per workgroup (one workgroup per CU)
+#endif
+#define ENGINE_WAVES_PER_SIMD (ENGINE_WG / 256)
+#define LDS_AES_BYTES 65536        // Te0/Te2, 32-bank replicated
+#define GHASH_TABLE_BYTES 8192     // 32 windows x 16 entries x 16 B
+#define LDS_BYTES (LDS_AES_BYTES + ENGINE_G * GHASH_TABLE_BYTES)
+#define LDS_ALLOC (LDS_BYTES + 16)  // + scratch word for the key-run scan
+
+// Chunked schedule (many-key batches): records are cut into units of at most CHUNK_BLOCKS GHASH-stream blocks, and
+// the per-unit GHASH partials are recombined with H^CHUNK_BLOCKS (one more 8 KiB table, LDS table slot 8).
+#ifndef CHUNK_BLOCKS
+#define CHUNK_BLOCKS 128  // 2 KiB units: 64K-key mixed +3 %, one-key mixed +7 % over 1 KiB units (interleaved A/B); 256: +1 % / +10 %
+#endif
+#define CHUNK_STEPS (CHUNK_BLOCKS / ENGINE_G)
+#define CHUNK_LOG2 (__builtin_ctz(CHUNK_STEPS))
+#ifndef CHUNK_MAX_UNITS
+#define CHUNK_MAX_UNITS CRUN_UNITS  // records longer than this many units (> ~2 MiB) use units of a multiple length
+#endif
+#define BKT_STRIDE (CHUNK_STEPS + 1)             // per-wave front-unit bucket counters in s_ctl (<= 32)
+#define CRUN_RECS 256        // records per run (one key)
+#ifndef CRUN_UNITS
+#define CRUN_UNITS 1024      // units per run
+#endif
+#define WHOLE_RUN_RECS 4096  // records per run when a one-key run is uniform (every record one unit)
+#define UNIFORM_SLACK 2      // a run is uniform when its records' step counts differ by at most this
+#define WHOLE_MIN_RECS (ENGINE_WG / ENGINE_G)  // whole-record mode needs at least one record per 8-lane group
+#define CLDS_CTL_WORDS ((32 + (CRUN_RECS / 64) * BKT_STRIDE + 127) / 128 * 128)
+#define CLDS_CTL (LDS_BYTES + GHASH_TABLE_BYTES)                // CLDS_CTL_WORDS control words
+#define CLDS_UBASE (CLDS_CTL + 4 * CLDS_CTL_WORDS)              // u32[CRUN_RECS + 1]: first unit of each record
+#define CLDS_DONE (CLDS_UBASE + 4 * (CRUN_RECS + 16))           // u32[CRUN_RECS]: finished units per record
+#define CLDS_EK0 (CLDS_DONE + 4 * CRUN_RECS)                    // 16 B per record: E(K, J0)
+#define CLDS_PART (CLDS_EK0 + 16 * CRUN_RECS)                   // 16 B per unit: GHASH partial
+#define CLDS_FRONT (CLDS_PART + 16 * CRUN_UNITS)                // u32[CRUN_RECS]: records by front-unit size
+#define CLDS_ALLOC (CLDS_FRONT + 4 * CRUN_RECS)
+static_assert(CLDS_ALLOC <= 160 * 1024, "chunked schedule LDS budget");
+static_assert(CHUNK_BLOCKS % ENGINE_G == 0, "units are whole steps");
+static_assert((CHUNK_STEPS & (CHUNK_STEPS - 1)) == 0 && CHUNK_STEPS <= 16, "unit lengths are powers of two up to 16 steps");
+
+
+// ------------------------------------------------------------------------------------------------ small helpers
+
+__device__ __forceinline__ u32 bswap32(u32 x) { return __builtin_bswap32(x); }
+__device__ __forceinline__ u32 rotl8(u32 x) { return __builtin_amdgcn_alignbit(x, x, 24); }
+__device__ __forceinline__ u32 rotr8(u32 x) { return __builtin_amdgcn_alignbit(x, x, 8); }
+__device__ __forceinline__ u32 xor3(u32 a, u32 b, u32 c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
+
+// Cross-lane steps on the VALU (DPP) instead of the LDS crossbar (__shfl lowers to ds_bpermute, which competes with the
+// table lookups for the LDS): XOR over each aligned group of 8 lanes (quad_perm [1,0,3,2], [2,3,0,1], then
+// row_half_mirror pairs the two quads), result in all 8 lanes.
+__device__ __forceinline__ u32 dpp_xor8(u32 v)
+{
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+    return v;
+}
+// lane 7 of each aligned 8-lane group, to all 8 lanes (quad_perm [3,3,3,3], then row_half_mirror for lanes 0-3)
+__device__ __forceinline__ u32 dpp_bcast7(u32 v, u32 lane)
+{
+    const u32 t = (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0xFF, 0xF, 0xF, false);
+    const u32 u = (u32)__builtin_amdgcn_update_dpp(0, (int)t, 0x141, 0xF, 0xF, false);
+    return (lane & 4) ? t : u;
+}
+// maximum over the wave of a value that is uniform within each 8-lane group
+__device__ __forceinline__ u32 wave_max_per8(u32 v)
+{
+    u32 m = (u32)__builtin_amdgcn_readlane((int)v, 0);
+#pragma unroll
+    for (int g = 1; g < 8; ++g)
+        m = max(m, (u32)__builtin_amdgcn_readlane((int)v, 8 * g));
+    return m;
+}
+// signed maximum / minimum over the wave of a value that is uniform within each 8-lane group
+__device__ __forceinline__ int wave_smax_per8(int v)
+{
+    int m = __builtin_amdgcn_readlane(v, 0);
+#pragma unroll
+    for (int g = 1; g < 8; ++g)
+        m = max(m, __builtin_amdgcn_readlane(v, 8 * g));
+    return m;
+}
+__device__ __forceinline__ int wave_smin_per8(int v)
+{
+    int m = __builtin_amdgcn_readlane(v, 0);
+#pragma unroll
+    for (int g = 1; g < 8; ++g)
+        m = min(m, __builtin_amdgcn_readlane(v, 8 * g));
+    return m;
+}
+
+// GF(2^128) * x on a GHASH element held as big-endian words (b0 most significant; bit 127 of the integer is x^0)
+__device__ __forceinline__ void gf_mulx_be(u32 &b0, u32 &b1, u32 &b2, u32 &b3)
+{
+    u32 lsb = b3 & 1;
+    b3 = (b3 >> 1) | (b2 << 31);
+    b2 = (b2 >> 1) | (b1 << 31);
+    b1 = (b1 >> 1) | (b0 << 31);
+    b0 = (b0 >> 1) ^ (lsb ? 0xe1000000u : 0u);
+}
+
+#endif  // PTLS_MI355X_ENGINE_COMMON_H

@@ -1,0 +1,97 @@
+// picotls_amd/csrc/engine/lds_tables.h -- LDS table builders: the replicated AES T-tables and the GHASH 4-bit-window tables.
+// Part of the single translation unit picotls_amd/csrc/aesgcm_engine.hip (included in order; not standalone).
+#ifndef PTLS_MI355X_ENGINE_LDS_TABLES_H
+#define PTLS_MI355X_ENGINE_LDS_TABLES_H
+
+// ------------------------------------------------------------------------------------------------ LDS tables
+
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) u32 lds_u32;
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+
+// AES T-table: Te0 replicated into banks 0..31 (bytes 0..127 of row n), Te2 = rotl16(Te0) into bytes 128..255
+__device__ void build_aes_tables(lds_u8 *lds)
+{
+    lds_u32 *t = (lds_u32 *)lds;
+    // entry n = idx >> 6 is wave-uniform (blockDim.x is a multiple of 64): scalar S-box loads, 16 in flight per batch,
+    // so a launch pays one memory latency here instead of one per loop trip (the per-record path is a launch of one)
+    for (u32 base = 0; base < 256 * 64; base += 16 * blockDim.x) {
+        u32 sv[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            sv[k] = c_sbox.v[__builtin_amdgcn_readfirstlane((base + threadIdx.x + k * blockDim.x) >> 6) & 255u];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const u32 idx = base + threadIdx.x + k * blockDim.x, slot = idx & 63;
+            const u32 s = sv[k];
+            const u32 s2 = ((s << 1) ^ ((s & 0x80) ? 0x1b : 0)) & 0xff;
+            const u32 te0 = s2 | s << 8 | s << 16 | (s2 ^ s) << 24;
+            if (idx < 256 * 64)
+                t[idx] = slot < 32 ? te0 : ((te0 << 16) | (te0 >> 16));
+        }
+    }
+}
+
+// (b0..b3) *= x^s in GF(2^128), big-endian words (GCM bit order: the MSB of b0 is x^0), 1 <= s <= 32, in closed form:
+// bit i of the s bits shifted out of b3 is x^(127 - i) and comes back as x^(s - 1 - i) * (1 + x + x^2 + x^7), i.e. the
+// shifted-out bits land at the top of b0 ("1") and again 1, 2 and 7 bits further down, the last spilling into b1
+__device__ __forceinline__ void gf_mulxs_be(u32 &b0, u32 &b1, u32 &b2, u32 &b3, u32 s)
+{
+    const u32 top = s == 32 ? b3 : b3 << (32 - s);
+    if (s == 32) {
+        b3 = b2, b2 = b1, b1 = b0, b0 = 0;
+    } else {
+        b3 = __builtin_amdgcn_alignbit(b2, b3, s);
+        b2 = __builtin_amdgcn_alignbit(b1, b2, s);
+        b1 = __builtin_amdgcn_alignbit(b0, b1, s);
+        b0 >>= s;
+    }
+    const u64 v = (u64)top << 32;
+    const u64 r = v ^ (v >> 1) ^ (v >> 2) ^ (v >> 7);
+    b0 ^= (u32)(r >> 32);
+    b1 ^= (u32)r;
+}
+
+// GHASH window tables of one key: table t (element key->h[t]), window p (x^(4p)..x^(4p+3)), entry n (4-bit value,
+// MSB = coefficient of x^(4p)) = sum over set bits of n of x^(4p+q) * h[t]. Thread (t, p) derives V_0 = x^(4p) h[t]
+// with at most three 32-bit steps and one step of 4 (p mod 8) bits, V_1..V_3 by single steps, and writes the window's
+// 16 entries. Entries are GF(2)-linear in n, so the XOR combinations are formed after the byte swap back to memory
+// order, and entry n ^ c = e(n) ^ e(c): at store n a lane writes slot n ^ (p mod 16), spreading a wave's 16-byte stores
+// over the bank groups. A few hundred VALU operations per thread: the build is a small part of a launch of one record.
+__device__ void build_ghash_tables(lds_u8 *lds, const KeyEntry *__restrict__ key, u32 ntables = ENGINE_G, u32 src8 = 8)
+{
+    for (u32 idx = threadIdx.x; idx < ntables * 32; idx += blockDim.x) {
+        const u32 t = idx >> 5, p = idx & 31;
+        const u32 *h = key->h[t == 8 ? src8 : t];  // table 8: the unit combine power (chunked kernel)
+        u32 b0 = bswap32(h[0]), b1 = bswap32(h[1]), b2 = bswap32(h[2]), b3 = bswap32(h[3]);
+        for (u32 k = 0; k < (p >> 3); ++k)
+            gf_mulxs_be(b0, b1, b2, b3, 32);
+        if (p & 7)
+            gf_mulxs_be(b0, b1, b2, b3, 4 * (p & 7));
+        u32x4 v[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            v[m] = u32x4{bswap32(b0), bswap32(b1), bswap32(b2), bswap32(b3)};
+            if (m < 3)
+                gf_mulxs_be(b0, b1, b2, b3, 1);
+        }
+        const u32 c = p & 15;
+        u32x4 ec = {0, 0, 0, 0};
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            if ((c >> (3 - m)) & 1u)
+                ec ^= v[m];
+        lds_u32x4 *row = (lds_u32x4 *)(lds + LDS_AES_BYTES + t * GHASH_TABLE_BYTES + p * 256);
+#pragma unroll
+        for (u32 n = 0; n < 16; ++n) {
+            u32x4 e = ec;
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+                if ((n >> (3 - m)) & 1u)
+                    e ^= v[m];
+            row[n ^ c] = e;
+        }
+    }
+}
+
+#endif  // PTLS_MI355X_ENGINE_LDS_TABLES_H

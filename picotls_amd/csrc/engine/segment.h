@@ -1,0 +1,232 @@
+// picotls_amd/csrc/engine/segment.h -- gcm_segment: AES-CTR + GHASH of a range of one record's stream by one 8-lane group.
+// Part of the single translation unit picotls_amd/csrc/aesgcm_engine.hip (included in order; not standalone).
+#ifndef PTLS_MI355X_ENGINE_SEGMENT_H
+#define PTLS_MI355X_ENGINE_SEGMENT_H
+
+// GHASH/CTR work of one G-lane group on steps [m_lo, m_hi) of record r's stream (see file header): lane j owns stream
+// positions j + G*m and runs them NB at a time. The NB AES-CTR blocks of a step are independent (NB x 16 LDS lookups
+// per round in flight); their GHASH folds stay sequential (Horner with H^G, the segment's last step with H^(G-j)).
+// On return every lane of the group holds the segment's GHASH partial sum(X_i * H^(end - i)) and the length lane
+// (lane G-1, when the segment holds the length block) holds E(K, J0) in ek0. Invalid groups pass m_lo == m_hi.
+template <int NR, bool OPEN, int NB, int FRAME = 0>
+__device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 *lds, const u32 (&rk)[NR + 1][4], u32 iv0,
+                                            u32 iv1, u32 iv2, const ptls_mi355x_record_t &r, bool valid, u32 m_lo,
+                                            u32 m_hi, u32 j, u32 laneoff, u32 tsel_horner, u32 tsel_last, u32x4 &acc,
+                                            u32x4 &ek0, bool finish, u64 rec)
+{
+    constexpr int G = ENGINE_G;
+    constexpr bool SEAL_FRAME = FRAME == 1 && !OPEN, OPEN_FRAME = FRAME == 1 && OPEN, TLS12 = FRAME == 2;
+    const u32 L = gcm_text_len<OPEN, FRAME>(r), A = gcm_aad_len<OPEN, FRAME>(r);
+    // bytes of text readable at src (a framed seal reads len payload bytes; its last text byte is the content type)
+    const u32 Lsrc = SEAL_FRAME ? L - 1 : L;
+    const u32 na = (A + 15) >> 4, nb = (L + 15) >> 4;
+    const u32 total = na + nb + 1;
+    const u32 K = (total + G - 1) / G;
+    const int P = (int)(K * G) - (int)total;
+
+    const u32 Smax = wave_max_per8(m_hi - m_lo);  // m_lo, m_hi are uniform within a group
+
+    // nonce = iv ^ (0^32 || BE64(seq)) (lib/picotls.c:6587-6601); TLS 1.2 takes the explicit nonce of the record in
+    // place of seq, read as stored (big endian), so its two words need no swap
+    u32 nw1 = bswap32((u32)(r.seq >> 32)), nw2 = bswap32((u32)r.seq);
+    if (TLS12) {
+        const uint8_t *e = args.in + r.in_off + (OPEN ? TLS_HEADER_SIZE : 0);
+        nw1 = *(const u32_u *)e;
+        nw2 = *(const u32_u *)(e + 4);
+    }
+    const u32 n0 = iv0 ^ rk[0][0];
+    const u32 n1 = iv1 ^ nw1 ^ rk[0][1];
+    const u32 n2 = iv2 ^ nw2 ^ rk[0][2];
+    const uint8_t *src = args.in + r.in_off + frame_in_skip<OPEN, FRAME>();
+    uint8_t *dst = args.out + r.out_off + frame_out_skip<OPEN, FRAME>();
+    const uint8_t *aadp = OPEN_FRAME ? args.in + r.in_off : args.aad + r.aad_off;
+
+    acc = u32x4{0, 0, 0, 0};
+    ek0 = u32x4{0, 0, 0, 0};
+
+    static_assert(NB == 1, "the counter cache runs one block per lane and step");
+    CtrCache1 cc1 = {};
+    u32 cc1_key = 0xffffffffu;  // counter >> 8 of the cached window (none yet)
+
+    // data block of lane j at step m: b = j + G*m - P - na; a full 16-byte input block is loaded one step ahead, so
+    // its HBM latency hides under the AES of the current step
+    auto full_block = [&](u32 m, int &b) -> bool {
+        b = (int)(j + G * m) - P - (int)na;
+        return m < m_hi && b >= 0 && b < (int)nb && Lsrc - 16u * (u32)b >= 16;
+    };
+    u32x4 nxt[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        int b;
+        nxt[i] = u32x4{0, 0, 0, 0};
+        if (full_block(m_lo + i, b))
+            nxt[i] = *(const u32x4_u *)(src + 16u * (u32)b);
+    }
+
+    // step m, part 1: the next step's input prefetch and this step's counter block (refreshing the counter cache when
+    // the lane enters a new 256-counter window)
+    u32x4 cur;
+    auto setup_step = [&](u32 m0, u32 (&st)[1][4]) {
+        cur = nxt[0];
+        int bn;
+        if (full_block(m0 + 1, bn))
+            nxt[0] = *(const u32x4_u *)(src + 16u * (u32)bn);
+        // AES-CTR input: data positions encrypt counter 2+b, all others J0 (kept by the length lane as E(K, J0))
+        const int logical = (int)(j + G * m0) - P;
+        const int b = logical - (int)na;
+        const bool is_data = m0 < m_hi && logical >= (int)na && b < (int)nb;
+        st[0][0] = n0, st[0][1] = n1, st[0][2] = n2;
+        const u32 ctr = is_data ? (u32)(b + 2) : 1u;
+        st[0][3] = bswap32(ctr) ^ rk[0][3];
+        if ((ctr >> 8) != cc1_key) {  // entering a new 256-counter window (divergent; skipped when no lane does)
+            cc1 = ctr_cache1_init<NR>(lds, laneoff, rk, n0, n1, n2, st[0][3]);
+            cc1_key = ctr >> 8;
+        }
+    };
+    // step m, part 2: with the keystream block ks, write the output and return the GHASH input block X of position
+    // j + G*m
+    auto finish_step = [&](u32 m, const u32x4 &ks) -> u32x4 {
+        const bool act = m < m_hi;
+        const int logical = (int)(j + G * m) - P;
+        const int b = logical - (int)na;
+        const bool is_data = act && logical >= (int)na && b < (int)nb;
+        const bool is_aad = act && logical >= 0 && logical < (int)na;
+        const bool is_len = act && logical == (int)(na + nb);
+        u32x4 X = {0, 0, 0, 0};
+#if ENGINE_FAST_STEP
+        // steady state: every active lane of the wave holds a full 16-byte text block (one uniform branch, no
+        // per-case dispatch)
+        const bool full = is_data && Lsrc - 16u * (u32)b >= 16;
+        if (__all(!act || full)) {
+            const u32x4 o = cur ^ ks;
+            if (act)
+                *(u32x4_u *)(dst + 16u * (u32)b) = o;
+            return OPEN ? cur : o;
+        }
+#endif
+        if (is_data) {
+            const u32 rem = L - 16u * (u32)b;
+            uint8_t *op = dst + 16u * (u32)b;
+            if (rem >= 16 && (!SEAL_FRAME || Lsrc - 16u * (u32)b >= 16)) {
+                const u32x4 v = cur;
+                const u32x4 o = v ^ ks;
+                *(u32x4_u *)op = o;
+                X = OPEN ? v : o;
+            } else {
+                const u32 srem = Lsrc - 16u * (u32)b;
+                u32x4 v = load_partial(src + 16u * (u32)b, srem);
+                if (SEAL_FRAME)  // the inner content type follows the payload
+                    v[srem >> 2] |= (u32)(r.flags & 0xffu) << (8 * (srem & 3));
+                const u32x4 o = rem >= 16 ? v ^ ks : mask_tail(v ^ ks, rem);
+                if (rem >= 16)
+                    *(u32x4_u *)op = o;
+                else
+                    store_partial(op, o, rem);
+                X = OPEN ? v : o;
+            }
+        } else if (is_aad) {
+            if (SEAL_FRAME) {  // the record header: built here, written to the wire, and authenticated
+                const u32 wl = L + 16;
+                X = u32x4{0x00030317u | ((wl >> 8) & 0xffu) << 24, wl & 0xffu, 0, 0};
+                store_partial(args.out + r.out_off, X, TLS_HEADER_SIZE);
+            } else if (TLS12) {  // AAD = BE64(seq) || type || 3 || 3 || BE16(len) (build_tls12_aad)
+                const u32 type = OPEN ? (u32)args.in[r.in_off] : (r.flags & 0xffu);
+                X = u32x4{bswap32((u32)(r.seq >> 32)), bswap32((u32)r.seq), type | 0x030300u | ((L >> 8) & 0xffu) << 24,
+                          L & 0xffu};
+                if (!OPEN) {  // the wire header and the explicit nonce
+                    const u32 wl = TLS12_RECORD_IV_SIZE + L + 16;
+                    const u32x4 h = {type | 0x030300u | ((wl >> 8) & 0xffu) << 24, (wl & 0xffu) | nw1 << 8,
+                                     nw1 >> 24 | nw2 << 8, nw2 >> 24};
+                    store_partial(args.out + r.out_off, h, TLS_HEADER_SIZE + TLS12_RECORD_IV_SIZE);
+                }
+            } else {
+                const u32 rem = A - 16u * (u32)logical;
+                const uint8_t *ap = aadp + 16u * (u32)logical;
+                X = rem >= 16 ? *(const u32x4_u *)ap : load_partial(ap, rem);
+            }
+        } else if (is_len) {
+            const u64 abits = (u64)A * 8, cbits = (u64)L * 8;
+            X[0] = bswap32((u32)(abits >> 32));
+            X[1] = bswap32((u32)abits);
+            X[2] = bswap32((u32)(cbits >> 32));
+            X[3] = bswap32((u32)cbits);
+            ek0 = ks;
+        }
+        return X;
+    };
+
+    // Steady state: the steps [sa, sb) (relative to m_lo, wave-uniform) in which every lane of every group of the wave
+    // holds a full text block, the next step's block is full too (the prefetch needs no check) and no group is at its
+    // segment's last step (Horner with H^G throughout). They run without the per-lane position logic: the counter,
+    // source and destination just advance by one step, about 30 VALU operations fewer per block.
+    const int D0 = P + (int)na;         // stream position of text block 0
+    const int nbf = (int)(Lsrc >> 4);   // full text blocks
+    const int ms = (D0 + G - 1) / G;    // first step whose 8 positions are all >= D0
+    const int me = nbf + D0 >= G ? (nbf + D0 - G) / G : -1;  // last step whose 8 positions are all full text
+    int sa = max(ms, (int)m_lo) - (int)m_lo;
+    int sb = min(me - 1, (int)m_hi - 2) + 1 - (int)m_lo;
+    if (!valid || m_hi <= m_lo)
+        sa = 1, sb = 0;
+    sa = wave_smax_per8(sa);
+    sb = wave_smin_per8(sb);
+
+    for (u32 s0 = 0; s0 < Smax; ++s0) {
+        if ((int)s0 == sa && sb > sa) {
+            const int b0 = (int)(j + G * (m_lo + (u32)sa)) - D0;  // this lane's text block at step sa
+            u32 off = 16u * (u32)b0;                               // its byte offset in the text
+            u32 ctr = (u32)b0 + 2;
+            for (int s = sa; s < sb; ++s) {
+                cur = nxt[0];
+                nxt[0] = *(const u32x4_u *)(src + off + 16 * G);
+                u32 st[1][4] = {{n0, n1, n2, bswap32(ctr) ^ rk[0][3]}};
+                if ((ctr >> 8) != cc1_key) {
+                    cc1 = ctr_cache1_init<NR>(lds, laneoff, rk, n0, n1, n2, st[0][3]);
+                    cc1_key = ctr >> 8;
+                }
+                aes_ctr_cached1<NR>(lds, laneoff, rk, cc1, st);
+                __builtin_amdgcn_sched_barrier(0);
+                const u32x4 o = cur ^ u32x4{st[0][0], st[0][1], st[0][2], st[0][3]};
+                *(u32x4_u *)(dst + off) = o;
+                __builtin_amdgcn_sched_barrier(0);
+                acc = gmul_tab(lds, acc ^ (OPEN ? cur : o), tsel_horner);
+                __builtin_amdgcn_sched_barrier(0);
+                ctr += G;
+                off += 16 * G;
+            }
+            s0 = (u32)sb;
+        }
+        const u32 m0 = m_lo + s0;
+        u32 st[1][4];
+        setup_step(m0, st);
+        aes_ctr_cached1<NR>(lds, laneoff, rk, cc1, st);
+        __builtin_amdgcn_sched_barrier(0);
+        const u32x4 X = finish_step(m0, u32x4{st[0][0], st[0][1], st[0][2], st[0][3]});
+        // scheduling fence: keeps the 32 table loads of this fold from being hoisted next to the other work (that
+        // hoisting spills them to scratch)
+        __builtin_amdgcn_sched_barrier(0);
+        const u32x4 prod = gmul_tab(lds, acc ^ X, m0 + 1 == m_hi ? tsel_last : tsel_horner);
+        if (m0 < m_hi)
+            acc = prod;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // XOR over the G lanes of the group
+    static_assert(G == 8, "dpp_xor8 reduces groups of 8 lanes");
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        acc[c] = dpp_xor8(acc[c]);
+    // whole record (finish): tag = GHASH ^ E(K, J0), written after the ciphertext (seal) or compared with the
+    // received one (open)
+    if (finish && valid && j == G - 1) {
+        const u32x4 tag = acc ^ ek0;
+        if (OPEN) {
+            const u32x4 rt = *(const u32x4_u *)(src + L);
+            const u32x4 d = rt ^ tag;
+            args.ok[rec] = (d[0] | d[1] | d[2] | d[3]) == 0;
+        } else {
+            *(u32x4_u *)(dst + L) = tag;
+        }
+    }
+}
+
+#endif  // PTLS_MI355X_ENGINE_SEGMENT_H
