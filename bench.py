@@ -128,6 +128,10 @@ def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool
     lens = b.seal["len"]
     res["seal_alg_bytes"] = algorithmic_bytes(lens, b.seal["aad_len"], True)
     res["open_alg_bytes"] = algorithmic_bytes(lens, b.seal["aad_len"], False)
+    # GHASH stream positions the seal kernel walks (8 lanes x steps per record, padding included): the LDS model's unit
+    na = (b.seal["aad_len"].astype(np.int64) + 15) // 16
+    nb = (lens.astype(np.int64) + 15) // 16
+    res["stream_blocks"] = int((((na + nb + 1 + 7) // 8) * 8).sum())
 
     if verify:
         ok_all = bool(d_ok.min().item() == 1) if b.n else True
@@ -350,6 +354,20 @@ def run_e2e(R, wl, nchunks: int = 16, reps: int = 3, schedule: str = "auto"):
     return out
 
 
+def lds_model(res, key_size: int):
+    """The bound the seal kernel actually meets: LDS table lookups. Per GHASH stream block an AES-128
+    block costs 133 ds_read_b32 (AES-256: 197) and its GHASH fold 32 ds_read_b128 (one 4-bit window each); at the MI355X
+    aggregate LDS rates (MI355X_MICROARCH.md: ~75 TB/s ds_read_b32, ~150 TB/s ds_read_b128 with every CU at 2.4 GHz)
+    that gives the chip's block rate ceiling; frac = achieved blocks/s over it (the clock under this load is lower)."""
+    lookups = 133 if key_size == 16 else 197
+    sec_per_block = lookups * 4 / 75e12 + 32 * 16 / 150e12
+    peak = 1.0 / sec_per_block
+    achieved = res["stream_blocks"] / (res["seal_ms"] / 1e3)
+    return {"bound": "lds", "unit": "stream blocks/s", "achieved": round(achieved, -6), "peak_at_2.4GHz": round(peak, -6),
+            "frac": round(achieved / peak, 4),
+            "per_block": f"{lookups} ds_read_b32 (AES) + 32 ds_read_b128 (GHASH)"}
+
+
 def traffic_from_profiles(workload: str, records: int):
     """Corrected HBM bytes per seal launch from the committed rocprofv3 PMC summary (profiles/pmc_<workload>.json),
     scaled to this run's record count when the profile was taken on a different one."""
@@ -408,6 +426,7 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic_from_profiles(wl.name, res["records"]),
                      "alg_bytes_per_launch": res["seal_alg_bytes"], "avg_launch_ms": round(res["seal_ms"], 4),
                      "open_achieved": round(res["open_alg_bytes"] / open_s / 1e9, 2)},
+        "lds_model": lds_model(res, wl.key_size),
         "verified": {"roundtrip": res.get("verified_roundtrip"), "fusion_spot_check": res.get("fusion_spot_check")},
     }
     extra = {}
