@@ -86,3 +86,31 @@ def test_payload_generator_is_seekable():
     a = workloads.payload_np(0x5EED, 0, 4096)
     b = workloads.payload_np(0x5EED, 1024, 2048)
     assert a[1024:3072].tobytes() == b.tobytes()
+
+
+def test_many_key_workload_orders():
+    # "mixed": records grouped by connection; "mixedrand": SURVEY 8(d) config 4 as written (key = splitmix(i) mod
+    # nkeys). Either way seq counts each connection's records 0, 1, 2, ... in batch order, and a shard is a slice
+    for name in ("mixed", "mixedrand"):
+        wl = workloads.WORKLOADS[name].scaled(20000)
+        key, seq = wl.key_and_seq(0, wl.nrecs)
+        assert key.max() < wl.nkeys
+        for k in np.unique(key)[:50]:
+            assert (seq[key == k] == np.arange((key == k).sum())).all()
+        k2, s2 = wl.key_and_seq(7000, 9000)
+        assert (k2 == key[7000:9000]).all() and (s2 == seq[7000:9000]).all()
+    grouped = workloads.WORKLOADS["mixed"].scaled(20000).key_and_seq(0, 20000)[0]
+    rand = workloads.WORKLOADS["mixedrand"].scaled(20000).key_and_seq(0, 20000)[0]
+    assert (np.diff(grouped.astype(np.int64)) >= 0).all()
+    assert (np.diff(rand.astype(np.int64)) != 0).mean() > 0.9  # runs of one record: the device regroups these
+
+
+def test_lds_model_ceiling():
+    import bench
+
+    res = {"stream_blocks": 10**9, "seal_ms": 10.0}
+    m = bench.lds_model(res, 16)
+    # 133 x 4 B at 75 TB/s + 32 x 16 B at 150 TB/s per block
+    assert abs(m["peak_at_2.4GHz"] - 1 / (532 / 75e12 + 512 / 150e12)) < 1e6
+    assert abs(m["frac"] - 1e11 / m["peak_at_2.4GHz"]) < 1e-3
+    assert bench.lds_model(res, 32)["peak_at_2.4GHz"] < m["peak_at_2.4GHz"]
