@@ -273,7 +273,7 @@ int ptls_mi355x_debug_profile(unsigned long long *out, int reset)
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(g_prof)));
     if (reset) {
-        static const unsigned long long z[8] = {};
+        static const unsigned long long z[16] = {};
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));
     }
     return 0;

@@ -129,6 +129,29 @@ __device__ __forceinline__ u32 dpp_bcast7(u32 v, u32 lane)
     const u32 u = (u32)__builtin_amdgcn_update_dpp(0, (int)t, 0x141, 0xF, 0xF, false);
     return (lane & 4) ? t : u;
 }
+// Whole-wave inclusive scans on DPP (row_shr 1/2/4/8 inside each 16-lane row, then row_bcast 15 / 31 across rows):
+// six dependent VALU ops instead of six ds_bpermute round trips. Lanes without a source take the identity.
+template <typename Op>
+__device__ __forceinline__ u32 dpp_scan(u32 v, u32 ident, Op op)
+{
+    v = op(v, (u32)__builtin_amdgcn_update_dpp((int)ident, (int)v, 0x111, 0xF, 0xF, false));
+    v = op(v, (u32)__builtin_amdgcn_update_dpp((int)ident, (int)v, 0x112, 0xF, 0xF, false));
+    v = op(v, (u32)__builtin_amdgcn_update_dpp((int)ident, (int)v, 0x114, 0xF, 0xF, false));
+    v = op(v, (u32)__builtin_amdgcn_update_dpp((int)ident, (int)v, 0x118, 0xF, 0xF, false));
+    v = op(v, (u32)__builtin_amdgcn_update_dpp((int)ident, (int)v, 0x142, 0xA, 0xF, false));
+    v = op(v, (u32)__builtin_amdgcn_update_dpp((int)ident, (int)v, 0x143, 0xC, 0xF, false));
+    return v;
+}
+__device__ __forceinline__ u32 wave_incl_sum(u32 v) { return dpp_scan(v, 0u, [](u32 a, u32 b) { return a + b; }); }
+__device__ __forceinline__ u32 wave_min(u32 v)
+{
+    return (u32)__builtin_amdgcn_readlane((int)dpp_scan(v, 0xffffffffu, [](u32 a, u32 b) { return min(a, b); }), 63);
+}
+__device__ __forceinline__ u32 wave_max(u32 v)
+{
+    return (u32)__builtin_amdgcn_readlane((int)dpp_scan(v, 0u, [](u32 a, u32 b) { return max(a, b); }), 63);
+}
+
 // maximum over the wave of a value that is uniform within each 8-lane group
 __device__ __forceinline__ u32 wave_max_per8(u32 v)
 {

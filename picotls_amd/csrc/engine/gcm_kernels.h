@@ -126,7 +126,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
 #define ENGINE_PROFILE 0
 #endif
 #if ENGINE_PROFILE
-__device__ unsigned long long g_prof[8];
+__device__ unsigned long long g_prof[16];
 __device__ __forceinline__ unsigned long long stamp()
 {
     unsigned long long t;
@@ -223,19 +223,10 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 if (!other_key)
                     smin = smax = steps;
             }
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) {
-                smin = min(smin, (u32)__shfl_xor((int)smin, off, 64));
-                smax = max(smax, (u32)__shfl_xor((int)smax, off, 64));
-            }
+            smin = wave_min(smin);
+            smax = wave_max(smax);
             const u64 kb = __ballot(other_key || t >= lim);
-            incl = nc;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const u32 y = (u32)__shfl_up((int)incl, off, 64);
-                if (lane >= (u32)off)
-                    incl += y;
-            }
+            incl = wave_incl_sum(nc);
             if (lane == 63) {
                 s_ctl[4 + wave] = incl;
                 s_ctl[8 + wave] = kb ? 64 * wave + (u32)__builtin_ctzll(kb) : 0xffffffffu;
@@ -247,6 +238,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 s_ctl[1] = 0;
         }
         __syncthreads();
+        PROF_STAMP(ts1);
         u32 run_n = lim, smin = 0xffffffffu, smax = 0;
 #pragma unroll
         for (u32 w = 0; w < SCAN_WAVES; ++w) {
@@ -272,6 +264,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 s_ctl[12 + wave] = cut ? 64 * wave + (u32)__builtin_ctzll(cut) : 0xffffffffu;
         }
         u32 nhuge = 0;
+        PROF_STAMP(ts2);
         if (!whole) {
             __syncthreads();
 #pragma unroll
@@ -293,6 +286,9 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 }
             }
             __syncthreads();
+            PROF_STAMP(ts3);
+            if (threadIdx.x == 0)
+                PROF_ADD(10, ts3 - ts2);
             if (wave < SCAN_WAVES) {
                 // lane b: first slot of this wave's bucket-b records = all records of earlier buckets (prefix over
                 // lanes) + bucket b of earlier waves; a record then takes lane bkt's value (no serial walk)
@@ -303,13 +299,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                     tot += c;
                     mine += w < wave ? c : 0u;
                 }
-                u32 before = tot;
-#pragma unroll
-                for (int off = 1; off < 32; off <<= 1) {
-                    const u32 y = (u32)__shfl_up((int)before, off, 64);
-                    if (lane >= (u32)off)
-                        before += y;
-                }
+                const u32 before = wave_incl_sum(tot);
                 const u32 first_slot = before - tot + mine;
                 const u32 base = (u32)__shfl((int)first_slot, (int)bkt, 64);
                 if (threadIdx.x < run_n)
@@ -454,6 +444,9 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             PROF_ADD(2, t3 - t2);
             PROF_ADD(5, total_units);
             PROF_ADD(6, 1);
+            PROF_ADD(8, ts1 - t0);
+            PROF_ADD(9, ts2 - ts1);
+            PROF_ADD(11, t1 - ts2);
             if (pos == beg)
                 PROF_ADD(3, t0 - tk);
         }

@@ -37,7 +37,7 @@ def main():
     ks = ctypes.c_void_p(lib.ptls_mi355x_keyset_new(keys.ctypes.data, ivs.ctypes.data, wl.nkeys, wl.key_size))
     lib.ptls_mi355x_keyset_set_schedule(ks, a.schedule)
     s = torch.cuda.current_stream().cuda_stream
-    prof = (ctypes.c_ulonglong * 8)()
+    prof = (ctypes.c_ulonglong * 16)()
     lib.ptls_mi355x_seal_batch(ks, d_seal.data_ptr(), b.n, d_pt.data_ptr(), d_aad.data_ptr(), sealed.data_ptr(), s)
     torch.cuda.synchronize()
     lib.ptls_mi355x_debug_profile(prof, 1)
@@ -56,6 +56,9 @@ def main():
           f"units/run {p[5] / runs:.1f}, table builds/launch {p[7] / a.reps:.0f}")
     for i, name in enumerate(["run setup", "table build", "unit loop", "prologue"]):
         print(f"  {name:12s} {p[i] / runs:10.0f} cycles/run  {100 * p[i] / max(tot, 1):5.1f} %")
+    if any(p[8:12]):
+        print("  run setup split (cycles/run): scan+B1 %.0f | decide+prefix %.0f | buckets+B3 %.0f | B2..end %.0f" %
+              (p[8] / runs, p[9] / runs, p[10] / runs, p[11] / runs))
     waves = 16
     print(f"  wave idle at unit-loop barrier: {p[4] / runs / waves:.0f} cycles/run/wave "
           f"({100 * p[4] / waves / max(p[2], 1):.1f} % of the unit loop)")
