@@ -249,7 +249,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         // uniform run: every record is one unit (no partials), and a one-key batch may take a much longer run. A
         // workgroup with fewer records left than it has groups cuts them into units instead, so that a small batch
         // (the per-record picotls path is a batch of one) spreads over the workgroup's waves.
-        const bool whole = smax <= smin + UNIFORM_SLACK && end - pos >= WHOLE_MIN_RECS;
+        const bool whole = __builtin_amdgcn_readfirstlane(smax <= smin + UNIFORM_SLACK && end - pos >= WHOLE_MIN_RECS);
         if (whole && !args.multi_key)
             run_n = (u32)min(end - pos, (u64)WHOLE_RUN_RECS);
         if (!whole && wave < SCAN_WAVES) {
@@ -310,7 +310,11 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 nhuge += s_ctl[32 + BKT_STRIDE * w];
             __syncthreads();
         }
-        const u32 total_units = whole ? run_n : s_ubase[run_n];
+        // run-level values are workgroup-uniform: keep them in SGPRs (they live across the unit loop, where VGPRs are
+        // the scarce resource)
+        run_n = __builtin_amdgcn_readfirstlane(run_n);
+        nhuge = __builtin_amdgcn_readfirstlane(nhuge);
+        const u32 total_units = __builtin_amdgcn_readfirstlane(whole ? run_n : s_ubase[run_n]);
         const u32 nfull = total_units - run_n;
         const u64 run_end = pos + run_n;
         PROF_STAMP(t1);
