@@ -262,6 +262,10 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             const u64 cut = __ballot(incl > CRUN_UNITS);
             if (lane == 0)
                 s_ctl[12 + wave] = cut ? 64 * wave + (u32)__builtin_ctzll(cut) : 0xffffffffu;
+            if (lim == 1 && threadIdx.x == 0) {  // a lone record (a launch of one): its unit order needs no sort
+                s_front[0] = 0;
+                s_ctl[2] = bkt == 0;
+            }
         }
         u32 nhuge = 0;
         PROF_STAMP(ts2);
@@ -270,45 +274,49 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
 #pragma unroll
             for (u32 w = 0; w < SCAN_WAVES; ++w)
                 run_n = min(run_n, max(s_ctl[12 + w], 1u));
+            if (lim == 1)
+                nhuge = s_ctl[2];
             // Unit order: [front units of very long records][all full units, record-major][the other front units by
             // size, largest first]. Lockstep waves then draw units of equal or similar length, and the run ends on
             // its shortest units. Counting sort of the front units by bucket: per-wave counts, then positions.
-            u32 rank = 0;
-            if (wave < SCAN_WAVES) {
-                const bool in = threadIdx.x < run_n;
+            if (lim != 1) {  // (a lone record's order was set before the barrier above)
+                u32 rank = 0;
+                if (wave < SCAN_WAVES) {
+                    const bool in = threadIdx.x < run_n;
 #pragma unroll
-                for (u32 b = 0; b <= CHUNK_STEPS; ++b) {
-                    const u64 m = __ballot(in && bkt == b);
-                    if (lane == 0)
-                        s_ctl[32 + BKT_STRIDE * wave + b] = (u32)__popcll(m);
-                    if (in && bkt == b)
-                        rank = (u32)__popcll(m & ((1ull << lane) - 1));
+                    for (u32 b = 0; b <= CHUNK_STEPS; ++b) {
+                        const u64 m = __ballot(in && bkt == b);
+                        if (lane == 0)
+                            s_ctl[32 + BKT_STRIDE * wave + b] = (u32)__popcll(m);
+                        if (in && bkt == b)
+                            rank = (u32)__popcll(m & ((1ull << lane) - 1));
+                    }
                 }
-            }
-            __syncthreads();
-            PROF_STAMP(ts3);
-            if (threadIdx.x == 0)
-                PROF_ADD(10, ts3 - ts2);
-            if (wave < SCAN_WAVES) {
-                // lane b: first slot of this wave's bucket-b records = all records of earlier buckets (prefix over
-                // lanes) + bucket b of earlier waves; a record then takes lane bkt's value (no serial walk)
-                u32 tot = 0, mine = 0;
+                __syncthreads();
+                PROF_STAMP(ts3);
+                if (threadIdx.x == 0)
+                    PROF_ADD(10, ts3 - ts2);
+                if (wave < SCAN_WAVES) {
+                    // lane b: first slot of this wave's bucket-b records = all records of earlier buckets (prefix over
+                    // lanes) + bucket b of earlier waves; a record then takes lane bkt's value (no serial walk)
+                    u32 tot = 0, mine = 0;
 #pragma unroll
-                for (u32 w = 0; w < SCAN_WAVES; ++w) {
-                    const u32 c = lane < BKT_STRIDE ? s_ctl[32 + BKT_STRIDE * w + lane] : 0u;
-                    tot += c;
-                    mine += w < wave ? c : 0u;
+                    for (u32 w = 0; w < SCAN_WAVES; ++w) {
+                        const u32 c = lane < BKT_STRIDE ? s_ctl[32 + BKT_STRIDE * w + lane] : 0u;
+                        tot += c;
+                        mine += w < wave ? c : 0u;
+                    }
+                    const u32 before = wave_incl_sum(tot);
+                    const u32 first_slot = before - tot + mine;
+                    const u32 base = (u32)__shfl((int)first_slot, (int)bkt, 64);
+                    if (threadIdx.x < run_n)
+                        s_front[base + rank] = threadIdx.x;
                 }
-                const u32 before = wave_incl_sum(tot);
-                const u32 first_slot = before - tot + mine;
-                const u32 base = (u32)__shfl((int)first_slot, (int)bkt, 64);
-                if (threadIdx.x < run_n)
-                    s_front[base + rank] = threadIdx.x;
-            }
 #pragma unroll
-            for (u32 w = 0; w < SCAN_WAVES; ++w)
-                nhuge += s_ctl[32 + BKT_STRIDE * w];
-            __syncthreads();
+                for (u32 w = 0; w < SCAN_WAVES; ++w)
+                    nhuge += s_ctl[32 + BKT_STRIDE * w];
+                __syncthreads();
+            }
         }
         // run-level values are workgroup-uniform: keep them in SGPRs (they live across the unit loop, where VGPRs are
         // the scarce resource)
