@@ -92,14 +92,19 @@ static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 #define WHOLE_RUN_RECS 4096  // records per run when a one-key run is uniform (every record one unit)
 #define UNIFORM_SLACK 2      // a run is uniform when its records' step counts differ by at most this
 #define WHOLE_MIN_RECS (ENGINE_WG / ENGINE_G)  // whole-record mode needs at least one record per 8-lane group
-#define CLDS_CTL_WORDS ((32 + (CRUN_RECS / 64) * BKT_STRIDE + 127) / 128 * 128)
-#define CLDS_CTL (LDS_BYTES + GHASH_TABLE_BYTES)                // CLDS_CTL_WORDS control words
-#define CLDS_UBASE (CLDS_CTL + 4 * CLDS_CTL_WORDS)              // u32[CRUN_RECS + 1]: first unit of each record
-#define CLDS_DONE (CLDS_UBASE + 4 * (CRUN_RECS + 16))           // u32[CRUN_RECS]: finished units per record
-#define CLDS_EK0 (CLDS_DONE + 4 * CRUN_RECS)                    // 16 B per record: E(K, J0)
-#define CLDS_PART (CLDS_EK0 + 16 * CRUN_RECS)                   // 16 B per unit: GHASH partial
-#define CLDS_FRONT (CLDS_PART + 16 * CRUN_UNITS)                // u32[CRUN_RECS]: records by front-unit size
-#define CLDS_ALLOC (CLDS_FRONT + 4 * CRUN_RECS)
+// Per-run state, double-buffered so that one wave can scan run r+1 while the others finish run r (scan_run):
+// ctl[16] | ubase u32[CRUN_RECS + 16] (first unit of each record) | done u32[CRUN_RECS] (finished units per record) |
+// front u32[CRUN_RECS] (records by front-unit size). Then the unit partials (single: run r+1's units start after the
+// end-of-run barrier).
+#define RUN_CTL_WORDS 16
+#define RUN_UBASE_OFF RUN_CTL_WORDS
+#define RUN_DONE_OFF (RUN_UBASE_OFF + CRUN_RECS + 16)
+#define RUN_FRONT_OFF (RUN_DONE_OFF + CRUN_RECS)
+#define RUN_WORDS (RUN_FRONT_OFF + CRUN_RECS)
+#define CLDS_RUN0 (LDS_BYTES + GHASH_TABLE_BYTES)
+#define CLDS_RUN1 (CLDS_RUN0 + 4 * RUN_WORDS)
+#define CLDS_PART (CLDS_RUN1 + 4 * RUN_WORDS)                    // 16 B per unit: GHASH partial
+#define CLDS_ALLOC (CLDS_PART + 16 * CRUN_UNITS)
 static_assert(CLDS_ALLOC <= 160 * 1024, "chunked schedule LDS budget");
 static_assert(CHUNK_BLOCKS % ENGINE_G == 0, "units are whole steps");
 static_assert((CHUNK_STEPS & (CHUNK_STEPS - 1)) == 0 && CHUNK_STEPS <= 16, "unit lengths are powers of two up to 16 steps");

@@ -142,6 +142,131 @@ __device__ __forceinline__ unsigned long long stamp()
 #define PROF_ADD(i, x)
 #endif
 
+// Run-state control words (RUN_CTL_WORDS per buffer)
+#define RC_KEY 0     // key index of the run
+#define RC_NEXT 1    // next unit to hand out
+#define RC_N 2       // records in the run
+#define RC_WHOLE 3   // every record is one unit
+#define RC_UNITS 4   // units in the run
+#define RC_HUGE 5    // records whose front unit goes first (longer than CHUNK_MAX_UNITS units)
+#define RC_CLAIM 6   // the first wave to find this run's queue empty scans the next run
+
+// Scans the run that starts at record p into one run-state buffer, with ONE wave and no workgroup barrier, so that it
+// runs while the other waves are still busy with the previous run (the end-of-run tail where they would otherwise
+// wait). A run is records [p, p + n) with one key: at most CRUN_RECS records and CRUN_UNITS units, or (a uniform run of
+// a one-key batch) up to WHOLE_RUN_RECS whole records. Each lane takes records q * 64 + lane, q < CRUN_RECS / 64.
+// Outputs: ctl[RC_*], ubase[0..n] (prefix of unit counts), front[] (records ordered [very long][the others by
+// front-unit size, largest first]; the kernel numbers units [their front units][all full units][the other front
+// units]) and done[0..n) = 0. All lanes of the wave must be active.
+template <bool OPEN, int FRAME>
+__device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355x_record_t *__restrict__ recs, u64 p, u64 end,
+                                      lds_u32 *rs)
+{
+    constexpr u32 Q = CRUN_RECS / 64;
+    lds_u32 *ubase = rs + RUN_UBASE_OFF, *done = rs + RUN_DONE_OFF, *front = rs + RUN_FRONT_OFF;
+    const u32 lane = threadIdx.x & 63;
+    const u32 log2 = args.unit_log2, ustep = 1u << log2;
+    const u32 lim = (u32)min(end - p, (u64)CRUN_RECS);
+    const u32 key = args.multi_key ? recs[p].key_idx : 0u;
+    u32 steps[Q], nc[Q], bkt[Q];
+    u32 n = lim;  // ends at the first record of another key
+#pragma unroll
+    for (u32 q = 0; q < Q; ++q) {
+        const u32 t = q * 64 + lane;
+        steps[q] = nc[q] = bkt[q] = 0;
+        bool other = false;
+        if (t < lim) {
+            ptls_mi355x_record_t r = recs[p + t];
+            other = args.multi_key && r.key_idx != key;
+            if (!record_ok(args, r))  // rejected: one empty unit (see the unit loop)
+                r.len = 0, r.aad_len = 0;
+            steps[q] = gcm_steps<OPEN, FRAME>(r);
+            // front-unit size bucket: 0 = a record too long for CHUNK_MAX_UNITS units (it takes units of a multiple
+            // length, unit_mul), else ustep + 1 - size of the record's first unit (1 = a full unit, ustep = one step)
+            const u32 mul = unit_mul(steps[q], log2);
+            nc[q] = (steps[q] + ustep - 1) >> log2;
+            if (mul > 1)  // rare: the only division
+                nc[q] = (steps[q] + mul * ustep - 1) / (mul * ustep);
+            bkt[q] = mul > 1 ? 0u : ustep + 1 - (steps[q] - (nc[q] - 1) * ustep);
+        }
+        const u64 kb = __ballot(other);
+        if (kb != 0)
+            n = min(n, q * 64 + (u32)__builtin_ctzll(kb));
+    }
+    n = __builtin_amdgcn_readfirstlane(n);
+    u32 smin = 0xffffffffu, smax = 0;
+#pragma unroll
+    for (u32 q = 0; q < Q; ++q)
+        if (q * 64 + lane < n)
+            smin = min(smin, steps[q]), smax = max(smax, steps[q]);
+    smin = wave_min(smin);
+    smax = wave_max(smax);
+    // uniform run: every record is one unit (no partials), and a one-key batch may take a much longer run. A workgroup
+    // with fewer records left than it has groups cuts them into units instead, so that a small batch (the per-record
+    // picotls path is a batch of one) spreads over the workgroup's waves.
+    const bool whole = smax <= smin + UNIFORM_SLACK && end - p >= WHOLE_MIN_RECS;
+    if (whole && !args.multi_key)
+        n = (u32)min(end - p, (u64)WHOLE_RUN_RECS);
+    u32 units = n, nhuge = 0;
+    if (!whole) {
+        // unit prefix in record order; the first record whose units overflow the run's partial slots ends the run
+        // (never the first record)
+        u32 carry = 0, cut = n;
+#pragma unroll
+        for (u32 q = 0; q < Q; ++q) {
+            const u32 t = q * 64 + lane;
+            const u32 incl = carry + wave_incl_sum(t < n ? nc[q] : 0u);
+            if (t < n)
+                ubase[t + 1] = incl;
+            const u64 c = __ballot(t < n && incl > CRUN_UNITS);
+            if (c != 0)
+                cut = min(cut, q * 64 + (u32)__builtin_ctzll(c));
+            carry = (u32)__builtin_amdgcn_readlane((int)incl, 63);
+        }
+        if (lane == 0)
+            ubase[0] = 0;
+        n = __builtin_amdgcn_readfirstlane(min(n, max(cut, 1u)));
+        // counting sort of the records by front-unit bucket: lane b counts bucket b, then an exclusive scan over lanes
+        u32 cnt = 0;
+#pragma unroll
+        for (u32 q = 0; q < Q; ++q)
+#pragma unroll 1
+            for (u32 b = 0; b <= CHUNK_STEPS; ++b) {
+                const u32 c = (u32)__popcll(__ballot(q * 64 + lane < n && bkt[q] == b));
+                cnt += lane == b ? c : 0u;
+            }
+        u32 next = wave_incl_sum(cnt) - cnt;  // lane b: next free slot of bucket b
+        nhuge = (u32)__builtin_amdgcn_readlane((int)cnt, 0);
+#pragma unroll
+        for (u32 q = 0; q < Q; ++q)
+#pragma unroll 1
+            for (u32 b = 0; b <= CHUNK_STEPS; ++b) {
+                const bool in = q * 64 + lane < n && bkt[q] == b;
+                const u64 m = __ballot(in);
+                if (m == 0)
+                    continue;
+                if (in)
+                    front[(u32)__builtin_amdgcn_readlane((int)next, (int)b) + (u32)__popcll(m & ((1ull << lane) - 1))] =
+                        q * 64 + lane;
+                next += lane == b ? (u32)__popcll(m) : 0u;
+            }
+        units = (u32)__builtin_amdgcn_readfirstlane((int)ubase[n]);
+    }
+#pragma unroll
+    for (u32 q = 0; q < Q; ++q)
+        if (q * 64 + lane < n)
+            done[q * 64 + lane] = 0;
+    if (lane == 0) {
+        rs[RC_KEY] = key;
+        rs[RC_NEXT] = 0;
+        rs[RC_N] = n;
+        rs[RC_WHOLE] = whole;
+        rs[RC_UNITS] = units;
+        rs[RC_HUGE] = nhuge;
+        rs[RC_CLAIM] = 0;
+    }
+}
+
 // Chunked schedule for many-key / mixed-length batches. The lockstep kernel above gives each G-lane group a whole
 // record, so a wave runs as long as its longest record and a key run (~64 records of a connection) as long as its
 // longest record too; with U[64 B, 16 KiB] lengths and a workgroup barrier per key that halves throughput twice.
@@ -158,17 +283,9 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     lds_u8 *lds = (lds_u8 *)smem;
     check_lds_base(smem);
     PROF_STAMP(tk);
-    // s_ctl: [1] next unit, [4..7] per-wave unit totals, [8..11] per-wave key boundary, [12..15] per-wave unit cut,
-    // [16..19] / [20..23] per-wave min / max steps, [32 + 16 w + b] per-wave count of front-unit bucket b
-    lds_u32 *s_front = (lds_u32 *)(lds + CLDS_FRONT);
-    lds_u32 *s_ctl = (lds_u32 *)(lds + CLDS_CTL);
-    lds_u32 *s_ubase = (lds_u32 *)(lds + CLDS_UBASE);
-    lds_u32 *s_done = (lds_u32 *)(lds + CLDS_DONE);
-    lds_u32x4 *s_ek0 = (lds_u32x4 *)(lds + CLDS_EK0);
     lds_u32x4 *s_part = (lds_u32x4 *)(lds + CLDS_PART);
     constexpr int G = ENGINE_G;
     constexpr int RPW = 64 / G;
-    constexpr u32 SCAN_WAVES = CRUN_RECS / 64;
 
     const u32 lane = threadIdx.x & 63;
     const u32 j = lane % G;
@@ -194,135 +311,24 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     auto ok_at = [&](u64 i) -> u64 { return perm != nullptr ? (u64)perm[i] : i; };
 
     build_aes_tables(lds);
+    // the first run's state (later runs are scanned during the previous run's tail)
+    if (wave == 0 && beg < end)
+        scan_run<OPEN, FRAME>(args, recs, beg, end, (lds_u32 *)(lds + CLDS_RUN0));
+    __syncthreads();
 
+    u32 rb = 0;  // run-state buffer of the current run
     for (u64 pos = beg; pos < end;) {
         PROF_STAMP(t0);
-        // ---- the run: records [pos, pos + run_n) with one key, at most CRUN_RECS records and CRUN_UNITS units.
-        // Threads 0..CRUN_RECS-1 read one descriptor each: the key boundary and the unit counts come from one pass.
-        const u32 key_idx = args.multi_key ? recs[pos].key_idx : 0u;
-        const u32 lim = (u32)min(end - pos, (u64)CRUN_RECS);
-        u32 nc = 0, incl = 0, bkt = 0;
-        if (wave < SCAN_WAVES) {
-            const u32 t = threadIdx.x;
-            bool other_key = false;
-            u32 smin = 0xffffffffu, smax = 0;
-            if (t < lim) {
-                ptls_mi355x_record_t r = recs[pos + t];
-                if (!record_ok(args, r))  // rejected: one empty unit (see the unit loop)
-                    r.len = 0, r.aad_len = 0;
-                const u32 steps = gcm_steps<OPEN, FRAME>(r);
-                // front-unit size bucket: 0 = a record too long for CHUNK_MAX_UNITS units (it takes units of a
-                // multiple length, unit_mul), else ustep + 1 - size of the record's first unit (1 = a full unit, ustep =
-                // one step)
-                const u32 mul = unit_mul(steps, args.unit_log2);
-                nc = (steps + ustep - 1) >> args.unit_log2;
-                if (mul > 1)  // rare: the only division
-                    nc = (steps + mul * ustep - 1) / (mul * ustep);
-                bkt = mul > 1 ? 0u : ustep + 1 - (steps - (nc - 1) * ustep);
-                other_key = args.multi_key && r.key_idx != key_idx;
-                if (!other_key)
-                    smin = smax = steps;
-            }
-            smin = wave_min(smin);
-            smax = wave_max(smax);
-            const u64 kb = __ballot(other_key || t >= lim);
-            incl = wave_incl_sum(nc);
-            if (lane == 63) {
-                s_ctl[4 + wave] = incl;
-                s_ctl[8 + wave] = kb ? 64 * wave + (u32)__builtin_ctzll(kb) : 0xffffffffu;
-                s_ctl[16 + wave] = smin;
-                s_ctl[20 + wave] = smax;
-            }
-            s_done[t] = 0;
-            if (t == 0)
-                s_ctl[1] = 0;
-        }
-        __syncthreads();
-        PROF_STAMP(ts1);
-        u32 run_n = lim, smin = 0xffffffffu, smax = 0;
-#pragma unroll
-        for (u32 w = 0; w < SCAN_WAVES; ++w) {
-            run_n = min(run_n, s_ctl[8 + w]);
-            smin = min(smin, s_ctl[16 + w]);
-            smax = max(smax, s_ctl[20 + w]);
-        }
-        // uniform run: every record is one unit (no partials), and a one-key batch may take a much longer run. A
-        // workgroup with fewer records left than it has groups cuts them into units instead, so that a small batch
-        // (the per-record picotls path is a batch of one) spreads over the workgroup's waves.
-        const bool whole = __builtin_amdgcn_readfirstlane(smax <= smin + UNIFORM_SLACK && end - pos >= WHOLE_MIN_RECS);
-        if (whole && !args.multi_key)
-            run_n = (u32)min(end - pos, (u64)WHOLE_RUN_RECS);
-        if (!whole && wave < SCAN_WAVES) {
-            for (u32 w = 0; w < wave; ++w)
-                incl += s_ctl[4 + w];
-            s_ubase[threadIdx.x + 1] = incl;
-            if (threadIdx.x == 0)
-                s_ubase[0] = 0;
-            // the first record whose units overflow the run's partial slots ends the run (never the first record)
-            const u64 cut = __ballot(incl > CRUN_UNITS);
-            if (lane == 0)
-                s_ctl[12 + wave] = cut ? 64 * wave + (u32)__builtin_ctzll(cut) : 0xffffffffu;
-            if (lim == 1 && threadIdx.x == 0) {  // a lone record (a launch of one): its unit order needs no sort
-                s_front[0] = 0;
-                s_ctl[2] = bkt == 0;
-            }
-        }
-        u32 nhuge = 0;
-        PROF_STAMP(ts2);
-        if (!whole) {
-            __syncthreads();
-#pragma unroll
-            for (u32 w = 0; w < SCAN_WAVES; ++w)
-                run_n = min(run_n, max(s_ctl[12 + w], 1u));
-            if (lim == 1)
-                nhuge = s_ctl[2];
-            // Unit order: [front units of very long records][all full units, record-major][the other front units by
-            // size, largest first]. Lockstep waves then draw units of equal or similar length, and the run ends on
-            // its shortest units. Counting sort of the front units by bucket: per-wave counts, then positions.
-            if (lim != 1) {  // (a lone record's order was set before the barrier above)
-                u32 rank = 0;
-                if (wave < SCAN_WAVES) {
-                    const bool in = threadIdx.x < run_n;
-#pragma unroll
-                    for (u32 b = 0; b <= CHUNK_STEPS; ++b) {
-                        const u64 m = __ballot(in && bkt == b);
-                        if (lane == 0)
-                            s_ctl[32 + BKT_STRIDE * wave + b] = (u32)__popcll(m);
-                        if (in && bkt == b)
-                            rank = (u32)__popcll(m & ((1ull << lane) - 1));
-                    }
-                }
-                __syncthreads();
-                PROF_STAMP(ts3);
-                if (threadIdx.x == 0)
-                    PROF_ADD(10, ts3 - ts2);
-                if (wave < SCAN_WAVES) {
-                    // lane b: first slot of this wave's bucket-b records = all records of earlier buckets (prefix over
-                    // lanes) + bucket b of earlier waves; a record then takes lane bkt's value (no serial walk)
-                    u32 tot = 0, mine = 0;
-#pragma unroll
-                    for (u32 w = 0; w < SCAN_WAVES; ++w) {
-                        const u32 c = lane < BKT_STRIDE ? s_ctl[32 + BKT_STRIDE * w + lane] : 0u;
-                        tot += c;
-                        mine += w < wave ? c : 0u;
-                    }
-                    const u32 before = wave_incl_sum(tot);
-                    const u32 first_slot = before - tot + mine;
-                    const u32 base = (u32)__shfl((int)first_slot, (int)bkt, 64);
-                    if (threadIdx.x < run_n)
-                        s_front[base + rank] = threadIdx.x;
-                }
-#pragma unroll
-                for (u32 w = 0; w < SCAN_WAVES; ++w)
-                    nhuge += s_ctl[32 + BKT_STRIDE * w];
-                __syncthreads();
-            }
-        }
+        lds_u32 *rs = (lds_u32 *)(lds + (rb ? CLDS_RUN1 : CLDS_RUN0));
+        lds_u32 *rs_next = (lds_u32 *)(lds + (rb ? CLDS_RUN0 : CLDS_RUN1));
+        lds_u32 *s_ubase = rs + RUN_UBASE_OFF, *s_done = rs + RUN_DONE_OFF, *s_front = rs + RUN_FRONT_OFF;
         // run-level values are workgroup-uniform: keep them in SGPRs (they live across the unit loop, where VGPRs are
         // the scarce resource)
-        run_n = __builtin_amdgcn_readfirstlane(run_n);
-        nhuge = __builtin_amdgcn_readfirstlane(nhuge);
-        const u32 total_units = __builtin_amdgcn_readfirstlane(whole ? run_n : s_ubase[run_n]);
+        const u32 key_idx = __builtin_amdgcn_readfirstlane(rs[RC_KEY]);
+        const u32 run_n = __builtin_amdgcn_readfirstlane(rs[RC_N]);
+        const bool whole = __builtin_amdgcn_readfirstlane(rs[RC_WHOLE]);
+        const u32 total_units = __builtin_amdgcn_readfirstlane(rs[RC_UNITS]);
+        const u32 nhuge = __builtin_amdgcn_readfirstlane(rs[RC_HUGE]);
         const u32 nfull = total_units - run_n;
         const u64 run_end = pos + run_n;
         PROF_STAMP(t1);
@@ -331,8 +337,11 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             if (OPEN)
                 for (u64 t = pos + threadIdx.x; t < run_end; t += blockDim.x)
                     args.ok[ok_at(t)] = 0;
+            if (wave == 0 && run_end < end)
+                scan_run<OPEN, FRAME>(args, recs, run_end, end, rs_next);
             __syncthreads();
             pos = run_end;
+            rb ^= 1;
             continue;
         }
         if (key_idx != loaded_key) {
@@ -357,7 +366,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         for (;;) {
             u32 ub = 0;
             if (lane == 0)
-                ub = atomicAdd((u32 *)&s_ctl[1], (u32)RPW);
+                ub = atomicAdd((u32 *)&rs[RC_NEXT], (u32)RPW);
             ub = __builtin_amdgcn_readfirstlane(ub);
             if (ub >= total_units)
                 break;
@@ -414,10 +423,10 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             if (live && unc > 1) {  // uniform over the group
                 u32 last = 0;
                 if (j == G - 1) {
-                    s_part[first + unc - 1 - k_back] = acc;  // stream order: the front unit first
-                    if (k_back == 0)
-                        s_ek0[ri] = ek0;
-                    __threadfence_block();  // partial and E(K, J0) land before the count that publishes them
+                    // stream order, the front unit first; the last unit (k_back 0, multiplier H^0 in the combine)
+                    // carries E(K, J0), so the combine ends on the tag
+                    s_part[first + unc - 1 - k_back] = k_back == 0 ? acc ^ ek0 : acc;
+                    __threadfence_block();  // the partial lands before the count that publishes it
                     last = atomicAdd((u32 *)&s_done[ri], 1u) == unc - 1;
                 }
                 last = dpp_bcast7(last, lane);
@@ -431,7 +440,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                             g = gmul_group(lds, g, tsel_chunk, j);
                         g ^= s_part[first + i];
                     }
-                    const u32x4 tag = g ^ s_ek0[ri];
+                    const u32x4 tag = g;
                     if (j != G - 1) {
                     } else if (OPEN) {
                         const u32x4 rt = *(const u32x4_u *)(args.in + r.in_off + frame_in_skip<OPEN, FRAME>() +
@@ -444,6 +453,13 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 }
             }
         }
+        // the run's units are all handed out: the first wave to get here scans the next run into the other buffer
+        // while the rest finish theirs
+        u32 claim = 0;
+        if (lane == 0)
+            claim = atomicAdd((u32 *)&rs[RC_CLAIM], 1u) == 0;
+        if (__builtin_amdgcn_readfirstlane(claim) && run_end < end)
+            scan_run<OPEN, FRAME>(args, recs, run_end, end, rs_next);
         PROF_STAMP(tw);
         __syncthreads();  // the run's tables, partials and counters are free again
         PROF_STAMP(t3);
@@ -456,14 +472,12 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             PROF_ADD(2, t3 - t2);
             PROF_ADD(5, total_units);
             PROF_ADD(6, 1);
-            PROF_ADD(8, ts1 - t0);
-            PROF_ADD(9, ts2 - ts1);
-            PROF_ADD(11, t1 - ts2);
             if (pos == beg)
                 PROF_ADD(3, t0 - tk);
         }
 #endif
         pos = run_end;
+        rb ^= 1;
     }
 }
 
