@@ -93,14 +93,14 @@ static int stage_reserve(ptls_mi355x_keyset_t *ks, size_t bytes)
         HIP_TRY(hipStreamCreateWithFlags(&ks->stream, hipStreamNonBlocking));
     if (ks->d_stage != NULL) {
         HIP_TRY(hipStreamSynchronize(ks->stream));
-        hipFree(ks->d_stage);
-        hipHostFree(ks->h_stage);
+        (void)hipFree(ks->d_stage);
+        (void)hipHostFree(ks->h_stage);
         ks->d_stage = ks->h_stage = NULL;
         ks->stage_cap = 0;
     }
     HIP_TRY(hipMalloc((void **)&ks->d_stage, cap));
     if (hipHostMalloc((void **)&ks->h_stage, cap, hipHostMallocDefault) != hipSuccess) {
-        hipFree(ks->d_stage);
+        (void)hipFree(ks->d_stage);
         ks->d_stage = NULL;
         return fail("%s", "stage: pinned host allocation failed");
     }
@@ -196,15 +196,15 @@ ptls_mi355x_keyset_t *ptls_mi355x_keyset_new(const void *keys, const void *ivs, 
     keyset_setup_kernel<<<(unsigned)((nkeys + 127) / 128), 128>>>(d_raw, d_raw + nkeys * key_size, ks->d_keys, (u32)nkeys, (u32)key_size);
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess)
         goto Fail;
-    hipMemset(d_raw, 0, nkeys * (key_size + 12));
-    hipFree(d_raw);
+    (void)hipMemset(d_raw, 0, nkeys * (key_size + 12));
+    (void)hipFree(d_raw);
     return ks;
 Fail:
     fail("%s", "ptls_mi355x_keyset_new: device setup failed");
     if (d_raw != NULL)
-        hipFree(d_raw);
+        (void)hipFree(d_raw);
     if (ks->d_keys != NULL)
-        hipFree(ks->d_keys);
+        (void)hipFree(ks->d_keys);
     free(ks);
     return NULL;
 }
@@ -235,9 +235,9 @@ int ptls_mi355x_keyset_update(ptls_mi355x_keyset_t *ks, const uint32_t *key_idx,
         if (hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess)
             ret = 0;
     }
-    hipMemset(d, 0, kb + ib);
-    hipDeviceSynchronize();
-    hipFree(d);
+    (void)hipMemset(d, 0, kb + ib);
+    (void)hipDeviceSynchronize();
+    (void)hipFree(d);
     if (ret != 0)
         fail("%s", "keyset_update: device setup failed");
     return ret;
@@ -247,23 +247,23 @@ void ptls_mi355x_keyset_free(ptls_mi355x_keyset_t *ks)
 {
     if (ks == NULL)
         return;
-    hipMemset(ks->d_keys, 0, ks->nkeys * sizeof(KeyEntry));
-    hipDeviceSynchronize();
-    hipFree(ks->d_keys);
+    (void)hipMemset(ks->d_keys, 0, ks->nkeys * sizeof(KeyEntry));
+    (void)hipDeviceSynchronize();
+    (void)hipFree(ks->d_keys);
     if (ks->d_stage != NULL) {
-        hipMemset(ks->d_stage, 0, ks->stage_cap);
+        (void)hipMemset(ks->d_stage, 0, ks->stage_cap);
         memset(ks->h_stage, 0, ks->stage_cap);  // staged plaintext and keystream-derived bytes
-        hipDeviceSynchronize();
-        hipFree(ks->d_stage);
-        hipHostFree(ks->h_stage);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(ks->d_stage);
+        (void)hipHostFree(ks->h_stage);
     }
     if (ks->stream != NULL)
-        hipStreamDestroy(ks->stream);
+        (void)hipStreamDestroy(ks->stream);
     if (ks->group_ev != NULL) {
-        hipEventSynchronize(ks->group_ev);
-        hipEventDestroy(ks->group_ev);
+        (void)hipEventSynchronize(ks->group_ev);
+        (void)hipEventDestroy(ks->group_ev);
     }
-    hipFree(ks->d_group);
+    (void)hipFree(ks->d_group);
     free(ks);
 }
 
@@ -349,7 +349,7 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
             HIP_TRY(hipEventCreateWithFlags(&ks->group_ev, hipEventDisableTiming));
         if (words > ks->group_cap) {
             HIP_TRY(hipEventSynchronize(ks->group_ev));
-            hipFree(ks->d_group);
+            (void)hipFree(ks->d_group);
             ks->d_group = NULL;
             ks->group_cap = 0;
             HIP_TRY(hipMalloc((void **)&ks->d_group, words * 4));

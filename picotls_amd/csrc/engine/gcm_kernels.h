@@ -26,7 +26,6 @@ __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u
                                               u32 iv1, u32 iv2, u64 rec, bool valid, u32 j, u32 laneoff, u32 tsel_horner,
                                               u32 tsel_last)
 {
-    constexpr int G = ENGINE_G;
     ptls_mi355x_record_t r = {};
     if (valid)
         r = args.recs[rec];

@@ -60,6 +60,7 @@ static void ctr_transform(ptls_cipher_context_t *_ctx, void *output, const void 
 
 static int aesctr_setup(ptls_cipher_context_t *_ctx, int is_enc, const void *key, size_t key_size)
 {
+    (void)is_enc; /* CTR is its own inverse */
     struct mi355x_ctr_context *ctx = (struct mi355x_ctr_context *)_ctx;
     static const uint8_t zero_iv[PTLS_AESGCM_IV_SIZE] = {0};
     if ((ctx->ks = ptls_mi355x_keyset_new(key, zero_iv, 1, key_size)) == NULL)
@@ -150,6 +151,7 @@ static size_t aead_do_decrypt(ptls_aead_context_t *_ctx, void *output, const voi
 
 static int aesgcm_setup(ptls_aead_context_t *_ctx, int is_enc, const void *key, const void *iv, size_t key_size)
 {
+    (void)is_enc; /* one context type serves both directions */
     struct mi355x_aead_context *ctx = (struct mi355x_aead_context *)_ctx;
 
     memcpy(ctx->static_iv, iv, sizeof(ctx->static_iv));
@@ -196,6 +198,7 @@ static void quiclb_dispose(ptls_cipher_context_t *_ctx)
 
 static void quiclb_init(ptls_cipher_context_t *ctx, const void *iv)
 {
+    (void)ctx, (void)iv;
     /* no-op, as picotls_quiclb_do_init (lib/quiclb-impl.h:102-105) */
 }
 
