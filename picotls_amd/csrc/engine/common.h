@@ -93,11 +93,12 @@ static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 #define UNIFORM_SLACK 2      // a run is uniform when its records' step counts differ by at most this
 #define WHOLE_MIN_RECS (ENGINE_WG / ENGINE_G)  // whole-record mode needs at least one record per 8-lane group
 // Per-run state, double-buffered so that one wave can scan run r+1 while the others finish run r (scan_run):
-// ctl[16] | ubase u32[CRUN_RECS + 16] (first unit of each record) | done u32[CRUN_RECS] (finished units per record) |
+// ctl[16] | the run's KeyEntry | ubase u32[CRUN_RECS + 16] (first unit of each record) | done u32[CRUN_RECS] (finished units per record) |
 // front u32[CRUN_RECS] (records by front-unit size). Then the unit partials (single: run r+1's units start after the
 // end-of-run barrier).
 #define RUN_CTL_WORDS 16
-#define RUN_UBASE_OFF RUN_CTL_WORDS
+#define RUN_KEY_OFF RUN_CTL_WORDS                                 // the run's KeyEntry (512 B), staged by the scanner
+#define RUN_UBASE_OFF (RUN_KEY_OFF + (int)(sizeof(KeyEntry) / 4))
 #define RUN_DONE_OFF (RUN_UBASE_OFF + CRUN_RECS + 16)
 #define RUN_FRONT_OFF (RUN_DONE_OFF + CRUN_RECS)
 #define RUN_WORDS (RUN_FRONT_OFF + CRUN_RECS)

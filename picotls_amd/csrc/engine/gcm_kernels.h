@@ -167,6 +167,9 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
     const u32 log2 = args.unit_log2, ustep = 1u << log2;
     const u32 lim = (u32)min(end - p, (u64)CRUN_RECS);
     const u32 key = args.multi_key ? recs[p].key_idx : 0u;
+    if (key < args.nkeys)  // the key entry (round keys, IV, H powers) moves to LDS now, off the next run's critical path
+        ((lds_u32 *)(rs + RUN_KEY_OFF))[lane] = ((const u32 *)(args.keys + key))[lane],
+        ((lds_u32 *)(rs + RUN_KEY_OFF))[lane + 64] = ((const u32 *)(args.keys + key))[lane + 64];
     u32 steps[Q], nc[Q], bkt[Q];
     u32 n = lim;  // ends at the first record of another key
 #pragma unroll
@@ -343,15 +346,16 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             rb ^= 1;
             continue;
         }
+        typedef __attribute__((address_space(3))) const KeyEntry lds_key_t;
+        lds_key_t *key = (lds_key_t *)(rs + RUN_KEY_OFF);  // staged by the scanner
         if (key_idx != loaded_key) {
-            build_ghash_tables(lds, args.keys + key_idx, 9, usrc);  // H^1..H^8 and the unit combine power
+            build_ghash_tables(lds, key, 9, usrc);  // H^1..H^8 and the unit combine power
             __syncthreads();
             loaded_key = key_idx;
             if (threadIdx.x == 0)
                 PROF_ADD(7, 1);
         }
         PROF_STAMP(t2);
-        const KeyEntry *key = args.keys + key_idx;
         u32 rk[NR + 1][4];
 #pragma unroll
         for (int r = 0; r <= NR; ++r)

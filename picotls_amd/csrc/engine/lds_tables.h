@@ -58,11 +58,12 @@ __device__ __forceinline__ void gf_mulxs_be(u32 &b0, u32 &b1, u32 &b2, u32 &b3, 
 // 16 entries. Entries are GF(2)-linear in n, so the XOR combinations are formed after the byte swap back to memory
 // order, and entry n ^ c = e(n) ^ e(c): at store n a lane writes slot n ^ (p mod 16), spreading a wave's 16-byte stores
 // over the bank groups. A few hundred VALU operations per thread: the build is a small part of a launch of one record.
-__device__ void build_ghash_tables(lds_u8 *lds, const KeyEntry *__restrict__ key, u32 ntables = ENGINE_G, u32 src8 = 8)
+template <typename KeyPtr>  // a KeyEntry in global memory, or its copy staged in LDS (the chunked kernel)
+__device__ void build_ghash_tables(lds_u8 *lds, KeyPtr key, u32 ntables = ENGINE_G, u32 src8 = 8)
 {
     for (u32 idx = threadIdx.x; idx < ntables * 32; idx += blockDim.x) {
         const u32 t = idx >> 5, p = idx & 31;
-        const u32 *h = key->h[t == 8 ? src8 : t];  // table 8: the unit combine power (chunked kernel)
+        const auto *h = key->h[t == 8 ? src8 : t];  // table 8: the unit combine power (chunked kernel)
         u32 b0 = bswap32(h[0]), b1 = bswap32(h[1]), b2 = bswap32(h[2]), b3 = bswap32(h[3]);
         for (u32 k = 0; k < (p >> 3); ++k)
             gf_mulxs_be(b0, b1, b2, b3, 32);
