@@ -89,7 +89,9 @@ static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 #ifndef CRUN_UNITS
 #define CRUN_UNITS 1024      // units per run
 #endif
+#ifndef WHOLE_RUN_RECS
 #define WHOLE_RUN_RECS 4096  // records per run when a one-key run is uniform (every record one unit)
+#endif
 #define UNIFORM_SLACK 2      // a run is uniform when its records' step counts differ by at most this
 #define WHOLE_MIN_RECS (ENGINE_WG / ENGINE_G)  // whole-record mode needs at least one record per 8-lane group
 // Per-run state, double-buffered so that one wave can scan run r+1 while the others finish run r (scan_run):
