@@ -156,8 +156,11 @@ __device__ __forceinline__ unsigned long long stamp()
 // a one-key batch) up to WHOLE_RUN_RECS whole records. Each lane takes records q * 64 + lane, q < CRUN_RECS / 64.
 // Outputs: ctl[RC_*], ubase[0..n] (prefix of unit counts), front[] (records ordered [very long][the others by
 // front-unit size, largest first]; the kernel numbers units [their front units][all full units][the other front
-// units]) and done[0..n) = 0. All lanes of the wave must be active.
-template <bool OPEN, int FRAME>
+// units]) and done[0..n) = 0. All lanes of the wave must be active. FIRST (a launch's first run, which the whole
+// workgroup waits for: the critical path of a launch of one record) stops the loops at the run's last 64-record block
+// and skips the sort for a lone record; the scans in the run tails keep the plain loops, whose registers the unit loop
+// shares (the guarded form adds VGPR spills to the open kernel).
+template <bool OPEN, int FRAME, bool FIRST = false>
 __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355x_record_t *__restrict__ recs, u64 p, u64 end,
                                       lds_u32 *rs)
 {
@@ -216,6 +219,8 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
         u32 carry = 0, cut = n;
 #pragma unroll
         for (u32 q = 0; q < Q; ++q) {
+            if (FIRST && q * 64 >= n)  // uniform: the rest of the lanes hold no record of this run
+                break;
             const u32 t = q * 64 + lane;
             const u32 incl = carry + wave_incl_sum(t < n ? nc[q] : 0u);
             if (t < n)
@@ -228,30 +233,43 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
         if (lane == 0)
             ubase[0] = 0;
         n = __builtin_amdgcn_readfirstlane(min(n, max(cut, 1u)));
-        // counting sort of the records by front-unit bucket: lane b counts bucket b, then an exclusive scan over lanes
-        u32 cnt = 0;
+        if (FIRST && n == 1) {  // a lone record (the per-record picotls path): no sort
+            nhuge = __builtin_amdgcn_readfirstlane(bkt[0]) == 0;
+            if (lane == 0)
+                front[0] = 0;
+        } else {
+            // counting sort of the records by front-unit bucket: lane b counts bucket b, then an exclusive scan over
+            // lanes
+            u32 cnt = 0;
 #pragma unroll
-        for (u32 q = 0; q < Q; ++q)
+            for (u32 q = 0; q < Q; ++q) {
+                if (FIRST && q * 64 >= n)
+                    break;
 #pragma unroll 1
-            for (u32 b = 0; b <= CHUNK_STEPS; ++b) {
-                const u32 c = (u32)__popcll(__ballot(q * 64 + lane < n && bkt[q] == b));
-                cnt += lane == b ? c : 0u;
+                for (u32 b = 0; b <= CHUNK_STEPS; ++b) {
+                    const u32 c = (u32)__popcll(__ballot(q * 64 + lane < n && bkt[q] == b));
+                    cnt += lane == b ? c : 0u;
+                }
             }
-        u32 next = wave_incl_sum(cnt) - cnt;  // lane b: next free slot of bucket b
-        nhuge = (u32)__builtin_amdgcn_readlane((int)cnt, 0);
+            u32 next = wave_incl_sum(cnt) - cnt;  // lane b: next free slot of bucket b
+            nhuge = (u32)__builtin_amdgcn_readlane((int)cnt, 0);
 #pragma unroll
-        for (u32 q = 0; q < Q; ++q)
+            for (u32 q = 0; q < Q; ++q) {
+                if (FIRST && q * 64 >= n)
+                    break;
 #pragma unroll 1
-            for (u32 b = 0; b <= CHUNK_STEPS; ++b) {
-                const bool in = q * 64 + lane < n && bkt[q] == b;
-                const u64 m = __ballot(in);
-                if (m == 0)
-                    continue;
-                if (in)
-                    front[(u32)__builtin_amdgcn_readlane((int)next, (int)b) + (u32)__popcll(m & ((1ull << lane) - 1))] =
-                        q * 64 + lane;
-                next += lane == b ? (u32)__popcll(m) : 0u;
+                for (u32 b = 0; b <= CHUNK_STEPS; ++b) {
+                    const bool in = q * 64 + lane < n && bkt[q] == b;
+                    const u64 m = __ballot(in);
+                    if (m == 0)
+                        continue;
+                    if (in)
+                        front[(u32)__builtin_amdgcn_readlane((int)next, (int)b) +
+                              (u32)__popcll(m & ((1ull << lane) - 1))] = q * 64 + lane;
+                    next += lane == b ? (u32)__popcll(m) : 0u;
+                }
             }
+        }
         units = (u32)__builtin_amdgcn_readfirstlane((int)ubase[n]);
     }
 #pragma unroll
@@ -313,9 +331,14 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     auto ok_at = [&](u64 i) -> u64 { return perm != nullptr ? (u64)perm[i] : i; };
 
     build_aes_tables(lds);
+    PROF_STAMP(ta);
     // the first run's state (later runs are scanned during the previous run's tail)
     if (wave == 0 && beg < end)
-        scan_run<OPEN, FRAME>(args, recs, beg, end, (lds_u32 *)(lds + CLDS_RUN0));
+        scan_run<OPEN, FRAME, true>(args, recs, beg, end, (lds_u32 *)(lds + CLDS_RUN0));
+#if ENGINE_PROFILE
+    if (threadIdx.x == 0)
+        PROF_ADD(8, ta - tk), PROF_ADD(9, stamp() - ta), PROF_ADD(10, 1);
+#endif
     __syncthreads();
 
     u32 rb = 0;  // run-state buffer of the current run

@@ -56,9 +56,9 @@ def main():
           f"units/run {p[5] / runs:.1f}, table builds/launch {p[7] / a.reps:.0f}")
     for i, name in enumerate(["run setup", "table build", "unit loop", "prologue"]):
         print(f"  {name:12s} {p[i] / runs:10.0f} cycles/run  {100 * p[i] / max(tot, 1):5.1f} %")
-    if any(p[8:12]):
-        print("  run setup split (cycles/run): scan+B1 %.0f | decide+prefix %.0f | buckets+B3 %.0f | B2..end %.0f" %
-              (p[8] / runs, p[9] / runs, p[10] / runs, p[11] / runs))
+    if p[10]:
+        print("  prologue split (cycles/workgroup, thread 0): tables (wave 1) %.0f | first run scan (wave 0) %.0f" %
+              (p[8] / p[10], p[9] / p[10]))
     waves = 16
     print(f"  wave idle at unit-loop barrier: {p[4] / runs / waves:.0f} cycles/run/wave "
           f"({100 * p[4] / waves / max(p[2], 1):.1f} % of the unit loop)")
