@@ -713,3 +713,51 @@ def test_ungrouped_many_key_batch_regrouped_on_device(ref, nkeys, frac_bad):
     order = np.argsort(key_idx, kind="stable")
     sealed2 = gpu_seal(ks, b.seal[order], pt, aad, b.sealed_bytes)
     assert np.array_equal(sealed2, sealed)
+
+
+# n = 1, 2, 33: one workgroup or a few; n = 256 * k: k records per workgroup on a 256-CU MI355X (one persistent
+# workgroup per CU once a batch has >= 32 records per CU)
+@pytest.mark.parametrize("n", [1, 2, 33, 256 * 63, 256 * 64, 256 * 65, 256 * 129, 256 * 256])
+def test_first_run_sizes(ref, n):
+    # a launch's first run is scanned by the guarded scan (scan_run<..., FIRST>): its loops stop at the run's last
+    # 64-record block and a lone record skips the front-unit sort; workgroup shares around those block edges, with
+    # mixed lengths so that runs are cut into units (not whole-record mode), one record longer than 1024 units
+    rng = np.random.default_rng(640 + n)
+    lens = rng.integers(0, 40000 if n < 64 else 3000, n)
+    lens[int(rng.integers(0, n))] = (3 << 20) + 5
+    b = RecordBatch.build(lens, rng.integers(0, 30, n), seqs=rng.integers(0, 2**48, n, dtype=np.uint64))
+    keys, ivs = np.frombuffer(rng.bytes(16), np.uint8), np.frombuffer(rng.bytes(12), np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(max(b.aad_bytes, 1)), np.uint8)
+    ks = pa.Keyset(keys, ivs, 16)
+    ks.set_schedule("chunked")
+    sealed = gpu_seal(ks, b.seal, pt, aad, b.sealed_bytes)
+    expect = np.zeros(b.sealed_bytes, np.uint8)
+    ref.run_batch(True, keys, ivs, 16, b.seal, pt, aad, expect, nthreads=8)
+    assert np.array_equal(sealed, expect)
+    victim = int(rng.integers(0, n))
+    bad = expect.copy()
+    bad[int(b.seal[victim]["out_off"]) + int(lens[victim])] ^= 0x01  # first tag byte
+    plain, ok = gpu_open(ks, b.open, bad, aad, b.pt_bytes)
+    want_ok = np.ones(n, np.uint8)
+    want_ok[victim] = 0
+    assert np.array_equal(ok, want_ok)
+    mask = record_mask(b.open, b.pt_bytes, field="out_off")
+    assert np.array_equal(plain[mask], pt[mask])
+    ks.free()
+
+
+def test_lone_huge_record_per_record_path(ref):
+    # the picotls vtable's batch of one with a record beyond 1024 units (the lone-record scan marks it huge)
+    rng = np.random.default_rng(650)
+    key, iv = rng.bytes(16), rng.bytes(12)
+    enc = pa.aead_new_direct(pa.aes128gcm, True, key, iv)
+    dec = pa.aead_new_direct(pa.aes128gcm, False, key, iv)
+    for ln in [(3 << 20) + 5, 1 << 24]:
+        pt, aad, seq = rng.bytes(ln), rng.bytes(13), int(rng.integers(0, 2**48))
+        want = ref.seal(key, iv, seq, aad, pt)
+        assert enc.encrypt(pt, seq, aad) == want, ln
+        assert dec.decrypt(want, seq, aad) == pt, ln
+        bad = bytearray(want)
+        bad[ln // 2] ^= 0x10
+        assert dec.decrypt(bytes(bad), seq, aad) is None, ln
