@@ -237,8 +237,9 @@ int ptls_mi355x_quiclb_transform(ptls_mi355x_keyset_t *ks, size_t key_idx, void 
                                  int encrypt);
 
 /**
- * Synchronous single-record helpers on HOST buffers (a batch of one, with H2D/D2H copies). These back the picotls
- * vtable (do_encrypt / do_decrypt) and mirror ptls_aead_encrypt / ptls_aead_decrypt: encrypt writes len+16 bytes;
+ * Synchronous single-record helpers on HOST buffers (a batch of one through the keyset's pinned staging buffer, which
+ * the kernel reads and writes in place over PCIe; not thread-safe per keyset, like a picotls AEAD context). These back
+ * the picotls vtable (do_encrypt / do_decrypt) and mirror ptls_aead_encrypt / ptls_aead_decrypt: encrypt writes len+16 bytes;
  * decrypt takes inlen = len+16 and returns the plaintext length or SIZE_MAX (tag mismatch or inlen < 16).
  */
 int ptls_mi355x_encrypt(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const void *input, size_t inlen, uint64_t seq,
