@@ -761,3 +761,42 @@ def test_lone_huge_record_per_record_path(ref):
         bad = bytearray(want)
         bad[ln // 2] ^= 0x10
         assert dec.decrypt(bytes(bad), seq, aad) is None, ln
+
+
+def test_batch_on_pinned_host_arenas(ref):
+    # the batch calls take pinned (device-mapped) host memory for every arena, descriptors and ok bytes included: the
+    # kernels read and write it over PCIe (bench.py --e2e "in_place"); bit-exact vs fusion, one tampered record
+    rng = np.random.default_rng(660)
+    n = 3000
+    lens = rng.integers(0, 20000, n)
+    b = RecordBatch.build(lens, rng.integers(0, 30, n), seqs=rng.integers(0, 2**48, n, dtype=np.uint64))
+    keys, ivs = np.frombuffer(rng.bytes(32), np.uint8), np.frombuffer(rng.bytes(12), np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(max(b.aad_bytes, 1)), np.uint8)
+
+    def pinned(a):
+        return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).pin_memory()
+
+    h_seal, h_open, h_pt, h_aad = pinned(b.seal), pinned(b.open), pinned(pt), pinned(aad)
+    h_sealed = torch.zeros(b.sealed_bytes, dtype=torch.uint8).pin_memory()
+    ks = pa.Keyset(keys, ivs, 32)
+    s = torch.cuda.current_stream().cuda_stream
+    pa.seal_batch(ks, h_seal.data_ptr(), n, h_pt.data_ptr(), h_aad.data_ptr(), h_sealed.data_ptr(), s)
+    torch.cuda.synchronize()
+    expect = np.zeros(b.sealed_bytes, np.uint8)
+    ref.run_batch(True, keys, ivs, 32, b.seal, pt, aad, expect, nthreads=8)
+    assert np.array_equal(h_sealed.numpy(), expect)
+    victim = 1234
+    h_sealed[int(b.seal[victim]["out_off"]) + 7] ^= 0x20
+    h_back = torch.zeros(b.pt_bytes, dtype=torch.uint8).pin_memory()
+    h_ok = torch.full((n,), 0xAA, dtype=torch.uint8).pin_memory()
+    pa.open_batch(ks, h_open.data_ptr(), n, h_sealed.data_ptr(), h_aad.data_ptr(), h_back.data_ptr(), h_ok.data_ptr(), s)
+    torch.cuda.synchronize()
+    want_ok = np.ones(n, np.uint8)
+    want_ok[victim] = 0
+    assert np.array_equal(h_ok.numpy(), want_ok)
+    want = pt.copy()
+    want[int(b.seal[victim]["in_off"]) + 7] ^= 0x20  # CTR: the flipped ciphertext bit flips the plaintext bit
+    mask = record_mask(b.open, b.pt_bytes, field="out_off")
+    assert np.array_equal(h_back.numpy()[mask], want[mask])
+    ks.free()
