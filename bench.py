@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """AES-GCM seal+open throughput of the MI355X record engine (BASELINE.json metric), device-resident.
 
-    python bench.py [--gpus N --steps K --warmup W] [--workload tls16k] [--extra quic1200] [--no-cpu-baseline]
+    python bench.py [--gpus N --steps K --warmup W] [--workload tls16k] [--extra quic1200,mixed,mixedrand,ptlsbench]
+                    [--no-cpu-baseline]
 
 One step = seal the whole batch, then open the sealed batch again (one launch each), inputs already in HBM.
 value = (sum L sealed + sum L opened) over all ranks / max-over-ranks wall time of the K timed steps, in GiB/s
@@ -12,8 +13,13 @@ Also reported:
   roofline      dominant kernel (seal), algorithmic bytes per launch / average launch time (HIP events on the
                 launch stream) against the 8 TB/s HBM peak of MI355X; traffic (PMC) from profiles/ when committed
   cpu_baseline  picotls' own lib/fusion.c (oracle/_ref, compiled from the reference) sealing+opening a bounded sample
-                of the same workload on this host's cores (rank 0, N=1 only)
-  extra         the 1200-byte QUIC configuration (configs[2]) at full size
+                of each workload on this host's cores (rank 0, N=1 only): ptls_fusion_aes{128,256}gcm (the ptlsbench
+                path, primary) and ptls_non_temporal_aes128gcm (the TLS path, secondary), median of reps with the
+                spread; t/ptlsbench.c's own loop for configs[0]. The same leg checks records sampled from every GPU leg
+                bit for bit against fusion (verified.fusion_spot_check).
+  extra         the other BASELINE configs at full size: quic1200 (configs[2]), mixed / mixedrand (configs[3], keys
+                grouped by connection / in random order as SURVEY §8(d) writes it), ptlsbench (configs[0]: 1000-record
+                batches under t/ptlsbench.c's conventions, on the GPU; fusion beside it in cpu_baseline)
 """
 from __future__ import annotations
 
@@ -38,10 +44,11 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="tls16k")
-    p.add_argument("--extra", default="quic1200", help="comma list of extra workloads to report ('' for none)")
+    p.add_argument("--extra", default="quic1200,mixed,mixedrand,ptlsbench",
+                   help="comma list of extra workloads to report ('' for none)")
     p.add_argument("--records", type=int, default=0, help="override record count (smaller runs)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget of the cpu_baseline leg")
+    p.add_argument("--cpu-seconds", type=float, default=3.0, help="wall budget of each cpu_baseline leg")
     p.add_argument("--e2e", action="store_true", help="also time pinned-host -> H2D -> seal -> D2H (DESIGN.md)")
     p.add_argument("--schedule", default="auto", choices=["auto", "lockstep", "chunked"],
                    help="batch schedule (ptls_mi355x_keyset_set_schedule)")
@@ -137,7 +144,8 @@ def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool
         ok_all = bool(d_ok.min().item() == 1) if b.n else True
         same = bool(torch.equal(d_back, d_pt))
         res["verified_roundtrip"] = ok_all and same
-        res["fusion_spot_check"] = spot_check(wl, b, keys, ivs, d_pt, d_aad, d_sealed, begin) if R.rank == 0 else None
+        # records for the bit-exact fusion check, which runs in the cpu_baseline leg (rank 0)
+        res["sample"] = collect_sample(wl, b, keys, ivs, d_pt, d_aad, d_sealed) if R.rank == 0 else None
     del d_pt, d_sealed, d_back, d_ok, d_seal, d_open, d_aad
     ks.free()
     torch.cuda.empty_cache()
@@ -159,24 +167,20 @@ def zero_slot_padding(arena, recs, dev):
         arena[sel] = 0
 
 
-def spot_check(wl, b, keys, ivs, d_pt, d_aad, d_sealed, begin, nsample: int = 64):
-    """Compares nsample records sealed on the GPU with lib/fusion.c on the same inputs (bit-exact)."""
-    try:
-        from oracle import FusionRef
-
-        ref = FusionRef()
-    except Exception as e:  # the checker is optional for the timing, never for the tests
-        return f"skipped: {e}"
+def collect_sample(wl, b, keys, ivs, d_pt, d_aad, d_sealed, nsample: int = 64):
+    """Host copies of nsample records (inputs and the GPU's sealed output), repacked as a small batch, for the
+    bit-exact comparison with lib/fusion.c in the cpu_baseline leg."""
     rng = np.random.default_rng(99)
     idx = np.unique(np.concatenate([[0, b.n - 1], rng.integers(0, b.n, nsample)]))
     sub = b.seal[idx].copy()
-    pt_parts, aad_parts, new_in, new_aad = [], [], [], []
+    pt_parts, aad_parts, gpu_parts, new_in, new_aad = [], [], [], [], []
     off = aoff = 0
     for r in sub:
         ln, al = int(r["len"]), int(r["aad_len"])
         pt_parts.append(d_pt[int(r["in_off"]):int(r["in_off"]) + ln].cpu().numpy())
         pt_parts.append(np.zeros(16, np.uint8))  # room for the tag (sealed in place)
         aad_parts.append(d_aad[int(r["aad_off"]):int(r["aad_off"]) + al].cpu().numpy())
+        gpu_parts.append(d_sealed[int(r["out_off"]):int(r["out_off"]) + ln + 16].cpu().numpy())
         new_in.append(off)
         new_aad.append(aoff)
         off += ln + 16
@@ -185,28 +189,81 @@ def spot_check(wl, b, keys, ivs, d_pt, d_aad, d_sealed, begin, nsample: int = 64
     recs["in_off"] = new_in
     recs["out_off"] = new_in
     recs["aad_off"] = new_aad
-    pt = np.concatenate(pt_parts + [np.zeros(1, np.uint8)])
-    aad = np.concatenate(aad_parts + [np.zeros(1, np.uint8)])
-    out = np.zeros(len(pt), np.uint8)
-    ref.run_batch(True, keys, ivs, wl.key_size, recs, pt, aad, out, nthreads=1)
-    for r, o in zip(sub, new_in):
-        ln = int(r["len"])
-        gpu = d_sealed[int(r["out_off"]):int(r["out_off"]) + ln + 16].cpu().numpy()
-        if not np.array_equal(gpu, out[o:o + ln + 16]):
-            return False
-    return True
+    return {"key_size": wl.key_size, "keys": keys, "ivs": ivs, "recs": recs,
+            "pt": np.concatenate(pt_parts + [np.zeros(1, np.uint8)]),
+            "aad": np.concatenate(aad_parts + [np.zeros(1, np.uint8)]), "gpu": np.concatenate(gpu_parts)}
 
 
-def cpu_baseline(wl, seconds: float):
-    """lib/fusion.c (the reference, compiled from /root/reference into oracle/_ref) on this host's cores."""
-    try:
-        from oracle import FusionRef
+def check_sample(ref, sample) -> bool:
+    """lib/fusion.c (ptls_aead_encrypt per record) on the sampled inputs, compared with the GPU's sealed records."""
+    out = np.zeros(len(sample["pt"]), np.uint8)
+    ref.run_batch(True, sample["keys"], sample["ivs"], sample["key_size"], sample["recs"], sample["pt"], sample["aad"], out,
+                  nthreads=1)
+    fus = np.concatenate([out[int(r["out_off"]):int(r["out_off"]) + int(r["len"]) + 16] for r in sample["recs"]])
+    return bool(np.array_equal(fus, sample["gpu"]))
 
-        ref = FusionRef()
-    except Exception as e:
-        return {"value": None, "unit": "GiB/s", "cores": 0, "kind": "reference", "sample": f"unavailable: {e}"}
+
+def run_ptlsbench(R, steps: int, warmup: int, rec_len: int = 16384):
+    """configs[0] on the GPU: ptlsbench's 1000-record batch (picotls_amd.workloads.ptlsbench_batch: HKDF key from
+    32 x 'z', AAD h[4] with h[0] = seq, zero plaintext) sealed and opened as one launch each, repeatedly. The
+    launch-bound small-batch shape of picotls' own benchmark; fusion runs the same records in cpu_baseline."""
+    import torch
+    import picotls_amd as pa
+    from picotls_amd.workloads import ptlsbench_batch
+
+    b, key, iv, aad = ptlsbench_batch(rec_len=rec_len)
+    ks = pa.Keyset(key, iv, 16)
+    dev = R.device
+    d_seal = torch.from_numpy(b.seal.view(np.uint8).copy()).to(dev)
+    d_open = torch.from_numpy(b.open.view(np.uint8).copy()).to(dev)
+    d_aad = torch.from_numpy(aad).to(dev)
+    d_pt = torch.zeros(b.pt_bytes, dtype=torch.uint8, device=dev)
+    d_sealed = torch.empty(b.sealed_bytes, dtype=torch.uint8, device=dev)
+    d_back = torch.ones(b.pt_bytes, dtype=torch.uint8, device=dev)
+    d_ok = torch.zeros(b.n, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    reps = max(steps, 1) * 20  # a batch is 16 MiB: 20 batches per step
+
+    def step():
+        pa.seal_batch(ks, d_seal.data_ptr(), b.n, d_pt.data_ptr(), d_aad.data_ptr(), d_sealed.data_ptr(), sp)
+        pa.open_batch(ks, d_open.data_ptr(), b.n, d_sealed.data_ptr(), d_aad.data_ptr(), d_back.data_ptr(),
+                      d_ok.data_ptr(), sp)
+
+    for _ in range(max(warmup, 1) * 20):
+        step()
+    torch.cuda.synchronize(dev)
+    R.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize(dev)
+    R.barrier()
+    wall = time.perf_counter() - t0
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    seal_ms = open_ms = 0.0
+    for _ in range(10):
+        e[0].record(stream)
+        pa.seal_batch(ks, d_seal.data_ptr(), b.n, d_pt.data_ptr(), d_aad.data_ptr(), d_sealed.data_ptr(), sp)
+        e[1].record(stream)
+        pa.open_batch(ks, d_open.data_ptr(), b.n, d_sealed.data_ptr(), d_aad.data_ptr(), d_back.data_ptr(), d_ok.data_ptr(), sp)
+        e[2].record(stream)
+        torch.cuda.synchronize(dev)
+        seal_ms += e[0].elapsed_time(e[1]) / 10
+        open_ms += e[1].elapsed_time(e[2]) / 10
+    res = {"records_per_batch": b.n, "record_len": rec_len, "batches": reps, "payload_bytes": b.payload_bytes,
+           "wall_s": wall, "seal_ms_per_batch": round(seal_ms, 4), "open_ms_per_batch": round(open_ms, 4),
+           "verified_roundtrip": bool(d_ok.min().item() == 1) and not bool(d_back.any().item())}
+    # every sealed record of the batch goes to the bit-exact check against fusion's ptlsbench run (cpu_baseline)
+    res["gpu_sealed"] = d_sealed.cpu().numpy() if R.rank == 0 else None
+    ks.free()
+    return res
+
+
+def _cpu_share():
+    """The cores this process may use (the box grants a CPU share smaller than the visible CPU set; OMP_NUM_THREADS /
+    nproc report it)."""
     cpus = sorted(os.sched_getaffinity(0))
-    # the box grants a CPU share smaller than the visible CPU set (OMP_NUM_THREADS / nproc report it)
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(cpus)
     try:
         import subprocess
@@ -214,42 +271,82 @@ def cpu_baseline(wl, seconds: float):
         share = min(share, int(subprocess.run(["nproc"], capture_output=True, text=True).stdout.strip() or share))
     except Exception:
         pass
-    cpus = cpus[:max(1, min(share, len(cpus)))]
-    nthreads = len(cpus)
-    n = min(wl.nrecs, max(1, (256 << 20) // (wl.rec_len or 8192)))  # ~256 MiB sample of the same workload
-    b = wl.descriptors(0, n)
-    keys, ivs = wl.keys()
+    return cpus[:max(1, min(share, len(cpus)))]
+
+
+def _fusion_leg(ref, wl, cpus, seconds: float, nontemporal: bool = False, sample_bytes: int = 256 << 20):
+    """fusion sealing then opening a bounded sample of the workload with len(cpus) pinned threads (contiguous shards,
+    CLOCK_MONOTONIC between a start barrier and the last thread's end), repeated for `seconds`: median and spread of
+    the per-rep seal+open rate."""
     from picotls_amd.workloads import payload_np
 
+    n = min(wl.nrecs, max(1, sample_bytes // (wl.rec_len or 8192)))
+    b = wl.descriptors(0, n)
+    keys, ivs = wl.keys()
     pt = payload_np(wl.seed, 0, b.pt_bytes).copy()
     aad = wl.aad_arena(b, 0)
     sealed = np.zeros(b.sealed_bytes, np.uint8)
     back = np.zeros(b.pt_bytes, np.uint8)
     ok = np.zeros(b.n, np.uint8)
-    t_seal = t_open = 0.0
-    reps = 0
+    rates, srates, orates = [], [], []
     start = time.perf_counter()
-    while True:
-        ts, _ = ref.run_batch(True, keys, ivs, wl.key_size, b.seal, pt, aad, sealed, nthreads=nthreads, cpus=cpus)
-        to, fails = ref.run_batch(False, keys, ivs, wl.key_size, b.open, sealed, aad, back, ok=ok, nthreads=nthreads, cpus=cpus)
+    while len(rates) < 3 or (time.perf_counter() - start < seconds and len(rates) < 50):
+        ts, _ = ref.run_batch(True, keys, ivs, wl.key_size, b.seal, pt, aad, sealed, nthreads=len(cpus), cpus=cpus,
+                              nontemporal=nontemporal)
+        to, fails = ref.run_batch(False, keys, ivs, wl.key_size, b.open, sealed, aad, back, ok=ok, nthreads=len(cpus),
+                                  cpus=cpus, nontemporal=nontemporal)
         assert fails == 0
-        t_seal += ts
-        t_open += to
-        reps += 1
-        if time.perf_counter() - start > seconds or reps >= 50:
-            break
-    gib = 2 * b.payload_bytes * reps / 2**30
-    # one core (1 thread and all cores), on a 1/8 slice of the same sample for ~3 s
-    n1 = max(1, b.n // 8)
-    b1 = wl.descriptors(0, n1)
-    t1, reps1, start1 = 0.0, 0, time.perf_counter()
-    while reps1 < 50 and (reps1 == 0 or time.perf_counter() - start1 < 3.0):
-        ts, _ = ref.run_batch(True, keys, ivs, wl.key_size, b1.seal, pt, aad, sealed, nthreads=1, cpus=cpus[:1])
-        to, fails = ref.run_batch(False, keys, ivs, wl.key_size, b1.open, sealed, aad, back, ok=ok, nthreads=1,
-                                  cpus=cpus[:1])
-        assert fails == 0
-        t1 += ts + to
-        reps1 += 1
+        gib = b.payload_bytes / 2**30
+        rates.append(2 * gib / (ts + to))
+        srates.append(gib / ts)
+        orates.append(gib / to)
+    algo = ("ptls_non_temporal_aes" if nontemporal else "ptls_fusion_aes") + f"{8 * wl.key_size}gcm"
+    return {"value": round(float(np.median(rates)), 3), "min": round(min(rates), 3), "max": round(max(rates), 3),
+            "reps": len(rates), "seal_GiBps": round(float(np.median(srates)), 3),
+            "open_GiBps": round(float(np.median(orates)), 3), "threads": len(cpus),
+            "sample": f"{b.n} x {wl.rec_len or 'U[64,16384]'} B records of '{wl.name}' ({b.payload_bytes / 2**20:.0f} MiB), "
+                      f"{algo} via ptls_aead_encrypt/decrypt"}
+
+
+def cpu_baseline(wl, seconds: float, samples: dict, ptlsbench_gpu):
+    """lib/fusion.c (the reference, compiled from /root/reference into oracle/_ref) on this host's cores, and the
+    bit-exact checks of the GPU legs' sampled records against it."""
+    try:
+        from oracle import FusionRef, PtlsBenchRef
+
+        ref = FusionRef()
+    except Exception as e:
+        return {"value": None, "unit": "GiB/s", "cores": 0, "kind": "reference", "sample": f"unavailable: {e}"}, {}
+    from picotls_amd.workloads import WORKLOADS
+
+    checks = {name: check_sample(ref, smp) for name, smp in samples.items() if smp is not None}
+    cpus = _cpu_share()
+    legs = {}
+    primary = _fusion_leg(ref, wl, cpus, seconds)
+    legs[wl.name] = {"fusion": primary}
+    if wl.name == "tls16k":  # the TLS path (SURVEY §8(d) secondary baseline)
+        legs[wl.name]["non_temporal"] = _fusion_leg(ref, wl, cpus, seconds, nontemporal=True)
+    legs[wl.name]["fusion_1_thread"] = _fusion_leg(ref, wl, cpus[:1], seconds, sample_bytes=64 << 20)
+    for name in ("quic1200", "mixed"):
+        if name != wl.name:
+            legs[name] = {"fusion": _fusion_leg(ref, WORKLOADS[name], cpus, seconds)}
+    # configs[0]: t/ptlsbench.c's own loop (one thread, its CPU clock), 20 batches of 1000 x 16384 B
+    try:
+        pb = PtlsBenchRef()
+        first = np.zeros(pb.BATCH * (16384 + 16), np.uint8)
+        t = pb.run(20 * pb.BATCH, 16384, 16, first)
+        gib = 20 * pb.BATCH * 16384 / 2**30
+        legs["ptlsbench"] = {"fusion": {
+            "value": round(2 * gib / (t["seal_cpu_s"] + t["open_cpu_s"]), 3), "seal_GiBps": round(gib / t["seal_cpu_s"], 3),
+            "open_GiBps": round(gib / t["open_cpu_s"], 3),
+            "seal_mbps": round(gib * 2**30 * 8 / (t["seal_cpu_s"] * 1e6), 1),
+            "open_mbps": round(gib * 2**30 * 8 / (t["open_cpu_s"] * 1e6), 1), "threads": 1,
+            "sample": "t/ptlsbench.c bench_run_one: 20 batches of 1000 x 16384 B, ptls_aead_new(ptls_fusion_aes128gcm, "
+                      "sha256, 32 x 'z'), AAD h[4], zero plaintext; CPU time of the thread (ptlsbench's clock)"}}
+        if ptlsbench_gpu is not None:
+            checks["ptlsbench"] = bool(np.array_equal(ptlsbench_gpu, first))
+    except Exception as e:
+        legs["ptlsbench"] = {"fusion": {"value": None, "sample": f"unavailable: {e}"}}
     model = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -258,13 +355,12 @@ def cpu_baseline(wl, seconds: float):
                 break
     except OSError:
         pass
-    return {"value": round(gib / (t_seal + t_open), 3), "unit": "GiB/s", "cores": nthreads, "kind": "reference",
-            "sample": f"{b.n} x {wl.rec_len or 'mixed'} B records of '{wl.name}' ({b.payload_bytes / 2**20:.0f} MiB), "
-                      f"seal+open x{reps}, ptls_fusion_aes{8 * wl.key_size}gcm via ptls_aead_encrypt/decrypt, "
-                      f"{nthreads} pinned threads, CLOCK_MONOTONIC; CPU: {model}",
-            "seal_GiBps": round(b.payload_bytes * reps / 2**30 / t_seal, 3),
-            "open_GiBps": round(b.payload_bytes * reps / 2**30 / t_open, 3),
-            "single_thread_GiBps": round(2 * b1.payload_bytes * reps1 / 2**30 / t1, 3)}
+    out = {"value": primary["value"], "unit": "GiB/s", "cores": len(cpus), "kind": "reference",
+           "sample": primary["sample"] + f", {len(cpus)} pinned threads, CLOCK_MONOTONIC, median of {primary['reps']} reps "
+                                         f"(min {primary['min']}, max {primary['max']}); CPU: {model}",
+           "seal_GiBps": primary["seal_GiBps"], "open_GiBps": primary["open_GiBps"],
+           "single_thread_GiBps": legs[wl.name]["fusion_1_thread"]["value"], "legs": legs}
+    return out, checks
 
 
 def run_e2e(R, wl, nchunks: int = 16, reps: int = 3, schedule: str = "auto"):
@@ -447,32 +543,51 @@ def main():
                      "alg_bytes_per_launch": res["seal_alg_bytes"], "avg_launch_ms": round(res["seal_ms"], 4),
                      "open_achieved": round(res["open_alg_bytes"] / open_s / 1e9, 2)},
         "lds_model": lds_model(res, wl.key_size),
-        "verified": {"roundtrip": res.get("verified_roundtrip"), "fusion_spot_check": res.get("fusion_spot_check")},
+        "verified": {"roundtrip": res.get("verified_roundtrip"), "fusion_spot_check": None},
     }
+    samples = {wl.name: res.get("sample")}
     extra = {}
+    ptlsbench_gpu = None
     for name in [x for x in args.extra.split(",") if x]:
         if name == args.workload:
+            continue
+        if name == "ptlsbench":
+            r2 = run_ptlsbench(R, args.steps, args.warmup)
+            v2, _ = aggregate_throughput(R, r2["payload_bytes"], r2["wall_s"], r2["batches"])
+            ptlsbench_gpu = r2.pop("gpu_sealed")
+            extra[name] = {"value": round(v2, 3), "unit": "GiB/s", "config": "configs[0]: t/ptlsbench.c conventions "
+                           "(HKDF key from 32 x 'z', AAD h[4] with h[0] = seq, zero plaintext), 1000 x 16384 B per launch, "
+                           "AES-128-GCM", **{k: r2[k] for k in ("records_per_batch", "batches", "seal_ms_per_batch",
+                                                                 "open_ms_per_batch")},
+                           "seal_GiBps": round(r2["records_per_batch"] * 16384 / (r2["seal_ms_per_batch"] / 1e3) / 2**30, 3),
+                           "open_GiBps": round(r2["records_per_batch"] * 16384 / (r2["open_ms_per_batch"] / 1e3) / 2**30, 3),
+                           "verified": {"roundtrip": r2["verified_roundtrip"], "fusion_spot_check": None}}
             continue
         w2 = WORKLOADS[name]
         if args.records:
             w2 = w2.scaled(max(1, args.records * (wl.rec_len or 8192) // (w2.rec_len or 8192)))
         r2 = run_workload(R, w2, args.steps, args.warmup, args.verify, name == "shard1200", args.schedule)
+        samples[name] = r2.get("sample")
         v2, _ = aggregate_throughput(R, r2["payload_bytes"], r2["wall_s"], args.steps)
-        extra[name] = {"value": round(v2, 3), "unit": "GiB/s",
-                       "records_per_gpu": r2["records"], "record_len": w2.rec_len,
+        extra[name] = {"value": round(v2, 3), "unit": "GiB/s", "desc": w2.desc,
+                       "records_per_gpu": r2["records"], "record_len": w2.rec_len or "U[64,16384]",
+                       "aead": f"AES-{8 * w2.key_size}-GCM", "keys": w2.nkeys, "key_order": w2.key_order,
                        "seal_GiBps": round(r2["payload_bytes"] / (r2["seal_ms"] / 1e3) / 2**30, 3),
                        "open_GiBps": round(r2["payload_bytes"] / (r2["open_ms"] / 1e3) / 2**30, 3),
                        "seal_achieved_GBps": round(r2["seal_alg_bytes"] / (r2["seal_ms"] / 1e3) / 1e9, 2),
                        "seal_hbm_frac": round(r2["seal_alg_bytes"] / (r2["seal_ms"] / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
-                       "verified": {"roundtrip": r2.get("verified_roundtrip"),
-                                    "fusion_spot_check": r2.get("fusion_spot_check")}}
+                       "seal_avg_launch_ms": round(r2["seal_ms"], 4),
+                       "verified": {"roundtrip": r2.get("verified_roundtrip"), "fusion_spot_check": None}}
     if extra:
         out["extra"] = extra
     if args.e2e:
         out["e2e_host_buffers"] = run_e2e(R, WORKLOADS[args.workload].scaled(min(wl.nrecs, max(1, (4 << 30) // (wl.rec_len or 8192)))),
                                           schedule=args.schedule)
     if R.rank == 0 and R.world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds)
+        out["cpu_baseline"], checks = cpu_baseline(wl, args.cpu_seconds, samples if args.verify else {}, ptlsbench_gpu)
+        out["verified"]["fusion_spot_check"] = checks.get(wl.name)
+        for name, e in extra.items():
+            e["verified"]["fusion_spot_check"] = checks.get(name)
     elif R.rank == 0:
         out["cpu_baseline"] = None
     if R.rank == 0:

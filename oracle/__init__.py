@@ -198,6 +198,41 @@ class FusionRef:
         return t, fails.value
 
 
+class PtlsBenchRef:
+    """ctypes front-end of oracle/ptlsbench_harness.c (in oracle/_ref/libtls12_ref.so): t/ptlsbench.c's benchmark loop
+    over fusion with its own conventions (BASELINE.json configs[0])."""
+
+    BATCH = 1000  # BENCH_BATCH, t/ptlsbench.c:86
+    SECRET = b"z" * 64  # memset(secret, 'z', sizeof(secret)), t/ptlsbench.c:223
+
+    def __init__(self):
+        path = os.path.join(REF_DIR, "libtls12_ref.so")
+        if not os.path.exists(path):
+            build()
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: build it with `make -C oracle` where /root/reference exists")
+        lib = ctypes.CDLL(path)
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        lib.ref_ptlsbench_keys.argtypes = [sz, vp, vp, vp]
+        lib.ref_ptlsbench.argtypes = [sz, sz, sz, vp, vp]
+        self.lib = lib
+
+    def keys(self, key_size: int = 16) -> tuple[bytes, bytes]:
+        """(key, IV) of ptls_aead_new(aead, hash, is_enc, 32 x 'z', NULL) (get_traffic_keys, lib/picotls.c:1634)."""
+        key, iv = bytearray(key_size), bytearray(12)
+        if self.lib.ref_ptlsbench_keys(key_size, _ptr(self.SECRET), _ptr(key), _ptr(iv)) != 0:
+            raise RuntimeError("ptls_hkdf_expand_label failed")
+        return bytes(key), bytes(iv)
+
+    def run(self, n: int, l: int, key_size: int = 16, first_batch: np.ndarray | None = None) -> dict:
+        """bench_run_one over n records of l bytes; first_batch (uint8, >= min(n, 1000) * (l + 16) bytes) receives the
+        first batch's sealed records. Returns CPU (ptlsbench's clock) and wall seconds per direction."""
+        times = np.zeros(4, np.float64)
+        if self.lib.ref_ptlsbench(key_size, l, n, _ptr(first_batch), _ptr(times)) != 0:
+            raise RuntimeError("ptlsbench: a record failed to open")
+        return {"seal_cpu_s": times[0] * 1e-6, "open_cpu_s": times[1] * 1e-6, "seal_wall_s": times[2], "open_wall_s": times[3]}
+
+
 class Tls12Ref:
     """ctypes front-end of picotls' own record layer (oracle/_ref/libtls12_ref.so, oracle/tls12_harness.c): TLS 1.2 over
     fusion's non-temporal AEADs (ptls_import of ptls_build_tls12_export_params) and TLS 1.3 over the same objects

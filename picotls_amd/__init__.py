@@ -6,7 +6,7 @@ ctypes so that Python tests and ``bench.py`` drive exactly the code a C caller w
 operator interface (``include/picotls.h:519-580, 2082-2164``; ``lib/picotls.c:6547-6601``):
 
 * :data:`aes128gcm` / :data:`aes256gcm` -- algorithm descriptors (``ptls_mi355x_aes{128,256}gcm``)
-* :func:`aead_new_direct` -> :class:`AeadContext` with ``encrypt`` / ``encrypt_s`` / ``decrypt`` / ``get_iv`` /
+* :func:`aead_new_direct` / :func:`aead_new` (traffic secret -> key, IV) -> :class:`AeadContext` with ``encrypt`` / ``encrypt_s`` / ``decrypt`` / ``get_iv`` /
   ``set_iv`` / ``xor_iv`` (``decrypt`` returns ``None`` where picotls returns ``SIZE_MAX``)
 * :class:`Keyset`, :func:`seal_batch`, :func:`open_batch`, :func:`ecb_batch`, :func:`hp_mask_batch`,
   :func:`seal_batch_hp`, :func:`quiclb_batch` -- the batch extension.
@@ -368,4 +368,13 @@ class QuicLbCipher:
 
 
 def aead_new_direct(algo: AeadAlgorithm, is_enc: bool, key: bytes, iv: bytes) -> AeadContext:
+    return AeadContext(algo, is_enc, key, iv)
+
+
+def aead_new(algo: AeadAlgorithm, hash_name: str, is_enc: bool, secret: bytes, label_prefix: str | None = None) -> AeadContext:
+    """ptls_aead_new (lib/picotls.c:6529-6551): traffic key and IV from a secret (get_traffic_keys), then
+    ptls_aead_new_direct. hash_name is the suite hash ("sha256", "sha384")."""
+    from .keyschedule import traffic_keys
+
+    key, iv = traffic_keys(algo.key_size, hash_name, secret, algo.iv_size, label_prefix)
     return AeadContext(algo, is_enc, key, iv)

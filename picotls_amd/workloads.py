@@ -1,6 +1,7 @@
 """The benchmark / parity workloads of BASELINE.json (synthetic record batches) and their deterministic generators.
 
 configs (BASELINE.json):
+  ptlsbench  1000-record batches of 16384 B under t/ptlsbench.c's conventions (ptlsbench_batch)          (configs[0])
   tls16k     1M x 16384 B TLS records, AES-128-GCM, one traffic key, AAD = TLS header {23,3,3,len}   (configs[1])
   quic1200   4M x 1200 B QUIC-sized records, AES-128-GCM, one key, 13-byte AAD                      (configs[2])
   mixed      4M records, L ~ U[64, 16384], AES-256-GCM, 64K keys (many-connection case)             (configs[3])
@@ -144,6 +145,26 @@ class Workload:
             return arena
         slot = batch.aad_bytes // max(batch.n, 1)
         return payload_np(self.seed ^ 0x414144, begin * slot, batch.aad_bytes).copy()
+
+
+# BASELINE.json configs[0]: t/ptlsbench.c's conventions (bench_run_aead :187-247, bench_run_one :88-185)
+PTLSBENCH_BATCH = 1000  # BENCH_BATCH, t/ptlsbench.c:86
+PTLSBENCH_SECRET = b"z" * 64  # memset(secret, 'z', sizeof(secret)), t/ptlsbench.c:223
+
+
+def ptlsbench_batch(n: int = PTLSBENCH_BATCH, rec_len: int = 16384, key_size: int = 16):
+    """One ptlsbench batch as a record batch: key and IV from ptls_aead_new(aead, hash, is_enc, 32 x 'z', NULL)
+    (:223-225; SHA-256 for AES-128, SHA-384 for AES-256, :271-274), seq = 1..n, AAD = uint64_t h[4] with h[0] = seq
+    (32 bytes, little endian, :130, :141), all-zero plaintext (:117). Returns (batch, key, iv, aad arena); the
+    plaintext arena is b.pt_bytes zero bytes."""
+    from .keyschedule import traffic_keys
+
+    key, iv = traffic_keys(key_size, "sha256" if key_size == 16 else "sha384", PTLSBENCH_SECRET)
+    seqs = np.arange(1, n + 1, dtype=np.uint64)
+    b = RecordBatch.build(np.full(n, rec_len, dtype=np.uint64), 32, seqs=seqs)
+    aad = np.zeros(b.aad_bytes, np.uint8)
+    aad.view("<u8").reshape(n, 4)[:, 0] = seqs
+    return b, key, iv, aad
 
 
 WORKLOADS = {
