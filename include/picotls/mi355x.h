@@ -41,16 +41,17 @@ extern "C" {
 
 /**
  * One record of a batch (40 bytes, little endian, 8-byte aligned array). Offsets are byte offsets into the arenas
- * passed to the batch call.
+ * passed to the batch call. The AAD length is aad_len | flags << 16 for seal_batch / open_batch (flags = 0 for AADs
+ * below 64 KiB; PTLS_MI355X_RECORD_AAD_LEN); the framed calls below give flags their own meaning.
  *   seal: reads  in[in_off .. in_off+len)            plaintext
  *         writes out[out_off .. out_off+len+16)      ciphertext || tag   (out may alias in)
  *   open: reads  in[in_off .. in_off+len+16)         ciphertext || tag
  *         writes out[out_off .. out_off+len)         plaintext            (out may alias in)
  *   aad:  aad[aad_off .. aad_off+aad_len)
  *   nonce = static_iv(key_idx) ^ (0^32 || seq big-endian)        (lib/picotls.c:6587-6601, lib/fusion.c:1127-1134)
- * len is at most PTLS_MI355X_MAX_RECORD_LEN and key_idx is below the keyset size: a record with a larger len or key_idx
- * is rejected (nothing is written for it; open reports ok = 0), so a corrupt descriptor cannot address memory beyond
- * the offsets it names.
+ * len is at most PTLS_MI355X_MAX_RECORD_LEN, the AAD at most PTLS_MI355X_MAX_AAD_LEN and key_idx is below the keyset
+ * size: a record with a larger len, AAD or key_idx is rejected (nothing is written for it; open reports ok = 0), so a
+ * corrupt descriptor cannot address memory beyond the offsets it names.
  */
 typedef struct st_ptls_mi355x_record_t {
     uint64_t in_off;
@@ -60,11 +61,13 @@ typedef struct st_ptls_mi355x_record_t {
     uint32_t len;
     uint32_t key_idx;
     uint16_t aad_len;
-    uint16_t flags; /* reserved, must be 0 */
+    uint16_t flags; /* seal_batch / open_batch: bits 16..31 of the AAD length; TLS framing: the content type */
 } ptls_mi355x_record_t;
 
 #define PTLS_MI355X_RECORD_SIZE 40
-#define PTLS_MI355X_MAX_RECORD_LEN (1u << 24) /* 16 MiB; TLS caps records at 2^14 + 256 */
+#define PTLS_MI355X_MAX_RECORD_LEN (1u << 30) /* 1 GiB; TLS caps records at 2^14 + 256 */
+#define PTLS_MI355X_MAX_AAD_LEN (1u << 30)
+#define PTLS_MI355X_RECORD_AAD_LEN(r) ((uint32_t)(r)->aad_len | (uint32_t)(r)->flags << 16)
 
 typedef struct st_ptls_mi355x_keyset_t ptls_mi355x_keyset_t;
 
@@ -77,10 +80,17 @@ int ptls_mi355x_is_supported(void);
  * Creates a keyset of nkeys AES-GCM traffic keys on the current HIP device.
  * keys: nkeys * key_size bytes (host memory), ivs: nkeys * 12 bytes (host memory), key_size: 16 or 32.
  * Returns NULL on invalid arguments or device failure.
+ *
+ * Keysets are independent, like picotls contexts (lib/picotls.c:6553-6568): creating, rekeying or freeing one never
+ * waits for the device as a whole, only (where stated) for that keyset's own work. A one-key keyset (what each
+ * ptls_aead_new_direct on the MI355X objects makes) takes an entry from a per-device pool and one setup launch whose key
+ * travels in the kernel arguments; the call does not wait for it (the keyset's first use does, on the GPU). A many-key
+ * keyset waits until its key arrays have been copied to the device.
  */
 ptls_mi355x_keyset_t *ptls_mi355x_keyset_new(const void *keys, const void *ivs, size_t nkeys, size_t key_size);
 /**
- * Destroys a keyset; device key material is cleared first (ptls_clear_memory, lib/fusion.c:1045).
+ * Destroys a keyset. Device key material is cleared (ptls_clear_memory, lib/fusion.c:1045) in stream order after every
+ * launch already made with the keyset, on any stream; the call itself does not wait.
  */
 void ptls_mi355x_keyset_free(ptls_mi355x_keyset_t *ks);
 size_t ptls_mi355x_keyset_size(const ptls_mi355x_keyset_t *ks);
@@ -89,7 +99,9 @@ size_t ptls_mi355x_keyset_key_size(const ptls_mi355x_keyset_t *ks);
  * Replaces the key and static IV of the n entries key_idx[0..n) (host arrays: n * key_size key bytes, n * 12 IV bytes),
  * deriving their schedules and H powers on the device: the rekey of some connections of a many-connection keyset, e.g.
  * after a TLS 1.3 KeyUpdate (picotls rekeys a sender once its record sequence number reaches 2^24,
- * lib/picotls.c:6220-6232, update_send_key -> setup_traffic_protection). Synchronous: waits for work in flight.
+ * lib/picotls.c:6220-6232, update_send_key -> setup_traffic_protection). Stream-ordered: launches made with the keyset
+ * before the call use the old entries, launches made after it the new ones; the call waits for the keyset's launches in
+ * flight (not for other work on the device) and for the copies of its arguments.
  * Returns 0, or -1 on invalid arguments / out-of-range or repeated indices (nothing changed) or device failure.
  */
 int ptls_mi355x_keyset_update(ptls_mi355x_keyset_t *ks, const uint32_t *key_idx, const void *keys, const void *ivs, size_t n);
@@ -115,7 +127,10 @@ int ptls_mi355x_keyset_set_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, const vo
 int ptls_mi355x_keyset_set_schedule(ptls_mi355x_keyset_t *ks, int schedule);
 
 /**
- * Seals nrecs records in one launch. recs, in, aad, out are DEVICE pointers. Asynchronous on `stream`.
+ * Seals nrecs records in one launch. Asynchronous on `stream`. recs, in, aad, out (and ok, results of the calls below)
+ * are addresses the device can access: device memory, host memory from hipHostMalloc (its address is the device
+ * address), or host memory registered with hipHostRegister passed as the address hipHostGetDevicePointer returns for it
+ * (that address may differ from the host pointer). Kernels reading and writing host memory do so over PCIe.
  * Records may come in any order: with a many-key keyset (up to 2^20 keys) a batch whose key runs would average under
  * 8 records is grouped by key_idx on the device first (scratch kept in the keyset; batches on different streams that
  * share the keyset are ordered through it).
@@ -124,13 +139,13 @@ int ptls_mi355x_keyset_set_schedule(ptls_mi355x_keyset_t *ks, int schedule);
 int ptls_mi355x_seal_batch(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
                            const void *aad, void *out, void *stream);
 /**
- * Opens nrecs records in one launch; ok[i] = 1 when record i authenticated, 0 otherwise. DEVICE pointers.
+ * Opens nrecs records in one launch; ok[i] = 1 when record i authenticated, 0 otherwise. Pointers as for seal_batch.
  */
 int ptls_mi355x_open_batch(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
                            const void *aad, void *out, uint8_t *ok, void *stream);
 
 /**
- * AES-ECB of nblocks 16-byte blocks, block i under key key_idx[i] (key_idx may be NULL: key 0). DEVICE pointers.
+ * AES-ECB of nblocks 16-byte blocks, block i under key key_idx[i] (key_idx may be NULL: key 0). Pointers as for seal_batch.
  * The single-block cipher of fusion (ptls_fusion_aesecb_encrypt, lib/fusion.c:924) batched; QUIC header-protection
  * masks are AES-ECB of the ciphertext sample (lib/fusion.c:1051-1101).
  */
@@ -192,7 +207,7 @@ int ptls_mi355x_open_tls12_records(ptls_mi355x_keyset_t *ks, const ptls_mi355x_r
  * header-protection key in hp_ks. mask[i] (16 bytes at masks + 16 i) = AES-ECB(hp key, sample), i.e. the first
  * keystream block of the AES-CTR cipher initialised with the sample, which is what ptls_aead_encrypt_s writes into
  * supp->output (include/picotls.h:441-456, lib/picotls.c ptls_aead__do_encrypt_s; fusion fuses it into the seal,
- * lib/fusion.c:425-430,636-651). Entries with key_idx >= the keyset size get a zero mask. DEVICE pointers.
+ * lib/fusion.c:425-430,636-651). Entries with key_idx >= the keyset size get a zero mask. Pointers as for seal_batch.
  */
 typedef struct st_ptls_mi355x_hp_t {
     uint64_t sample_off; /* byte offset of the 16-byte sample from base */
@@ -217,7 +232,7 @@ int ptls_mi355x_seal_batch_hp(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record
  * its IVs are unused): encrypt = 1 gives ptls_cipher_encrypt on a context made with ptls_cipher_new(&quiclb, 1, key),
  * encrypt = 0 the inverse (is_enc = 0). len is PTLS_QUICLB_MIN_BLOCK_SIZE (7) .. PTLS_QUICLB_MAX_BLOCK_SIZE (19)
  * (include/picotls.h:116-122); entries with another len or an out-of-range key_idx are skipped (nothing written), where
- * the reference asserts. DEVICE pointers; returns -1 on invalid arguments or a keyset that is not AES-128.
+ * the reference asserts. Pointers as for seal_batch; returns -1 on invalid arguments or a keyset that is not AES-128.
  */
 #define PTLS_MI355X_QUICLB_MIN_LEN 7
 #define PTLS_MI355X_QUICLB_MAX_LEN 19
@@ -237,15 +252,38 @@ int ptls_mi355x_quiclb_transform(ptls_mi355x_keyset_t *ks, size_t key_idx, void 
                                  int encrypt);
 
 /**
- * Synchronous single-record helpers on HOST buffers (a batch of one through the keyset's pinned staging buffer, which
- * the kernel reads and writes in place over PCIe; not thread-safe per keyset, like a picotls AEAD context). These back
- * the picotls vtable (do_encrypt / do_decrypt) and mirror ptls_aead_encrypt / ptls_aead_decrypt: encrypt writes len+16 bytes;
- * decrypt takes inlen = len+16 and returns the plaintext length or SIZE_MAX (tag mismatch or inlen < 16).
+ * Synchronous single-record helpers on HOST buffers: a batch of one through a pinned staging buffer taken from a
+ * per-device pool for the duration of the call (its kernels read and write it in place over PCIe), so calls on different
+ * keysets from different threads run concurrently and share nothing. These back the picotls vtable (do_encrypt /
+ * do_decrypt / do_encrypt_v) and mirror ptls_aead_encrypt / ptls_aead_decrypt: encrypt writes len+16 bytes (output may
+ * alias input); decrypt takes inlen = len+16 and returns the plaintext length or SIZE_MAX (tag mismatch, inlen < 16, or
+ * an engine error, which ptls_mi355x_last_error then describes). len and aadlen are limited by
+ * PTLS_MI355X_MAX_RECORD_LEN / PTLS_MI355X_MAX_AAD_LEN (fusion has no limit; TLS and QUIC records are far below it).
+ * Environment, read when a device is first used: PTLS_MI355X_MAX_STAGE_BYTES caps the staging buffer of one call (a
+ * larger record fails), PTLS_MI355X_STAGE_COPY=1 copies through device memory instead of mapping the pinned buffer.
  */
 int ptls_mi355x_encrypt(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const void *input, size_t inlen, uint64_t seq,
                         const void *aad, size_t aadlen);
 size_t ptls_mi355x_decrypt(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const void *input, size_t inlen,
                            uint64_t seq, const void *aad, size_t aadlen);
+/**
+ * encrypt over the concatenation of incnt input vectors (do_encrypt_v, include/picotls.h:501-507; the TLS record layer's
+ * {payload, content type}, lib/picotls.c:728-738), gathered straight into the staging buffer. Same layout as ptls_iovec_t.
+ */
+typedef struct st_ptls_mi355x_iovec_t {
+    const void *base;
+    size_t len;
+} ptls_mi355x_iovec_t;
+int ptls_mi355x_encrypt_v(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const ptls_mi355x_iovec_t *input, size_t incnt,
+                          uint64_t seq, const void *aad, size_t aadlen);
+/**
+ * encrypt, then the QUIC header-protection mask of the 16 sealed bytes at output + sample_off (sample_off + 16 <=
+ * inlen + 16) under key hp_key_idx of hp_ks, in the same round trip: ptls_aead_encrypt_s with supp (include/picotls.h:
+ * 441-456, 2109-2113), whose mask fusion computes inside the seal (lib/fusion.c:425-430,636-651). mask: 16 bytes.
+ */
+int ptls_mi355x_encrypt_s(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const void *input, size_t inlen, uint64_t seq,
+                          const void *aad, size_t aadlen, ptls_mi355x_keyset_t *hp_ks, size_t hp_key_idx, size_t sample_off,
+                          void *mask);
 
 /**
  * One AES-ECB block on HOST buffers under key key_idx (ptls_fusion_aesecb_encrypt, lib/fusion.c:924). Backs the

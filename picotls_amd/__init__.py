@@ -52,6 +52,8 @@ ABI_FUNCTIONS = (
     "ptls_mi355x_quiclb_batch",
     "ptls_mi355x_quiclb_transform",
     "ptls_mi355x_encrypt",
+    "ptls_mi355x_encrypt_v",
+    "ptls_mi355x_encrypt_s",
     "ptls_mi355x_decrypt",
     "ptls_mi355x_encrypt_block",
     "ptls_mi355x_last_error",
@@ -97,6 +99,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.ptls_mi355x_open_tls12_records.argtypes = [vp, vp, sz, vp, vp, vp, vp, vp]
     lib.ptls_mi355x_seal_batch_hp.argtypes = [vp, vp, sz, vp, vp, vp, vp, vp, vp, vp]
     lib.ptls_mi355x_encrypt.argtypes = [vp, sz, vp, vp, sz, u64, vp, sz]
+    lib.ptls_mi355x_encrypt_v.argtypes = [vp, sz, vp, vp, sz, u64, vp, sz]
+    lib.ptls_mi355x_encrypt_s.argtypes = [vp, sz, vp, vp, sz, u64, vp, sz, vp, sz, sz, vp]
     lib.ptls_mi355x_decrypt.argtypes = [vp, sz, vp, vp, sz, u64, vp, sz]
     lib.ptls_mi355x_decrypt.restype = sz
     lib.ptls_mi355x_encrypt_block.argtypes = [vp, sz, vp, vp]
@@ -313,11 +317,29 @@ class AeadContext:
             raise _err("ptls_mi355x_encrypt")
         return bytes(out)
 
-    # ptls_aead_encrypt_s with a header-protection cipher (include/picotls.h:2109-2113, lib/fusion.c:425-430,636-651)
+    # ptls_aead_encrypt_v (include/picotls.h:2115-2119): the vectors sealed as one record
+    def encrypt_v(self, vecs: list, seq: int, aad: bytes = b"") -> bytes:
+        bufs = [bytes(v) for v in vecs]
+        arr = (ctypes.c_void_p * (2 * max(len(bufs), 1)))()
+        for i, b in enumerate(bufs):
+            arr[2 * i] = ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value if b else None
+            arr[2 * i + 1] = len(b)
+        total = sum(len(b) for b in bufs)
+        out = bytearray(total + self.algo.tag_size)
+        if load_library().ptls_mi355x_encrypt_v(self.ks.handle, 0, _buf(out), ctypes.cast(arr, ctypes.c_void_p), len(bufs), seq,
+                                               _buf(bytes(aad)), len(aad)) != 0:
+            raise _err("ptls_mi355x_encrypt_v")
+        return bytes(out)
+
+    # ptls_aead_encrypt_s with a header-protection cipher (include/picotls.h:2109-2113, lib/fusion.c:425-430,636-651):
+    # the mask of the sealed sample at sample_off, computed in the seal's round trip (ptls_mi355x_encrypt_s)
     def encrypt_s(self, pt: bytes, seq: int, aad: bytes, hp: "CtrCipher", sample_off: int) -> tuple[bytes, bytes]:
-        sealed = self.encrypt(pt, seq, aad)
-        sample = sealed[sample_off:sample_off + 16]
-        return sealed, hp.mask(sample)
+        out = bytearray(len(pt) + self.algo.tag_size)
+        mask = bytearray(16)
+        if load_library().ptls_mi355x_encrypt_s(self.ks.handle, 0, _buf(out), _buf(bytes(pt)), len(pt), seq, _buf(bytes(aad)),
+                                               len(aad), hp.ks.handle, 0, sample_off, _buf(mask)) != 0:
+            raise _err("ptls_mi355x_encrypt_s")
+        return bytes(out), bytes(mask)
 
     # ptls_aead_decrypt (include/picotls.h:2160-2164): plaintext, or None for SIZE_MAX
     def decrypt(self, ct_tag: bytes, seq: int, aad: bytes = b"") -> bytes | None:

@@ -28,8 +28,12 @@
 // 4c..4c+3 = AES state column c. GHASH elements use the same byte order (byte 0 holds x^0..x^7, MSB first).
 
 #include <hip/hip_runtime.h>
+#include <atomic>
+#include <mutex>
+#include <new>
 #include <type_traits>
 #include <vector>
+#include <stdlib.h>
 #include <stdint.h>
 #include <string.h>
 #include <stdio.h>
@@ -64,83 +68,65 @@ static int fail(const char *fmt, const char *detail)
             return fail(#expr ": %s", hipGetErrorString(e_));                                                                 \
     } while (0)
 
-struct st_ptls_mi355x_keyset_t {
-    int device;
-    size_t nkeys, key_size;
-    int nr;
-    KeyEntry *d_keys;
-    int ncu;
-    int schedule;
-    // staging for the synchronous host-buffer helpers (the per-record picotls path): one pinned host buffer and one
-    // device buffer, grown on demand, and a stream of their own, so a call is one H2D copy, one launch, one D2H copy
-    uint8_t *d_stage, *h_stage;
-    uint8_t *h_stage_dev;  // device address of h_stage (NULL: not mapped, every round trip copies)
-    size_t stage_cap;
+static void clear_memory(void *p, size_t n)  // ptls_clear_memory: a memset the compiler may not drop
+{
+    volatile uint8_t *v = (volatile uint8_t *)p;
+    while (n-- != 0)
+        *v++ = 0;
+}
+
+// ---- per-device state
+//
+// picotls contexts are independent (lib/picotls.c:6553-6568: a context is malloc'd, set up and freed by its owner,
+// fusion's setup touches nothing shared; SURVEY 8(b) Threading), and a QUIC or TLS server creates and frees them per
+// connection and epoch. So nothing here waits for the whole device (no hipDeviceSynchronize, no hipFree, whose implicit
+// device-wide synchronisation would stall every batch in flight):
+//   * one-key keysets (a picotls context) take a 512-byte entry from a per-device slab and are set up by one launch whose
+//     key travels in the kernel arguments, on the device's setup stream, with an event their first use waits for;
+//   * teardown, rekey and IV changes run on the device's maintenance stream, ordered after the keyset's own launches
+//     (an event per stream it was used on), and a freed slab entry returns to the pool only once it has been cleared;
+//   * the synchronous host-buffer helpers (the per-record picotls path) take a staging buffer and its stream from a
+//     per-device pool for the duration of one call, so concurrent contexts on different threads never share one.
+
+#define MAX_DEVICES 64
+#define STAGE_CLASSES 26   // pinned staging buffers of 4 KiB << class
+#define SLAB_ENTRIES 1024  // one-key keyset entries per slab (512 KiB)
+
+struct Stager {
     hipStream_t stream;
-    // key grouping of ungrouped many-key batches (key_group_*): scratch for key counts and the record permutation,
-    // grown on demand; group_ev orders its users when batches on several streams share the keyset
-    u32 *d_group;
-    size_t group_cap;
-    hipEvent_t group_ev;
+    uint8_t *h;      // pinned host buffer
+    uint8_t *h_dev;  // its device address (NULL: not mapped, or PTLS_MI355X_STAGE_COPY=1: round trips copy through d)
+    uint8_t *d;      // device buffer of the copy path
+    size_t cap;
+    int cls;
+    Stager *next;
 };
 
-static int stage_reserve(ptls_mi355x_keyset_t *ks, size_t bytes)
-{
-    if (bytes <= ks->stage_cap)
-        return 0;
-    size_t cap = ks->stage_cap * 2 > bytes ? ks->stage_cap * 2 : bytes;
-    cap = cap < 4096 ? 4096 : (cap + 4095) & ~(size_t)4095;
-    if (ks->stream == NULL)
-        HIP_TRY(hipStreamCreateWithFlags(&ks->stream, hipStreamNonBlocking));
-    if (ks->d_stage != NULL) {
-        HIP_TRY(hipStreamSynchronize(ks->stream));
-        (void)hipFree(ks->d_stage);
-        (void)hipHostFree(ks->h_stage);
-        ks->d_stage = ks->h_stage = ks->h_stage_dev = NULL;
-        ks->stage_cap = 0;
-    }
-    HIP_TRY(hipMalloc((void **)&ks->d_stage, cap));
-    if (hipHostMalloc((void **)&ks->h_stage, cap, hipHostMallocDefault) != hipSuccess) {
-        (void)hipFree(ks->d_stage);
-        ks->d_stage = NULL;
-        return fail("%s", "stage: pinned host allocation failed");
-    }
-    if (hipHostGetDevicePointer((void **)&ks->h_stage_dev, ks->h_stage, 0) != hipSuccess)
-        ks->h_stage_dev = NULL;
-    ks->stage_cap = cap;
-    return 0;
-}
+struct PendingSlot {
+    KeyEntry *e;
+    hipEvent_t cleared;
+};
 
-// Round trips run on the pinned host buffer itself when it is mapped into the device's address space: the kernel reads
-// its input and writes its output over PCIe, and the call saves the two copy launches. Measured against copying
-// (tools/latency.py, interleaved): 16 B 29 -> 26 us, 1200 B 31 -> 29, 16 KiB 52 -> 38, 4 MiB 1.70 -> 1.58 ms.
-static uint8_t *stage_dev(const ptls_mi355x_keyset_t *ks)
-{
-    return ks->h_stage_dev != NULL ? ks->h_stage_dev : ks->d_stage;
-}
+struct DeviceState {
+    int device = 0, ncu = 0;
+    hipStream_t setup = nullptr;  // one-key and many-key setup launches (never waits on anything)
+    hipStream_t maint = nullptr;  // teardown, rekey, set_iv: ordered after the keyset's launches
+    int priority = 0;             // the device's greatest stream priority: the engine's own streams (setup, teardown,
+                                  // per-record round trips) are dispatched ahead of bulk batches on ordinary streams
+    bool force_copy = false;      // PTLS_MI355X_STAGE_COPY=1: the staging round trip copies instead of mapping
+    size_t stage_limit = 0;       // PTLS_MI355X_MAX_STAGE_BYTES: the largest staging buffer one call may use
+    std::mutex mu;                // the pools below
+    Stager *stagers[STAGE_CLASSES] = {};
+    std::vector<KeyEntry *> slots;
+    std::vector<PendingSlot> pending;
+    std::vector<hipEvent_t> events;
+};
 
-// the synchronous round trip of the host-buffer helpers, on the buffer stage_dev returned (d): unless that is the
-// pinned buffer itself, H2D of the first `up` staged bytes before the launch (run by the caller's lambda) and D2H of
-// [down_off, down_off + down) after it; then wait
-template <typename Launch>
-static int stage_roundtrip(ptls_mi355x_keyset_t *ks, const uint8_t *d, size_t up, size_t down_off, size_t down, Launch launch)
-{
-    const bool copy = d == ks->d_stage;
-    if (copy)
-        HIP_TRY(hipMemcpyAsync(ks->d_stage, ks->h_stage, up, hipMemcpyHostToDevice, ks->stream));
-    if (launch() != 0)
-        return -1;
-    if (copy)
-        HIP_TRY(hipMemcpyAsync(ks->h_stage + down_off, ks->d_stage + down_off, down, hipMemcpyDeviceToHost, ks->stream));
-    HIP_TRY(hipStreamSynchronize(ks->stream));
-    return 0;
-}
+static std::atomic<DeviceState *> g_devs[MAX_DEVICES];
+static std::mutex g_devs_mu;
 
-static int engine_init_attrs(void)
+static int set_kernel_attrs(void)
 {
-    static int done = 0;
-    if (done)
-        return 0;
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<10, false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<10, true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<14, false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
@@ -166,8 +152,270 @@ static int engine_init_attrs(void)
     HIP_TRY(hipFuncSetAttribute((const void *)hp_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
     HIP_TRY(hipFuncSetAttribute((const void *)hp_kernel<14>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
     HIP_TRY(hipFuncSetAttribute((const void *)quiclb_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
-    done = 1;
     return 0;
+}
+
+// The state of HIP device `dev` (the current device of the calling thread), created on first use under a lock; it
+// lives as long as the process (it holds the pools).
+static DeviceState *device_state(int dev)
+{
+    if (dev < 0 || dev >= MAX_DEVICES) {
+        fail("%s", "device index out of range");
+        return nullptr;
+    }
+    DeviceState *ds = g_devs[dev].load(std::memory_order_acquire);
+    if (ds != nullptr)
+        return ds;
+    std::lock_guard<std::mutex> lk(g_devs_mu);
+    if ((ds = g_devs[dev].load(std::memory_order_relaxed)) != nullptr)
+        return ds;
+    ds = new (std::nothrow) DeviceState();
+    if (ds == nullptr) {
+        fail("%s", "out of memory");
+        return nullptr;
+    }
+    ds->device = dev;
+    const char *copy = getenv("PTLS_MI355X_STAGE_COPY"), *limit = getenv("PTLS_MI355X_MAX_STAGE_BYTES");
+    ds->force_copy = copy != nullptr && strcmp(copy, "1") == 0;
+    ds->stage_limit = limit != nullptr ? (size_t)strtoull(limit, nullptr, 0) : (size_t)4096 << (STAGE_CLASSES - 1);
+    int least = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &ds->priority) != hipSuccess)
+        ds->priority = 0;
+    if (hipDeviceGetAttribute(&ds->ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || set_kernel_attrs() != 0 ||
+        hipStreamCreateWithPriority(&ds->setup, hipStreamNonBlocking, ds->priority) != hipSuccess ||
+        hipStreamCreateWithPriority(&ds->maint, hipStreamNonBlocking, ds->priority) != hipSuccess) {
+        if (ds->setup != nullptr)
+            (void)hipStreamDestroy(ds->setup);
+        delete ds;
+        fail("%s", "device initialisation failed");
+        return nullptr;
+    }
+    g_devs[dev].store(ds, std::memory_order_release);
+    return ds;
+}
+
+static DeviceState *current_device_state(void)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        fail("%s", "hipGetDevice failed");
+        return nullptr;
+    }
+    return device_state(dev);
+}
+
+// makes `dev` the calling thread's current device for the scope of a call (a context may be used from a thread whose
+// current device is another one), restoring the previous one after
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(int dev)
+    {
+        int cur = 0;
+        if (hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess)
+            prev = cur;
+    }
+    ~DeviceScope()
+    {
+        if (prev >= 0)
+            (void)hipSetDevice(prev);
+    }
+};
+
+static hipEvent_t event_get(DeviceState *ds)
+{
+    {
+        std::lock_guard<std::mutex> lk(ds->mu);
+        if (!ds->events.empty()) {
+            hipEvent_t e = ds->events.back();
+            ds->events.pop_back();
+            return e;
+        }
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+        return nullptr;
+    return e;
+}
+
+static void event_put(DeviceState *ds, hipEvent_t e)
+{
+    if (e == nullptr)
+        return;
+    std::lock_guard<std::mutex> lk(ds->mu);
+    ds->events.push_back(e);
+}
+
+// one cleared keyset entry from the slab: a free one, else one whose clearing (keyset_free) has completed, else a new slab
+static KeyEntry *slot_get(DeviceState *ds)
+{
+    {
+        std::lock_guard<std::mutex> lk(ds->mu);
+        if (ds->slots.empty()) {
+            for (size_t i = 0; i < ds->pending.size();) {
+                if (hipEventQuery(ds->pending[i].cleared) == hipSuccess) {
+                    ds->slots.push_back(ds->pending[i].e);
+                    ds->events.push_back(ds->pending[i].cleared);
+                    ds->pending[i] = ds->pending.back();
+                    ds->pending.pop_back();
+                } else {
+                    ++i;
+                }
+            }
+        }
+        if (!ds->slots.empty()) {
+            KeyEntry *e = ds->slots.back();
+            ds->slots.pop_back();
+            return e;
+        }
+    }
+    KeyEntry *slab = nullptr;
+    if (hipMalloc((void **)&slab, SLAB_ENTRIES * sizeof(KeyEntry)) != hipSuccess) {
+        fail("%s", "keyset slab allocation failed");
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> lk(ds->mu);
+    for (int i = SLAB_ENTRIES - 1; i >= 1; --i)
+        ds->slots.push_back(slab + i);
+    return slab;
+}
+
+static Stager *stager_get(DeviceState *ds, size_t bytes)
+{
+    if (bytes > ds->stage_limit) {
+        fail("%s", "staging: the call needs more than PTLS_MI355X_MAX_STAGE_BYTES");
+        return nullptr;
+    }
+    int cls = 0;
+    while (cls < STAGE_CLASSES && ((size_t)4096 << cls) < bytes)
+        ++cls;
+    if (cls == STAGE_CLASSES) {
+        fail("%s", "staging: record too large");
+        return nullptr;
+    }
+    {
+        std::lock_guard<std::mutex> lk(ds->mu);
+        Stager *s = ds->stagers[cls];
+        if (s != nullptr) {
+            ds->stagers[cls] = s->next;
+            return s;
+        }
+    }
+    Stager *s = new (std::nothrow) Stager();
+    if (s == nullptr) {
+        fail("%s", "out of memory");
+        return nullptr;
+    }
+    s->cap = (size_t)4096 << cls;
+    s->cls = cls;
+    if (hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, ds->priority) != hipSuccess) {
+        delete s;
+        fail("%s", "staging: stream creation failed");
+        return nullptr;
+    }
+    if (hipHostMalloc((void **)&s->h, s->cap, hipHostMallocDefault) != hipSuccess) {
+        (void)hipStreamDestroy(s->stream);
+        delete s;
+        fail("%s", "staging: pinned host allocation failed");
+        return nullptr;
+    }
+    if (ds->force_copy || hipHostGetDevicePointer((void **)&s->h_dev, s->h, 0) != hipSuccess)
+        s->h_dev = nullptr;
+    if (s->h_dev == nullptr && hipMalloc((void **)&s->d, s->cap) != hipSuccess) {
+        (void)hipHostFree(s->h);
+        (void)hipStreamDestroy(s->stream);
+        delete s;
+        fail("%s", "staging: device allocation failed");
+        return nullptr;
+    }
+    return s;
+}
+
+static void stager_put(DeviceState *ds, Stager *s)
+{
+    std::lock_guard<std::mutex> lk(ds->mu);
+    s->next = ds->stagers[s->cls];
+    ds->stagers[s->cls] = s;
+}
+
+struct st_ptls_mi355x_keyset_t {
+    DeviceState *ds;
+    int device;
+    size_t nkeys, key_size;
+    int nr;
+    KeyEntry *d_keys;
+    bool slot;  // d_keys is one entry of the device's slab (one-key keysets)
+    int schedule;
+    hipEvent_t ready;                  // the last setup / update / set_iv of the entries
+    std::atomic<bool> ready_seen;      // ... known to be complete: launches need not wait for it
+    std::vector<uint8_t> ivs;          // the static IVs (do_get_iv reads these; the device copy is what seals use)
+    std::mutex mu;                     // launches from several threads: uses, group scratch
+    std::vector<std::pair<hipStream_t, hipEvent_t>> uses;  // per stream: after this keyset's last launch on it
+    // key grouping of ungrouped many-key batches (key_group_*): scratch for key counts and the record permutation,
+    // grown on demand (stream-ordered); group_ev orders its users when batches on several streams share the keyset
+    u32 *d_group;
+    size_t group_cap;
+    hipEvent_t group_ev;
+};
+
+// makes `s` wait for the keyset's last setup / update / set_iv, unless that is known to be complete
+static int wait_ready(ptls_mi355x_keyset_t *ks, hipStream_t s)
+{
+    if (ks->ready_seen.load(std::memory_order_acquire))
+        return 0;
+    hipError_t q = hipEventQuery(ks->ready);
+    if (q == hipSuccess) {
+        ks->ready_seen.store(true, std::memory_order_release);
+        return 0;
+    }
+    if (q != hipErrorNotReady)
+        return fail("keyset setup failed: %s", hipGetErrorString(q));
+    HIP_TRY(hipStreamWaitEvent(s, ks->ready, 0));
+    return 0;
+}
+
+// records that the keyset's entries were used by work just launched on `s` (teardown and rekey wait for it)
+static int note_use(ptls_mi355x_keyset_t *ks, hipStream_t s)
+{
+    std::lock_guard<std::mutex> lk(ks->mu);
+    for (auto &u : ks->uses)
+        if (u.first == s)
+            return hipEventRecord(u.second, s) == hipSuccess ? 0 : fail("%s", "hipEventRecord failed");
+    hipEvent_t e = event_get(ks->ds);
+    if (e == nullptr)
+        return fail("%s", "event creation failed");
+    ks->uses.emplace_back(s, e);
+    HIP_TRY(hipEventRecord(e, s));
+    return 0;
+}
+
+// orders the maintenance stream after every launch that used the keyset and after its last setup
+static int maint_after_uses(ptls_mi355x_keyset_t *ks)
+{
+    std::lock_guard<std::mutex> lk(ks->mu);
+    for (auto &u : ks->uses)
+        HIP_TRY(hipStreamWaitEvent(ks->ds->maint, u.second, 0));
+    if (!ks->ready_seen.load(std::memory_order_acquire))
+        HIP_TRY(hipStreamWaitEvent(ks->ds->maint, ks->ready, 0));
+    return 0;
+}
+
+static int mark_ready(ptls_mi355x_keyset_t *ks, hipStream_t s)
+{
+    ks->ready_seen.store(false, std::memory_order_release);
+    HIP_TRY(hipEventRecord(ks->ready, s));
+    return 0;
+}
+
+static void keyset_destroy(ptls_mi355x_keyset_t *ks)
+{
+    DeviceState *ds = ks->ds;
+    for (auto &u : ks->uses)
+        event_put(ds, u.second);
+    event_put(ds, ks->ready);
+    if (ks->group_ev != nullptr)
+        (void)hipEventDestroy(ks->group_ev);
+    clear_memory(ks->ivs.data(), ks->ivs.size());
+    delete ks;
 }
 
 extern "C" {
@@ -192,36 +440,71 @@ ptls_mi355x_keyset_t *ptls_mi355x_keyset_new(const void *keys, const void *ivs, 
         fail("%s", "ptls_mi355x_keyset_new: invalid arguments");
         return NULL;
     }
-    if (engine_init_attrs() != 0)
+    DeviceState *ds = current_device_state();
+    if (ds == nullptr)
         return NULL;
-    ptls_mi355x_keyset_t *ks = (ptls_mi355x_keyset_t *)calloc(1, sizeof(*ks));
-    uint8_t *d_raw = NULL;
-    if (ks == NULL)
+    ptls_mi355x_keyset_t *ks = new (std::nothrow) st_ptls_mi355x_keyset_t();
+    if (ks == nullptr) {
+        fail("%s", "out of memory");
         return NULL;
+    }
+    ks->ds = ds;
+    ks->device = ds->device;
     ks->nkeys = nkeys, ks->key_size = key_size, ks->nr = key_size == 16 ? 10 : 14;
-    if (hipGetDevice(&ks->device) != hipSuccess || hipDeviceGetAttribute(&ks->ncu, hipDeviceAttributeMultiprocessorCount, ks->device) != hipSuccess)
-        goto Fail;
-    if (hipMalloc((void **)&ks->d_keys, nkeys * sizeof(KeyEntry)) != hipSuccess)
-        goto Fail;
-    if (hipMalloc((void **)&d_raw, nkeys * (key_size + 12)) != hipSuccess)
-        goto Fail;
-    if (hipMemcpy(d_raw, keys, nkeys * key_size, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(d_raw + nkeys * key_size, ivs, nkeys * 12, hipMemcpyHostToDevice) != hipSuccess)
-        goto Fail;
-    keyset_setup_kernel<<<(unsigned)((nkeys + 127) / 128), 128>>>(d_raw, d_raw + nkeys * key_size, ks->d_keys, (u32)nkeys, (u32)key_size);
-    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess)
-        goto Fail;
-    (void)hipMemset(d_raw, 0, nkeys * (key_size + 12));
-    (void)hipFree(d_raw);
+    ks->ready_seen.store(false);
+    ks->ivs.assign((const uint8_t *)ivs, (const uint8_t *)ivs + nkeys * 12);
+    if ((ks->ready = event_get(ds)) == nullptr) {
+        fail("%s", "ptls_mi355x_keyset_new: event creation failed");
+        delete ks;
+        return NULL;
+    }
+    if (nkeys == 1) {
+        // a picotls context: a slab entry and one launch with the key in its arguments, nothing to wait for
+        if ((ks->d_keys = slot_get(ds)) == nullptr) {
+            keyset_destroy(ks);
+            return NULL;
+        }
+        ks->slot = true;
+        RawKey raw = {};
+        memcpy(raw.key, keys, key_size);
+        memcpy(raw.iv, ivs, 12);
+        raw.key_size = (u32)key_size;
+        keyset_setup_one_kernel<<<1, 64, 0, ds->setup>>>(raw, ks->d_keys);
+        clear_memory(&raw, sizeof(raw));
+        if (hipGetLastError() != hipSuccess || mark_ready(ks, ds->setup) != 0) {
+            fail("%s", "ptls_mi355x_keyset_new: setup launch failed");
+            keyset_destroy(ks);  // the entry is not returned to the pool: its state is unknown
+            return NULL;
+        }
+        return ks;
+    }
+    // many keys: entries and the raw key material in stream-ordered memory on the setup stream. The caller's arrays are
+    // pageable host memory, so the call waits (for the setup stream only) until the copies have consumed them.
+    uint8_t *d_raw = nullptr;
+    const size_t raw_bytes = nkeys * (key_size + 12);
+    bool ok = hipMallocAsync((void **)&ks->d_keys, nkeys * sizeof(KeyEntry), ds->setup) == hipSuccess &&
+              hipMallocAsync((void **)&d_raw, raw_bytes, ds->setup) == hipSuccess &&
+              hipMemcpyAsync(d_raw, keys, nkeys * key_size, hipMemcpyHostToDevice, ds->setup) == hipSuccess &&
+              hipMemcpyAsync(d_raw + nkeys * key_size, ivs, nkeys * 12, hipMemcpyHostToDevice, ds->setup) == hipSuccess;
+    if (ok) {
+        keyset_setup_kernel<<<(unsigned)((nkeys + 127) / 128), 128, 0, ds->setup>>>(d_raw, d_raw + nkeys * key_size, ks->d_keys,
+                                                                                   (u32)nkeys, (u32)key_size);
+        ok = hipGetLastError() == hipSuccess;
+    }
+    if (d_raw != nullptr) {
+        (void)hipMemsetAsync(d_raw, 0, raw_bytes, ds->setup);
+        (void)hipFreeAsync(d_raw, ds->setup);
+    }
+    if (ok)
+        ok = mark_ready(ks, ds->setup) == 0 && hipStreamSynchronize(ds->setup) == hipSuccess;
+    if (!ok) {
+        if (ks->d_keys != nullptr)
+            (void)hipFreeAsync(ks->d_keys, ds->setup);
+        fail("%s", "ptls_mi355x_keyset_new: device setup failed");
+        keyset_destroy(ks);
+        return NULL;
+    }
     return ks;
-Fail:
-    fail("%s", "ptls_mi355x_keyset_new: device setup failed");
-    if (d_raw != NULL)
-        (void)hipFree(d_raw);
-    if (ks->d_keys != NULL)
-        (void)hipFree(ks->d_keys);
-    free(ks);
-    return NULL;
 }
 
 int ptls_mi355x_keyset_update(ptls_mi355x_keyset_t *ks, const uint32_t *key_idx, const void *keys, const void *ivs, size_t n)
@@ -238,48 +521,63 @@ int ptls_mi355x_keyset_update(ptls_mi355x_keyset_t *ks, const uint32_t *key_idx,
     }
     if (n == 0)
         return 0;
+    DeviceScope scope(ks->device);
+    DeviceState *ds = ks->ds;
+    // stream-ordered on the maintenance stream: after every launch already made with the old entries, before any made
+    // after this call (they wait for `ready`)
+    if (maint_after_uses(ks) != 0)
+        return -1;
     uint8_t *d = NULL;
     const size_t kb = n * ks->key_size, ib = n * 12, sb = n * 4;
-    HIP_TRY(hipMalloc((void **)&d, kb + ib + sb));
+    HIP_TRY(hipMallocAsync((void **)&d, kb + ib + sb, ds->maint));
     int ret = -1;
-    if (hipDeviceSynchronize() == hipSuccess &&  // no launch in flight still reads the old entries
-        hipMemcpy(d, keys, kb, hipMemcpyHostToDevice) == hipSuccess && hipMemcpy(d + kb, ivs, ib, hipMemcpyHostToDevice) == hipSuccess &&
-        hipMemcpy(d + kb + ib, key_idx, sb, hipMemcpyHostToDevice) == hipSuccess) {
-        keyset_setup_kernel<<<(unsigned)((n + 127) / 128), 128>>>(d, d + kb, ks->d_keys, (u32)n, (u32)ks->key_size,
-                                                                 (const u32 *)(d + kb + ib));
-        if (hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess)
+    if (hipMemcpyAsync(d, keys, kb, hipMemcpyHostToDevice, ds->maint) == hipSuccess &&
+        hipMemcpyAsync(d + kb, ivs, ib, hipMemcpyHostToDevice, ds->maint) == hipSuccess &&
+        hipMemcpyAsync(d + kb + ib, key_idx, sb, hipMemcpyHostToDevice, ds->maint) == hipSuccess) {
+        keyset_setup_kernel<<<(unsigned)((n + 127) / 128), 128, 0, ds->maint>>>(d, d + kb, ks->d_keys, (u32)n, (u32)ks->key_size,
+                                                                               (const u32 *)(d + kb + ib));
+        if (hipGetLastError() == hipSuccess && mark_ready(ks, ds->maint) == 0)
             ret = 0;
     }
-    (void)hipMemset(d, 0, kb + ib);
-    (void)hipDeviceSynchronize();
-    (void)hipFree(d);
+    (void)hipMemsetAsync(d, 0, kb + ib, ds->maint);
+    (void)hipFreeAsync(d, ds->maint);
+    // the caller's pageable arrays must have been consumed before returning
+    if (hipStreamSynchronize(ds->maint) != hipSuccess)
+        ret = -1;
     if (ret != 0)
-        fail("%s", "keyset_update: device setup failed");
-    return ret;
+        return fail("%s", "keyset_update: device setup failed");
+    for (size_t i = 0; i < n; ++i)
+        memcpy(ks->ivs.data() + (size_t)key_idx[i] * 12, (const uint8_t *)ivs + i * 12, 12);
+    return 0;
 }
 
 void ptls_mi355x_keyset_free(ptls_mi355x_keyset_t *ks)
 {
     if (ks == NULL)
         return;
-    (void)hipMemset(ks->d_keys, 0, ks->nkeys * sizeof(KeyEntry));
-    (void)hipDeviceSynchronize();
-    (void)hipFree(ks->d_keys);
-    if (ks->d_stage != NULL) {
-        (void)hipMemset(ks->d_stage, 0, ks->stage_cap);
-        memset(ks->h_stage, 0, ks->stage_cap);  // staged plaintext and keystream-derived bytes
-        (void)hipDeviceSynchronize();
-        (void)hipFree(ks->d_stage);
-        (void)hipHostFree(ks->h_stage);
+    DeviceScope scope(ks->device);
+    DeviceState *ds = ks->ds;
+    // key material is cleared (ptls_clear_memory, lib/fusion.c:1045) after the keyset's last launch, on the maintenance
+    // stream; nothing here waits on the host
+    bool ordered = maint_after_uses(ks) == 0;
+    if (ks->group_ev != nullptr && hipStreamWaitEvent(ds->maint, ks->group_ev, 0) != hipSuccess)
+        ordered = false;
+    if (!ordered)  // cannot order the teardown: keep the entries (never reused) rather than clear them under a launch
+        (void)hipStreamSynchronize(ds->maint);
+    (void)hipMemsetAsync(ks->d_keys, 0, ks->nkeys * sizeof(KeyEntry), ds->maint);
+    if (ks->d_group != nullptr)
+        (void)hipFreeAsync(ks->d_group, ds->maint);
+    if (ks->slot) {
+        // back to the pool once the clear has run (slot_get checks the event)
+        hipEvent_t cleared = event_get(ds);
+        if (cleared != nullptr && hipEventRecord(cleared, ds->maint) == hipSuccess) {
+            std::lock_guard<std::mutex> lk(ds->mu);
+            ds->pending.push_back({ks->d_keys, cleared});
+        }
+    } else {
+        (void)hipFreeAsync(ks->d_keys, ds->maint);
     }
-    if (ks->stream != NULL)
-        (void)hipStreamDestroy(ks->stream);
-    if (ks->group_ev != NULL) {
-        (void)hipEventSynchronize(ks->group_ev);
-        (void)hipEventDestroy(ks->group_ev);
-    }
-    (void)hipFree(ks->d_group);
-    free(ks);
+    keyset_destroy(ks);
 }
 
 #if ENGINE_PROFILE
@@ -308,119 +606,75 @@ size_t ptls_mi355x_keyset_key_size(const ptls_mi355x_keyset_t *ks) { return ks->
 
 int ptls_mi355x_keyset_get_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, void *iv)
 {
-    if (ks == NULL || key_idx >= ks->nkeys)
+    if (ks == NULL || key_idx >= ks->nkeys || iv == NULL)
         return fail("%s", "get_iv: bad key index");
-    u32 w[3];
-    HIP_TRY(hipMemcpy(w, ks->d_keys[key_idx].iv, 12, hipMemcpyDeviceToHost));
-    memcpy(iv, w, 12);
+    memcpy(iv, ks->ivs.data() + key_idx * 12, 12);
     return 0;
 }
 
 int ptls_mi355x_keyset_set_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, const void *iv)
 {
-    if (ks == NULL || key_idx >= ks->nkeys)
+    if (ks == NULL || key_idx >= ks->nkeys || iv == NULL)
         return fail("%s", "set_iv: bad key index");
+    DeviceScope scope(ks->device);
+    if (maint_after_uses(ks) != 0)
+        return -1;
     u32 w[3];
     memcpy(w, iv, 12);
-    HIP_TRY(hipMemcpy(ks->d_keys[key_idx].iv, w, 12, hipMemcpyHostToDevice));
+    keyset_set_iv_kernel<<<1, 1, 0, ks->ds->maint>>>(ks->d_keys + key_idx, w[0], w[1], w[2]);
+    HIP_TRY(hipGetLastError());
+    if (mark_ready(ks, ks->ds->maint) != 0)
+        return -1;
+    memcpy(ks->ivs.data() + key_idx * 12, iv, 12);
     return 0;
 }
+
+}  // extern "C"
 
 // Schedule choice (ptls_mi355x_keyset_set_schedule): AUTO = chunked. Its uniform runs take the whole-record path,
 // which measured at or above the lockstep kernel on one-key uniform batches (929 vs 841 GiB/s on 16 KiB records,
 // 784 vs 751 on 1200 B), and its chunked runs balance mixed lengths and short key runs.
-static bool use_chunked(const ptls_mi355x_keyset_t *ks) { return ks->schedule != PTLS_MI355X_SCHEDULE_LOCKSTEP; }
+static bool use_chunked(int schedule) { return schedule != PTLS_MI355X_SCHEDULE_LOCKSTEP; }
 
-static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
-                        const void *aad, void *out, uint8_t *ok, void *stream, int frame = 0, u32 unit_log2 = CHUNK_LOG2)
+// The GCM kernel launch of a batch over `nkeys` entries at `keys` (no key grouping, no keyset bookkeeping).
+static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int schedule, bool open, const ptls_mi355x_record_t *recs,
+                      size_t nrecs, const void *in, const void *aad, void *out, uint8_t *ok, hipStream_t s, int frame,
+                      u32 unit_log2, const ptls_mi355x_record_t *grouped = nullptr, const u32 *perm = nullptr,
+                      const u32 *perm_on = nullptr)
 {
-    if (ks == NULL || (nrecs != 0 && (recs == NULL || in == NULL || out == NULL || (open && ok == NULL))))
-        return fail("%s", "batch: invalid arguments");
-    if (nrecs == 0)
-        return 0;
-    BatchArgs a = {ks->d_keys, recs, (u64)nrecs, (const uint8_t *)in, (const uint8_t *)aad, (uint8_t *)out, ok,
-                   ks->nkeys > 1 ? 1u : 0u, (u32)ks->nkeys, unit_log2, nullptr, nullptr, nullptr};
+    BatchArgs a = {keys, recs, (u64)nrecs, (const uint8_t *)in, (const uint8_t *)aad, (uint8_t *)out, ok,
+                   nkeys > 1 ? 1u : 0u, nkeys, unit_log2, grouped, perm, perm_on};
     if (a.aad == NULL)
         a.aad = a.in;
     const u64 groups = (nrecs + (64 / ENGINE_G) - 1) / (64 / ENGINE_G);
     // one persistent workgroup per CU; small batches use fewer workgroups so each still gets >= 4 record groups
-    u64 grid = (u64)ks->ncu;
+    u64 grid = (u64)ncu;
     if (grid > (groups + 3) / 4)
         grid = (groups + 3) / 4;
     if (grid < 1)
         grid = 1;
-    hipStream_t s = (hipStream_t)stream;
-    // ungrouped many-key batches: group the records by key on the device first (see key_hist_kernel)
-#ifndef KEY_GROUP_DISABLE
-    const bool group = use_chunked(ks) && ks->nkeys > 1 && ks->nkeys <= KEY_GROUP_MAX_KEYS && nrecs > 1 &&
-                       nrecs <= 0xffffffffu;
-#else
-    const bool group = false;
-#endif
-    if (group) {
-        // scratch: ctl[2] | counts[nkeys + 1] | perm[n] | (8-byte aligned) grouped descriptors[n]
-        const size_t nb = ks->nkeys + 1, words = ((2 + nb + nrecs + 1) & ~(size_t)1) + nrecs * (sizeof(ptls_mi355x_record_t) / 4);
-        if (ks->group_ev == NULL)
-            HIP_TRY(hipEventCreateWithFlags(&ks->group_ev, hipEventDisableTiming));
-        if (words > ks->group_cap) {
-            HIP_TRY(hipEventSynchronize(ks->group_ev));
-            (void)hipFree(ks->d_group);
-            ks->d_group = NULL;
-            ks->group_cap = 0;
-            HIP_TRY(hipMalloc((void **)&ks->d_group, words * 4));
-            ks->group_cap = words;
-        }
-        HIP_TRY(hipStreamWaitEvent(s, ks->group_ev, 0));  // a batch on another stream may still use the scratch
-        u32 *ctl = ks->d_group, *cnt = ctl + 2, *perm = cnt + nb;
-        HIP_TRY(hipMemsetAsync(ctl, 0, (2 + nb) * 4, s));
-        const unsigned gh = (unsigned)min((nrecs + 255) / 256, (size_t)ks->ncu * 8);
-        key_changes_kernel<<<gh, 256, 0, s>>>(recs, nrecs, ctl);
-        key_hist_kernel<<<gh, 256, 0, s>>>(recs, nrecs, (u32)ks->nkeys, cnt, ctl);
-        key_scan_kernel<<<1, 1024, 0, s>>>(cnt, (u32)nb, nrecs, ctl);
-        ptls_mi355x_record_t *grouped = (ptls_mi355x_record_t *)(ctl + ((2 + nb + nrecs + 1) & ~(size_t)1));
-        key_scatter_kernel<<<gh, 256, 0, s>>>(recs, nrecs, (u32)ks->nkeys, cnt, perm, grouped, ctl);
-        a.grouped = grouped;
-        a.perm = perm;
-        a.perm_on = ctl + 1;
-    }
-#define CHUNKED_LAUNCH(nr, op, frame) gcm_chunked_kernel<nr, op, frame><<<(unsigned)grid, ENGINE_WG, CLDS_ALLOC, s>>>(a)
-    if (frame == 1) {
-        if (ks->nr == 10) {
-            if (open)
-                CHUNKED_LAUNCH(10, true, 1);
-            else
-                CHUNKED_LAUNCH(10, false, 1);
-        } else {
-            if (open)
-                CHUNKED_LAUNCH(14, true, 1);
-            else
-                CHUNKED_LAUNCH(14, false, 1);
-        }
-    } else if (frame == 2) {
-        if (ks->nr == 10) {
-            if (open)
-                CHUNKED_LAUNCH(10, true, 2);
-            else
-                CHUNKED_LAUNCH(10, false, 2);
-        } else {
-            if (open)
-                CHUNKED_LAUNCH(14, true, 2);
-            else
-                CHUNKED_LAUNCH(14, false, 2);
-        }
-    } else if (use_chunked(ks)) {
-        if (ks->nr == 10) {
-            if (open)
-                CHUNKED_LAUNCH(10, true, 0);
-            else
-                CHUNKED_LAUNCH(10, false, 0);
-        } else {
-            if (open)
-                CHUNKED_LAUNCH(14, true, 0);
-            else
-                CHUNKED_LAUNCH(14, false, 0);
-        }
-    } else if (ks->nr == 10) {
+#define CHUNKED_LAUNCH(nr_, op, frame_) gcm_chunked_kernel<nr_, op, frame_><<<(unsigned)grid, ENGINE_WG, CLDS_ALLOC, s>>>(a)
+#define CHUNKED_BY_KEY(frame_)                                                                                          \
+    do {                                                                                                                \
+        if (nr == 10) {                                                                                                 \
+            if (open)                                                                                                   \
+                CHUNKED_LAUNCH(10, true, frame_);                                                                       \
+            else                                                                                                        \
+                CHUNKED_LAUNCH(10, false, frame_);                                                                      \
+        } else {                                                                                                        \
+            if (open)                                                                                                   \
+                CHUNKED_LAUNCH(14, true, frame_);                                                                       \
+            else                                                                                                        \
+                CHUNKED_LAUNCH(14, false, frame_);                                                                      \
+        }                                                                                                               \
+    } while (0)
+    if (frame == 1)
+        CHUNKED_BY_KEY(1);
+    else if (frame == 2)
+        CHUNKED_BY_KEY(2);
+    else if (use_chunked(schedule))
+        CHUNKED_BY_KEY(0);
+    else if (nr == 10) {
         if (open)
             gcm_batch_kernel<10, true><<<(unsigned)grid, ENGINE_WG, LDS_ALLOC, s>>>(a);
         else
@@ -431,11 +685,100 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
         else
             gcm_batch_kernel<14, false><<<(unsigned)grid, ENGINE_WG, LDS_ALLOC, s>>>(a);
     }
+#undef CHUNKED_BY_KEY
+#undef CHUNKED_LAUNCH
     HIP_TRY(hipGetLastError());
-    if (group)
-        HIP_TRY(hipEventRecord(ks->group_ev, s));
     return 0;
 }
+
+// A batch call on a keyset: waits for the keyset's setup, groups an ungrouped many-key batch by key on the device, launches,
+// and records the use (teardown and rekey are ordered after it).
+static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
+                        const void *aad, void *out, uint8_t *ok, void *stream, int frame = 0)
+{
+    if (ks == NULL || (nrecs != 0 && (recs == NULL || in == NULL || out == NULL || (open && ok == NULL))))
+        return fail("%s", "batch: invalid arguments");
+    if (nrecs == 0)
+        return 0;
+    DeviceScope scope(ks->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (wait_ready(ks, s) != 0)
+        return -1;
+    // ungrouped many-key batches: group the records by key on the device first (see key_hist_kernel)
+#ifndef KEY_GROUP_DISABLE
+    const bool group = use_chunked(ks->schedule) && ks->nkeys > 1 && ks->nkeys <= KEY_GROUP_MAX_KEYS && nrecs > 1 &&
+                       nrecs <= 0xffffffffu;
+#else
+    const bool group = false;
+#endif
+    int ret;
+    if (group) {
+        std::lock_guard<std::mutex> lk(ks->mu);
+        // scratch: ctl[2] | counts[nkeys + 1] | perm[n] | (8-byte aligned) grouped descriptors[n]
+        const size_t nb = ks->nkeys + 1, words = ((2 + nb + nrecs + 1) & ~(size_t)1) + nrecs * (sizeof(ptls_mi355x_record_t) / 4);
+        if (ks->group_ev == NULL)
+            HIP_TRY(hipEventCreateWithFlags(&ks->group_ev, hipEventDisableTiming));
+        HIP_TRY(hipStreamWaitEvent(s, ks->group_ev, 0));  // a batch on another stream may still use the scratch
+        if (words > ks->group_cap) {  // grown in stream order on this stream (no device-wide free)
+            if (ks->d_group != NULL)
+                HIP_TRY(hipFreeAsync(ks->d_group, s));
+            ks->d_group = NULL;
+            ks->group_cap = 0;
+            HIP_TRY(hipMallocAsync((void **)&ks->d_group, words * 4, s));
+            ks->group_cap = words;
+        }
+        u32 *ctl = ks->d_group, *cnt = ctl + 2, *perm = cnt + nb;
+        HIP_TRY(hipMemsetAsync(ctl, 0, (2 + nb) * 4, s));
+        const unsigned gh = (unsigned)min((nrecs + 255) / 256, (size_t)ks->ds->ncu * 8);
+        key_changes_kernel<<<gh, 256, 0, s>>>(recs, nrecs, ctl);
+        key_hist_kernel<<<gh, 256, 0, s>>>(recs, nrecs, (u32)ks->nkeys, cnt, ctl);
+        key_scan_kernel<<<1, 1024, 0, s>>>(cnt, (u32)nb, nrecs, ctl);
+        ptls_mi355x_record_t *grouped = (ptls_mi355x_record_t *)(ctl + ((2 + nb + nrecs + 1) & ~(size_t)1));
+        key_scatter_kernel<<<gh, 256, 0, s>>>(recs, nrecs, (u32)ks->nkeys, cnt, perm, grouped, ctl);
+        ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, open, recs, nrecs, in, aad, out, ok, s, frame,
+                         CHUNK_LOG2, grouped, perm, ctl + 1);
+        if (ret == 0)
+            HIP_TRY(hipEventRecord(ks->group_ev, s));
+    } else {
+        ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, open, recs, nrecs, in, aad, out, ok, s,
+                         frame, CHUNK_LOG2);
+    }
+    if (ret != 0)
+        return -1;
+    return note_use(ks, s);
+}
+
+static unsigned aux_grid(size_t n, int ncu)
+{
+    u64 grid = (n + 255) / 256;
+    return (unsigned)(grid > (u64)ncu * 4 ? (u64)ncu * 4 : grid);
+}
+
+static int launch_ecb(const KeyEntry *keys, u32 nkeys, int nr, int ncu, const uint32_t *key_idx, const void *in, void *out,
+                      size_t nblocks, hipStream_t s)
+{
+    if (nr == 10)
+        ecb_kernel<10><<<aux_grid(nblocks, ncu), 256, LDS_AES_BYTES, s>>>(keys, nkeys, key_idx, (const uint8_t *)in, (uint8_t *)out,
+                                                                          nblocks);
+    else
+        ecb_kernel<14><<<aux_grid(nblocks, ncu), 256, LDS_AES_BYTES, s>>>(keys, nkeys, key_idx, (const uint8_t *)in, (uint8_t *)out,
+                                                                          nblocks);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+static int launch_hp(const KeyEntry *keys, u32 nkeys, int nr, int ncu, const ptls_mi355x_hp_t *hp, size_t n, const void *base,
+                     void *masks, hipStream_t s)
+{
+    if (nr == 10)
+        hp_kernel<10><<<aux_grid(n, ncu), 256, LDS_AES_BYTES, s>>>(keys, nkeys, hp, (const uint8_t *)base, (uint8_t *)masks, n);
+    else
+        hp_kernel<14><<<aux_grid(n, ncu), 256, LDS_AES_BYTES, s>>>(keys, nkeys, hp, (const uint8_t *)base, (uint8_t *)masks, n);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+extern "C" {
 
 int ptls_mi355x_seal_batch(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
                            const void *aad, void *out, void *stream)
@@ -456,18 +799,11 @@ int ptls_mi355x_ecb_batch(ptls_mi355x_keyset_t *ks, const uint32_t *key_idx, con
         return fail("%s", "ecb: invalid arguments");
     if (nblocks == 0)
         return 0;
-    u64 grid = (nblocks + 255) / 256;
-    if (grid > (u64)ks->ncu * 4)
-        grid = (u64)ks->ncu * 4;
+    DeviceScope scope(ks->device);
     hipStream_t s = (hipStream_t)stream;
-    if (ks->nr == 10)
-        ecb_kernel<10><<<(unsigned)grid, 256, LDS_AES_BYTES, s>>>(ks->d_keys, (u32)ks->nkeys, key_idx, (const uint8_t *)in,
-                                                                  (uint8_t *)out, nblocks);
-    else
-        ecb_kernel<14><<<(unsigned)grid, 256, LDS_AES_BYTES, s>>>(ks->d_keys, (u32)ks->nkeys, key_idx, (const uint8_t *)in,
-                                                                  (uint8_t *)out, nblocks);
-    HIP_TRY(hipGetLastError());
-    return 0;
+    if (wait_ready(ks, s) != 0 || launch_ecb(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, key_idx, in, out, nblocks, s) != 0)
+        return -1;
+    return note_use(ks, s);
 }
 
 int ptls_mi355x_seal_tls_records(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
@@ -483,11 +819,9 @@ int ptls_mi355x_open_tls_records(ptls_mi355x_keyset_t *ks, const ptls_mi355x_rec
         return -1;
     if (nrecs == 0)
         return 0;
-    u64 grid = (nrecs + 255) / 256;
-    if (grid > (u64)ks->ncu * 4)
-        grid = (u64)ks->ncu * 4;
-    tls_unpad_kernel<<<(unsigned)grid, 256, 0, (hipStream_t)stream>>>(recs, nrecs, (const uint8_t *)in, (const uint8_t *)out,
-                                                                       ok, results);
+    DeviceScope scope(ks->device);
+    tls_unpad_kernel<<<aux_grid(nrecs, ks->ds->ncu), 256, 0, (hipStream_t)stream>>>(recs, nrecs, (const uint8_t *)in,
+                                                                                     (const uint8_t *)out, ok, results);
     HIP_TRY(hipGetLastError());
     return 0;
 }
@@ -505,10 +839,9 @@ int ptls_mi355x_open_tls12_records(ptls_mi355x_keyset_t *ks, const ptls_mi355x_r
         return -1;
     if (nrecs == 0)
         return 0;
-    u64 grid = (nrecs + 255) / 256;
-    if (grid > (u64)ks->ncu * 4)
-        grid = (u64)ks->ncu * 4;
-    tls12_check_kernel<<<(unsigned)grid, 256, 0, (hipStream_t)stream>>>(recs, nrecs, (const uint8_t *)in, ok, results);
+    DeviceScope scope(ks->device);
+    tls12_check_kernel<<<aux_grid(nrecs, ks->ds->ncu), 256, 0, (hipStream_t)stream>>>(recs, nrecs, (const uint8_t *)in, ok,
+                                                                                       results);
     HIP_TRY(hipGetLastError());
     return 0;
 }
@@ -520,18 +853,11 @@ int ptls_mi355x_hp_mask_batch(ptls_mi355x_keyset_t *hp_ks, const ptls_mi355x_hp_
         return fail("%s", "hp_mask: invalid arguments");
     if (n == 0)
         return 0;
-    u64 grid = (n + 255) / 256;
-    if (grid > (u64)hp_ks->ncu * 4)
-        grid = (u64)hp_ks->ncu * 4;
+    DeviceScope scope(hp_ks->device);
     hipStream_t s = (hipStream_t)stream;
-    if (hp_ks->nr == 10)
-        hp_kernel<10><<<(unsigned)grid, 256, LDS_AES_BYTES, s>>>(hp_ks->d_keys, (u32)hp_ks->nkeys, hp, (const uint8_t *)base,
-                                                                 (uint8_t *)masks, n);
-    else
-        hp_kernel<14><<<(unsigned)grid, 256, LDS_AES_BYTES, s>>>(hp_ks->d_keys, (u32)hp_ks->nkeys, hp, (const uint8_t *)base,
-                                                                 (uint8_t *)masks, n);
-    HIP_TRY(hipGetLastError());
-    return 0;
+    if (wait_ready(hp_ks, s) != 0 || launch_hp(hp_ks->d_keys, (u32)hp_ks->nkeys, hp_ks->nr, hp_ks->ds->ncu, hp, n, base, masks, s) != 0)
+        return -1;
+    return note_use(hp_ks, s);
 }
 
 int ptls_mi355x_seal_batch_hp(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
@@ -554,96 +880,154 @@ int ptls_mi355x_quiclb_batch(ptls_mi355x_keyset_t *ks, const ptls_mi355x_cid_t *
         return fail("%s", "quiclb: the QUIC-LB cipher is keyed with AES-128 (PTLS_QUICLB_KEY_SIZE)");
     if (n == 0)
         return 0;
-    u64 grid = (n + 255) / 256;
-    if (grid > (u64)ks->ncu * 4)
-        grid = (u64)ks->ncu * 4;
-    quiclb_kernel<10><<<(unsigned)grid, 256, LDS_AES_BYTES, (hipStream_t)stream>>>(ks->d_keys, (u32)ks->nkeys, cids,
-                                                                                    (const uint8_t *)in, (uint8_t *)out, n);
+    DeviceScope scope(ks->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (wait_ready(ks, s) != 0)
+        return -1;
+    quiclb_kernel<10><<<aux_grid(n, ks->ds->ncu), 256, LDS_AES_BYTES, s>>>(ks->d_keys, (u32)ks->nkeys, cids, (const uint8_t *)in,
+                                                                            (uint8_t *)out, n);
     HIP_TRY(hipGetLastError());
-    return 0;
+    return note_use(ks, s);
 }
 
-int ptls_mi355x_quiclb_transform(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const void *input, size_t len, int encrypt)
-{
-    if (ks == NULL || key_idx >= ks->nkeys || output == NULL || input == NULL || len < PTLS_MI355X_QUICLB_MIN_LEN ||
-        len > PTLS_MI355X_QUICLB_MAX_LEN)
-        return fail("%s", "quiclb_transform: invalid arguments");
-    if (stage_reserve(ks, 96) != 0)
-        return -1;
-    // staging: [0, 32) CID in, [32, 56) descriptor | [64, 96) CID out
-    const ptls_mi355x_cid_t c = {0, 64, (uint32_t)key_idx, (uint8_t)len, (uint8_t)(encrypt != 0), 0};
-    memcpy(ks->h_stage, input, len);
-    memcpy(ks->h_stage + 32, &c, sizeof(c));
-    uint8_t *d = stage_dev(ks);
-    if (stage_roundtrip(ks, d, 64, 64, 32, [&] {
-            return ptls_mi355x_quiclb_batch(ks, (const ptls_mi355x_cid_t *)(d + 32), 1, d, d, ks->stream);
-        }) != 0)
-        return -1;
-    memcpy(output, ks->h_stage + 64, len);
-    return 0;
-}
+}  // extern "C"
 
-int ptls_mi355x_encrypt_block(ptls_mi355x_keyset_t *ks, size_t key_idx, void *out, const void *in)
-{
-    if (ks == NULL || key_idx >= ks->nkeys || out == NULL || in == NULL)
-        return fail("%s", "encrypt_block: invalid arguments");
-    if (stage_reserve(ks, 64) != 0)
-        return -1;
-    // staging: [0, 16) block in, [16, 20) key index | [32, 48) block out
-    const u32 idx = (u32)key_idx;
-    memcpy(ks->h_stage, in, 16);
-    memcpy(ks->h_stage + 16, &idx, 4);
-    uint8_t *d = stage_dev(ks);
-    if (stage_roundtrip(ks, d, 32, 32, 16, [&] {
-            return ptls_mi355x_ecb_batch(ks, (const uint32_t *)(d + 16), d, d + 32, 1, ks->stream);
-        }) != 0)
-        return -1;
-    memcpy(out, ks->h_stage + 32, 16);
-    return 0;
-}
+// ---- the synchronous host-buffer helpers (the per-record picotls path)
+//
+// One call = a staging buffer and its stream from the device pool, a host copy of the inputs into it, launches whose
+// kernels read and write the pinned buffer in place over PCIe (or, where it cannot be mapped, an H2D copy before and a
+// D2H copy after), a wait for that stream only, a host copy of the results, and the staged bytes cleared.
+// Measured against copying (tools/latency.py, interleaved): 16 B 29 -> 26 us, 1200 B 31 -> 29, 16 KiB 52 -> 38,
+// 4 MiB 1.70 -> 1.58 ms.
+struct StageCall {
+    DeviceState *ds;
+    Stager *st = nullptr;
+    size_t total = 0;
+    StageCall(DeviceState *d) : ds(d) {}
+    ~StageCall()
+    {
+        if (st != nullptr) {
+            memset(st->h, 0, total);  // staged plaintext and keystream-derived bytes do not outlive the call
+            stager_put(ds, st);
+        }
+    }
+    int acquire(size_t bytes)
+    {
+        total = bytes;
+        return (st = stager_get(ds, bytes)) != nullptr ? 0 : -1;
+    }
+    uint8_t *host() const { return st->h; }
+    uint8_t *dev() const { return st->h_dev != nullptr ? st->h_dev : st->d; }
+    hipStream_t stream() const { return st->stream; }
+    // runs launch() on the staged buffer: H2D of [0, up) before and D2H of [up, total) after on the copy path; then waits
+    template <typename Launch>
+    int roundtrip(size_t up, Launch launch)
+    {
+        const bool copy = st->h_dev == nullptr;
+        if (copy)
+            HIP_TRY(hipMemcpyAsync(st->d, st->h, up, hipMemcpyHostToDevice, st->stream));
+        if (launch() != 0)
+            return -1;
+        if (copy)
+            HIP_TRY(hipMemcpyAsync(st->h + up, st->d + up, total - up, hipMemcpyDeviceToHost, st->stream));
+        HIP_TRY(hipStreamSynchronize(st->stream));
+        return 0;
+    }
+};
 
-// single record on host buffers: a batch of one through the keyset's staging buffers
-static int single(ptls_mi355x_keyset_t *ks, size_t key_idx, bool open, void *output, const void *input, size_t len, uint64_t seq,
-                  const void *aad, size_t aadlen, int *verified)
+// after a synchronous call on `ks` completed on a stager stream, its setup is complete too
+static void seen_ready(ptls_mi355x_keyset_t *ks) { ks->ready_seen.store(true, std::memory_order_release); }
+
+// one record on host buffers (input as iovecs), optionally with the header-protection mask of a sample of the sealed
+// output under hp_ks (fusion's supp, lib/fusion.c:425-430,636-651): a batch of one through a staging buffer
+static int single(ptls_mi355x_keyset_t *ks, size_t key_idx, bool open, void *output, const ptls_mi355x_iovec_t *vec, size_t incnt,
+                  size_t len, uint64_t seq, const void *aad, size_t aadlen, int *verified, ptls_mi355x_keyset_t *hp_ks = NULL,
+                  size_t hp_key_idx = 0, size_t sample_off = 0, void *mask = NULL)
 {
-    if (ks == NULL || key_idx >= ks->nkeys || aadlen > 0xffff || len > PTLS_MI355X_MAX_RECORD_LEN)
+    if (ks == NULL || key_idx >= ks->nkeys || (aadlen != 0 && aad == NULL) || (len != 0 && output == NULL))
         return fail("%s", "single: invalid arguments");
+    if (len > PTLS_MI355X_MAX_RECORD_LEN || aadlen > PTLS_MI355X_MAX_AAD_LEN)
+        return fail("%s", "single: record or AAD longer than PTLS_MI355X_MAX_RECORD_LEN / PTLS_MI355X_MAX_AAD_LEN");
+    if (hp_ks != NULL && (hp_key_idx >= hp_ks->nkeys || hp_ks->device != ks->device || sample_off + 16 > len + 16))
+        return fail("%s", "single: invalid header-protection arguments");
+    DeviceScope scope(ks->device);
     const size_t inbytes = len + (open ? 16 : 0), outbytes = len + (open ? 0 : 16);
-    // staging: [in | aad | descriptor] goes up, [out | ok] comes back
+    // staging: [in | aad | descriptor | hp entry] goes up, [out | ok | mask] comes back
     const size_t off_in = 0, off_aad = (inbytes + 15) & ~(size_t)15, off_rec = off_aad + ((aadlen + 15) & ~(size_t)15),
-                 off_out = off_rec + 64, off_ok = off_out + ((outbytes + 15) & ~(size_t)15), total = off_ok + 16;
-    if (stage_reserve(ks, total) != 0)
+                 off_hp = off_rec + 48, off_out = off_hp + 16, off_ok = off_out + ((outbytes + 15) & ~(size_t)15),
+                 off_mask = off_ok + 16, total = off_mask + 16;
+    StageCall call(ks->ds);
+    if (call.acquire(total) != 0)
         return -1;
-    const ptls_mi355x_record_t r = {0, 0, seq, 0, (u32)len, 0, (uint16_t)aadlen, 0};  // offsets relative to the arenas below
-    ptls_mi355x_keyset_t view = *ks;
-    view.d_keys = ks->d_keys + key_idx;
-    view.nkeys = 1;
-    uint8_t *h = ks->h_stage, *d = stage_dev(ks);
-    if (inbytes != 0)
-        memcpy(h + off_in, input, inbytes);
+    const ptls_mi355x_record_t r = {0, 0, seq, 0, (u32)len, 0, (uint16_t)aadlen, (uint16_t)(aadlen >> 16)};
+    uint8_t *h = call.host(), *d = call.dev();
+    for (size_t i = 0, off = 0; i < incnt; off += vec[i].len, ++i)
+        if (vec[i].len != 0)
+            memcpy(h + off_in + off, vec[i].base, vec[i].len);
     if (aadlen != 0)
         memcpy(h + off_aad, aad, aadlen);
     memcpy(h + off_rec, &r, sizeof(r));
+    if (hp_ks != NULL) {
+        const ptls_mi355x_hp_t e = {sample_off, 0, 0};  // key 0 of the one-entry view hp_ks->d_keys + hp_key_idx
+        memcpy(h + off_hp, &e, sizeof(e));
+    }
     // one record on one workgroup: shorter units put more of its waves to work (a unit step costs a lone wave ~2 us of
     // latency, a unit combine ~0.15 us); steps / 2^k units balance the two
     const size_t steps = ((aadlen + 15) / 16 + (len + 15) / 16 + 1 + ENGINE_G - 1) / ENGINE_G;
     const u32 unit_log2 = steps <= 24 ? 0 : steps <= 96 ? 1 : steps <= 400 ? 2 : steps <= 1600 ? 3 : CHUNK_LOG2;
-    if (stage_roundtrip(ks, d, off_out, off_out, total - off_out, [&] {
-            return launch_batch(&view, open, (const ptls_mi355x_record_t *)(d + off_rec), 1, d + off_in, d + off_aad,
-                                d + off_out, d + off_ok, ks->stream, 0, unit_log2 < CHUNK_LOG2 ? unit_log2 : CHUNK_LOG2);
+    const hipStream_t s = call.stream();
+    if (wait_ready(ks, s) != 0 || (hp_ks != NULL && wait_ready(hp_ks, s) != 0))
+        return -1;
+    if (call.roundtrip(off_out, [&] {
+            if (launch_gcm(ks->d_keys + key_idx, 1, ks->nr, ks->ds->ncu, ks->schedule, open, (const ptls_mi355x_record_t *)(d + off_rec),
+                           1, d + off_in, d + off_aad, d + off_out, d + off_ok, s, 0, unit_log2 < CHUNK_LOG2 ? unit_log2 : CHUNK_LOG2) != 0)
+                return -1;
+            return hp_ks == NULL ? 0
+                                 : launch_hp(hp_ks->d_keys + hp_key_idx, 1, hp_ks->nr, hp_ks->ds->ncu,
+                                             (const ptls_mi355x_hp_t *)(d + off_hp), 1, d + off_out, d + off_mask, s);
         }) != 0)
         return -1;
+    seen_ready(ks);
+    if (hp_ks != NULL)
+        seen_ready(hp_ks);
     if (outbytes != 0)
         memcpy(output, h + off_out, outbytes);
     if (open)
         *verified = h[off_ok];
+    if (hp_ks != NULL)
+        memcpy(mask, h + off_mask, 16);
     return 0;
 }
+
+extern "C" {
 
 int ptls_mi355x_encrypt(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const void *input, size_t inlen, uint64_t seq,
                         const void *aad, size_t aadlen)
 {
-    return single(ks, key_idx, false, output, input, inlen, seq, aad, aadlen, NULL);
+    const ptls_mi355x_iovec_t v = {input, inlen};
+    return single(ks, key_idx, false, output, &v, 1, inlen, seq, aad, aadlen, NULL);
+}
+
+int ptls_mi355x_encrypt_v(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const ptls_mi355x_iovec_t *input, size_t incnt,
+                          uint64_t seq, const void *aad, size_t aadlen)
+{
+    size_t len = 0;
+    for (size_t i = 0; i < incnt; ++i) {
+        if (input[i].len != 0 && input[i].base == NULL)
+            return fail("%s", "encrypt_v: invalid iovec");
+        len += input[i].len;
+    }
+    return single(ks, key_idx, false, output, input, incnt, len, seq, aad, aadlen, NULL);
+}
+
+int ptls_mi355x_encrypt_s(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const void *input, size_t inlen, uint64_t seq,
+                          const void *aad, size_t aadlen, ptls_mi355x_keyset_t *hp_ks, size_t hp_key_idx, size_t sample_off,
+                          void *mask)
+{
+    if (hp_ks == NULL || mask == NULL)
+        return fail("%s", "encrypt_s: invalid arguments");
+    const ptls_mi355x_iovec_t v = {input, inlen};
+    return single(ks, key_idx, false, output, &v, 1, inlen, seq, aad, aadlen, NULL, hp_ks, hp_key_idx, sample_off, mask);
 }
 
 size_t ptls_mi355x_decrypt(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const void *input, size_t inlen, uint64_t seq,
@@ -652,9 +1036,56 @@ size_t ptls_mi355x_decrypt(ptls_mi355x_keyset_t *ks, size_t key_idx, void *outpu
     if (inlen < 16)
         return SIZE_MAX;
     int verified = 0;
-    if (single(ks, key_idx, true, output, input, inlen - 16, seq, aad, aadlen, &verified) != 0)
+    const ptls_mi355x_iovec_t v = {input, inlen};
+    if (single(ks, key_idx, true, output, &v, 1, inlen - 16, seq, aad, aadlen, &verified) != 0)
         return SIZE_MAX;
     return verified ? inlen - 16 : SIZE_MAX;
+}
+
+int ptls_mi355x_quiclb_transform(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const void *input, size_t len, int encrypt)
+{
+    if (ks == NULL || key_idx >= ks->nkeys || output == NULL || input == NULL || len < PTLS_MI355X_QUICLB_MIN_LEN ||
+        len > PTLS_MI355X_QUICLB_MAX_LEN || ks->key_size != 16)
+        return fail("%s", "quiclb_transform: invalid arguments");
+    DeviceScope scope(ks->device);
+    StageCall call(ks->ds);
+    // staging: [0, 32) CID in, [32, 56) descriptor | [64, 96) CID out
+    if (call.acquire(96) != 0)
+        return -1;
+    const ptls_mi355x_cid_t c = {0, 64, 0, (uint8_t)len, (uint8_t)(encrypt != 0), 0};
+    memcpy(call.host(), input, len);
+    memcpy(call.host() + 32, &c, sizeof(c));
+    uint8_t *d = call.dev();
+    const hipStream_t s = call.stream();
+    if (wait_ready(ks, s) != 0 || call.roundtrip(64, [&] {
+            quiclb_kernel<10><<<1, 256, LDS_AES_BYTES, s>>>(ks->d_keys + key_idx, 1, (const ptls_mi355x_cid_t *)(d + 32), d, d, 1);
+            HIP_TRY(hipGetLastError());
+            return 0;
+        }) != 0)
+        return -1;
+    seen_ready(ks);
+    memcpy(output, call.host() + 64, len);
+    return 0;
+}
+
+int ptls_mi355x_encrypt_block(ptls_mi355x_keyset_t *ks, size_t key_idx, void *out, const void *in)
+{
+    if (ks == NULL || key_idx >= ks->nkeys || out == NULL || in == NULL)
+        return fail("%s", "encrypt_block: invalid arguments");
+    DeviceScope scope(ks->device);
+    StageCall call(ks->ds);
+    // staging: [0, 16) block in | [32, 48) block out
+    if (call.acquire(64) != 0)
+        return -1;
+    memcpy(call.host(), in, 16);
+    uint8_t *d = call.dev();
+    const hipStream_t s = call.stream();
+    if (wait_ready(ks, s) != 0 ||
+        call.roundtrip(32, [&] { return launch_ecb(ks->d_keys + key_idx, 1, ks->nr, ks->ds->ncu, NULL, d, d + 32, 1, s); }) != 0)
+        return -1;
+    seen_ready(ks);
+    memcpy(out, call.host() + 32, 16);
+    return 0;
 }
 
 }  // extern "C"

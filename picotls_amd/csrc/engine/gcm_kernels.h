@@ -12,12 +12,15 @@ __device__ __forceinline__ u32 unit_mul(u32 steps, u32 log2)
     return nc > CHUNK_MAX_UNITS ? (nc + CHUNK_MAX_UNITS - 1) / CHUNK_MAX_UNITS : 1u;
 }
 
-// Descriptors whose len exceeds PTLS_MI355X_MAX_RECORD_LEN or whose key_idx is not below the keyset size are rejected
-// as a whole: nothing is written for them and an open reports ok = 0, so a corrupt length cannot make the kernel address
-// memory far past the record's offsets. (Multi-key batches also reject invalid keys per key run, before any table build.)
+// Descriptors whose len exceeds PTLS_MI355X_MAX_RECORD_LEN, whose AAD exceeds PTLS_MI355X_MAX_AAD_LEN or whose key_idx
+// is not below the keyset size are rejected as a whole: nothing is written for them and an open reports ok = 0, so a
+// corrupt length cannot make the kernel address memory far past the record's offsets. (Multi-key batches also reject
+// invalid keys per key run, before any table build.)
+template <int FRAME = 0>
 __device__ __forceinline__ bool record_ok(const BatchArgs &args, const ptls_mi355x_record_t &r)
 {
-    return r.len <= PTLS_MI355X_MAX_RECORD_LEN && r.key_idx < args.nkeys;
+    return r.len <= PTLS_MI355X_MAX_RECORD_LEN && gcm_aad_len<false, FRAME>(r) <= PTLS_MI355X_MAX_AAD_LEN &&
+           r.key_idx < args.nkeys;
 }
 
 // Seals / opens one whole record per G-lane group.
@@ -183,8 +186,8 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
         if (t < lim) {
             ptls_mi355x_record_t r = recs[p + t];
             other = args.multi_key && r.key_idx != key;
-            if (!record_ok(args, r))  // rejected: one empty unit (see the unit loop)
-                r.len = 0, r.aad_len = 0;
+            if (!record_ok<FRAME>(args, r))  // rejected: one empty unit (see the unit loop)
+                r.len = 0, r.aad_len = 0, r.flags = 0;
             steps[q] = gcm_steps<OPEN, FRAME>(r);
             // front-unit size bucket: 0 = a record too long for CHUNK_MAX_UNITS units (it takes units of a multiple
             // length, unit_mul), else ustep + 1 - size of the record's first unit (1 = a full unit, ustep = one step)
@@ -426,9 +429,9 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             if (valid)
                 r = recs[pos + ri];
             const u64 rid = OPEN && valid ? ok_at(pos + ri) : pos + ri;  // the record's batch index (ok byte)
-            const bool live = valid && record_ok(args, r);
+            const bool live = valid && record_ok<FRAME>(args, r);
             if (valid && !live) {  // rejected descriptor: the scan gave it one unit; nothing is written
-                r.len = 0, r.aad_len = 0;
+                r.len = 0, r.aad_len = 0, r.flags = 0;
                 if (OPEN && j == 0)
                     args.ok[rid] = 0;
             }

@@ -5,10 +5,6 @@
 
 // ------------------------------------------------------------------------------------------------ LDS tables
 
-typedef __attribute__((address_space(3))) uint8_t lds_u8;
-typedef __attribute__((address_space(3))) u32 lds_u32;
-typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
-
 // AES T-table: Te0 replicated into banks 0..31 (bytes 0..127 of row n), Te2 = rotl16(Te0) into bytes 128..255
 __device__ void build_aes_tables(lds_u8 *lds)
 {
@@ -30,26 +26,6 @@ __device__ void build_aes_tables(lds_u8 *lds)
                 t[idx] = slot < 32 ? te0 : ((te0 << 16) | (te0 >> 16));
         }
     }
-}
-
-// (b0..b3) *= x^s in GF(2^128), big-endian words (GCM bit order: the MSB of b0 is x^0), 1 <= s <= 32, in closed form:
-// bit i of the s bits shifted out of b3 is x^(127 - i) and comes back as x^(s - 1 - i) * (1 + x + x^2 + x^7), i.e. the
-// shifted-out bits land at the top of b0 ("1") and again 1, 2 and 7 bits further down, the last spilling into b1
-__device__ __forceinline__ void gf_mulxs_be(u32 &b0, u32 &b1, u32 &b2, u32 &b3, u32 s)
-{
-    const u32 top = s == 32 ? b3 : b3 << (32 - s);
-    if (s == 32) {
-        b3 = b2, b2 = b1, b1 = b0, b0 = 0;
-    } else {
-        b3 = __builtin_amdgcn_alignbit(b2, b3, s);
-        b2 = __builtin_amdgcn_alignbit(b1, b2, s);
-        b1 = __builtin_amdgcn_alignbit(b0, b1, s);
-        b0 >>= s;
-    }
-    const u64 v = (u64)top << 32;
-    const u64 r = v ^ (v >> 1) ^ (v >> 2) ^ (v >> 7);
-    b0 ^= (u32)(r >> 32);
-    b1 ^= (u32)r;
 }
 
 // GHASH window tables of one key: table t (element key->h[t]), window p (x^(4p)..x^(4p+3)), entry n (4-bit value,

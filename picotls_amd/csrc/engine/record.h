@@ -81,10 +81,11 @@ __device__ __forceinline__ u32 gcm_text_len(const ptls_mi355x_record_t &r)
 {
     return FRAME == 1 && !OPEN ? r.len + 1 : r.len;
 }
+// unframed records carry bits 16..31 of the AAD length in flags (PTLS_MI355X_RECORD_AAD_LEN)
 template <bool OPEN, int FRAME>
 __device__ __forceinline__ u32 gcm_aad_len(const ptls_mi355x_record_t &r)
 {
-    return FRAME == 1 ? (u32)TLS_HEADER_SIZE : FRAME == 2 ? (u32)TLS12_AAD_SIZE : (u32)r.aad_len;
+    return FRAME == 1 ? (u32)TLS_HEADER_SIZE : FRAME == 2 ? (u32)TLS12_AAD_SIZE : (u32)r.aad_len | (u32)r.flags << 16;
 }
 // bytes in front of the GCM text in the input / output record
 template <bool OPEN, int FRAME>

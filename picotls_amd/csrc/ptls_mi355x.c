@@ -9,12 +9,27 @@
  *   aesgcm_get/set_iv   lib/fusion.c:1173-1187
  *   ctr cipher          lib/fusion.c:1051-1101  (one 16-byte AES-CTR block per init, for QUIC header protection)
  *   quiclb cipher       lib/fusion.c:2186-2233  (QUIC-LB CID encryption, lib/quiclb-impl.h)
- * Unlike fusion, do_encrypt_v (TLS over TCP) is implemented: the iovecs are gathered and sealed as one record.
+ * Unlike fusion, do_encrypt_v (TLS over TCP) is implemented: the iovecs are gathered straight into the staging buffer and
+ * sealed as one record.
+ *
+ * Failure behaviour. picotls' encrypt callbacks cannot report errors (fusion asserts on OOM, lib/fusion.c:1143), so
+ * every engine failure fails closed in every build: a failed seal overwrites the whole output (inlen + 16 bytes) with
+ * zeros, which no peer authenticates and which holds no plaintext even when sealing in place; a cipher that cannot
+ * produce its keystream (CTR / header protection, QUIC-LB) aborts, because any output it could return would leak its
+ * input. Decrypt reports failures as SIZE_MAX, as for a bad tag; ptls_mi355x_last_error() tells them apart.
  */
-#include <assert.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include "picotls/mi355x_picotls.h"
+
+_Static_assert(sizeof(ptls_iovec_t) == sizeof(ptls_mi355x_iovec_t), "ptls_iovec_t and ptls_mi355x_iovec_t share a layout");
+
+static void engine_fatal(const char *what)
+{
+    fprintf(stderr, "picotls MI355X engine: %s failed: %s\n", what, ptls_mi355x_last_error());
+    abort();
+}
 
 struct mi355x_aead_context {
     ptls_aead_context_t super;
@@ -41,16 +56,16 @@ static void ctr_dispose(ptls_cipher_context_t *_ctx)
 static void ctr_init(ptls_cipher_context_t *_ctx, const void *iv)
 {
     struct mi355x_ctr_context *ctx = (struct mi355x_ctr_context *)_ctx;
-    int ret = ptls_mi355x_encrypt_block(ctx->ks, 0, ctx->bits, iv);
-    assert(ret == 0 && "MI355X engine failure");
-    (void)ret;
+    if (ptls_mi355x_encrypt_block(ctx->ks, 0, ctx->bits, iv) != 0)
+        engine_fatal("AES-CTR keystream");
     ctx->is_ready = 1;
 }
 
 static void ctr_transform(ptls_cipher_context_t *_ctx, void *output, const void *input, size_t len)
 {
     struct mi355x_ctr_context *ctx = (struct mi355x_ctr_context *)_ctx;
-    assert(ctx->is_ready && len <= 16 && "CTR transformation is supported once per init, up to 16 bytes");
+    if (!(ctx->is_ready && len <= 16)) /* fusion asserts the same (lib/fusion.c:1065-1073) */
+        engine_fatal("CTR transform (supported once per init, up to 16 bytes)");
     ctx->is_ready = 0;
     const uint8_t *in = input;
     uint8_t *out = output;
@@ -102,18 +117,42 @@ static void aesgcm_set_iv(ptls_aead_context_t *_ctx, const void *iv)
 {
     struct mi355x_aead_context *ctx = (struct mi355x_aead_context *)_ctx;
     memcpy(ctx->static_iv, iv, sizeof(ctx->static_iv));
-    int ret = ptls_mi355x_keyset_set_iv(ctx->ks, 0, iv);
-    assert(ret == 0 && "MI355X engine failure");
-    (void)ret;
+    /* a wrong IV on the device would seal under a nonce the caller did not ask for: nothing safe to return */
+    if (ptls_mi355x_keyset_set_iv(ctx->ks, 0, iv) != 0)
+        engine_fatal("set_iv");
+}
+
+/* a seal that did not happen leaves zeros, never plaintext or a partial result, in the output */
+static void seal_failed(void *output, size_t inlen, ptls_aead_supplementary_encryption_t *supp)
+{
+    memset(output, 0, inlen + PTLS_AESGCM_TAG_SIZE);
+    if (supp != NULL)
+        memset(supp->output, 0, sizeof(supp->output));
+}
+
+static int is_mi355x_ctr(ptls_cipher_context_t *c)
+{
+    return c->algo == &ptls_mi355x_aes128ctr || c->algo == &ptls_mi355x_aes256ctr;
 }
 
 static void aead_do_encrypt(ptls_aead_context_t *_ctx, void *output, const void *input, size_t inlen, uint64_t seq,
                             const void *aad, size_t aadlen, ptls_aead_supplementary_encryption_t *supp)
 {
     struct mi355x_aead_context *ctx = (struct mi355x_aead_context *)_ctx;
-    int ret = ptls_mi355x_encrypt(ctx->ks, 0, output, input, inlen, seq, aad, aadlen);
-    assert(ret == 0 && "MI355X engine failure");
-    (void)ret;
+    if (supp != NULL && is_mi355x_ctr(supp->ctx) && (const uint8_t *)supp->input >= (const uint8_t *)output &&
+        (const uint8_t *)supp->input + 16 <= (const uint8_t *)output + inlen + PTLS_AESGCM_TAG_SIZE) {
+        /* the header-protection mask of a sample inside the sealed output, computed in the seal's round trip (fusion
+         * computes it inside the seal, lib/fusion.c:425-430,636-651) */
+        struct mi355x_ctr_context *hp = (struct mi355x_ctr_context *)supp->ctx;
+        if (ptls_mi355x_encrypt_s(ctx->ks, 0, output, input, inlen, seq, aad, aadlen, hp->ks, 0,
+                                  (size_t)((const uint8_t *)supp->input - (const uint8_t *)output), supp->output) != 0)
+            seal_failed(output, inlen, supp);
+        return;
+    }
+    if (ptls_mi355x_encrypt(ctx->ks, 0, output, input, inlen, seq, aad, aadlen) != 0) {
+        seal_failed(output, inlen, supp);
+        return;
+    }
     if (supp != NULL) {
         /* the sample may point into the freshly written ciphertext, so it is read only now (include/picotls.h:446-449) */
         supp->ctx->do_init(supp->ctx, supp->input);
@@ -125,19 +164,13 @@ static void aead_do_encrypt(ptls_aead_context_t *_ctx, void *output, const void 
 static void aead_do_encrypt_v(ptls_aead_context_t *_ctx, void *output, ptls_iovec_t *input, size_t incnt, uint64_t seq,
                               const void *aad, size_t aadlen)
 {
-    size_t total = 0;
-    for (size_t i = 0; i < incnt; ++i)
-        total += input[i].len;
-    uint8_t *buf = malloc(total + 1);
-    assert(buf != NULL);
-    size_t off = 0;
-    for (size_t i = 0; i < incnt; ++i) {
-        if (input[i].len != 0)
-            memcpy(buf + off, input[i].base, input[i].len);
-        off += input[i].len;
+    struct mi355x_aead_context *ctx = (struct mi355x_aead_context *)_ctx;
+    if (ptls_mi355x_encrypt_v(ctx->ks, 0, output, (const ptls_mi355x_iovec_t *)input, incnt, seq, aad, aadlen) != 0) {
+        size_t total = 0;
+        for (size_t i = 0; i < incnt; ++i)
+            total += input[i].len;
+        seal_failed(output, total, NULL);
     }
-    aead_do_encrypt(_ctx, output, buf, total, seq, aad, aadlen, NULL);
-    free(buf);
 }
 
 static size_t aead_do_decrypt(ptls_aead_context_t *_ctx, void *output, const void *input, size_t inlen, uint64_t seq,
@@ -206,9 +239,8 @@ static void quiclb_transform(ptls_cipher_context_t *_ctx, void *output, const vo
 {
     struct mi355x_quiclb_context *ctx = (struct mi355x_quiclb_context *)_ctx;
     /* the reference asserts PTLS_QUICLB_MIN_BLOCK_SIZE <= len <= PTLS_QUICLB_MAX_BLOCK_SIZE (lib/quiclb-impl.h:127) */
-    int ret = ptls_mi355x_quiclb_transform(ctx->ks, 0, output, input, len, ctx->is_enc);
-    assert(ret == 0 && "QUIC-LB: len out of range or MI355X engine failure");
-    (void)ret;
+    if (ptls_mi355x_quiclb_transform(ctx->ks, 0, output, input, len, ctx->is_enc) != 0)
+        engine_fatal("QUIC-LB transform");
 }
 
 static int quiclb_setup(ptls_cipher_context_t *_ctx, int is_enc, const void *key)

@@ -4,6 +4,7 @@
  * ctx and ctx_peer on different backends; t/fusion.c:385-466 test_generated; t/fusion.c:346-380 gcm_iv96).
  * TAP-like output; exit status 0 iff every check passed.
  */
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -269,12 +270,147 @@ static void tls12_test(ptls_aead_algorithm_t *ours, ptls_aead_algorithm_t *ref, 
     ptls_buffer_dispose(&pb);
 }
 
-int main(void)
+/* Distinct contexts are independent and need no locking (SURVEY 8(b) Threading, lib/picotls.c:6553-6568): threads that
+ * each own their contexts seal and open concurrently, and create and free contexts while the others run, with results
+ * equal to fusion's. Each thread has its own generator and counts its own failures. */
+struct thread_job {
+    int id, iters, failures;
+    ptls_aead_algorithm_t *ours, *ref;
+};
+
+static void *thread_main(void *_j)
+{
+    struct thread_job *j = _j;
+    uint64_t st = 0x9e3779b97f4a7c15ull * (uint64_t)(j->id + 1);
+#define TRND() (st ^= st << 13, st ^= st >> 7, st ^= st << 17, (uint8_t)(st >> 24))
+    uint8_t key[32], iv[12], text[3000], aad[64], a[3016], b[3016], dec[3000];
+    for (int i = 0; i < 32; ++i)
+        key[i] = TRND();
+    for (int i = 0; i < 12; ++i)
+        iv[i] = TRND();
+    /* long-lived contexts of this thread, as a connection's send and receive sides */
+    ptls_aead_context_t *enc = ptls_aead_new_direct(j->ours, 1, key, iv), *dec_ctx = ptls_aead_new_direct(j->ours, 0, key, iv),
+                        *ref = ptls_aead_new_direct(j->ref, 1, key, iv);
+    if (enc == NULL || dec_ctx == NULL || ref == NULL) {
+        j->failures = j->iters;
+        return NULL;
+    }
+    for (int it = 0; it < j->iters; ++it) {
+        size_t len = ((size_t)TRND() << 4 | TRND() >> 4) % sizeof(text), aadlen = TRND() % sizeof(aad);
+        uint64_t seq = (uint64_t)it * 7919 + (uint64_t)j->id;
+        for (size_t i = 0; i < len; ++i)
+            text[i] = TRND();
+        for (size_t i = 0; i < aadlen; ++i)
+            aad[i] = TRND();
+        ptls_aead_encrypt(enc, a, text, len, seq, aad, aadlen);
+        ptls_aead_encrypt(ref, b, text, len, seq, aad, aadlen);
+        if (memcmp(a, b, len + 16) != 0)
+            ++j->failures;
+        if (ptls_aead_decrypt(dec_ctx, dec, a, len + 16, seq, aad, aadlen) != len || memcmp(dec, text, len) != 0)
+            ++j->failures;
+        /* a short-lived context created and freed while the other threads seal and open */
+        if (it % 4 == 0) {
+            uint8_t k2[32], v2[12];
+            for (int i = 0; i < 32; ++i)
+                k2[i] = TRND();
+            for (int i = 0; i < 12; ++i)
+                v2[i] = TRND();
+            ptls_aead_context_t *t1 = ptls_aead_new_direct(j->ours, 1, k2, v2), *t2 = ptls_aead_new_direct(j->ref, 1, k2, v2);
+            if (t1 == NULL || t2 == NULL) {
+                ++j->failures;
+            } else {
+                ptls_aead_encrypt(t1, a, text, len, seq, aad, aadlen);
+                ptls_aead_encrypt(t2, b, text, len, seq, aad, aadlen);
+                if (memcmp(a, b, len + 16) != 0)
+                    ++j->failures;
+            }
+            if (t1 != NULL)
+                ptls_aead_free(t1);
+            if (t2 != NULL)
+                ptls_aead_free(t2);
+        }
+    }
+#undef TRND
+    ptls_aead_free(enc), ptls_aead_free(dec_ctx), ptls_aead_free(ref);
+    return NULL;
+}
+
+static void threads_test(ptls_aead_algorithm_t *ours, ptls_aead_algorithm_t *ref, int nthreads, int iters, const char *what)
+{
+    pthread_t th[16];
+    struct thread_job jobs[16];
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t] = (struct thread_job){t, iters, 0, ours, ref};
+        pthread_create(&th[t], NULL, thread_main, &jobs[t]);
+    }
+    int failures = 0;
+    for (int t = 0; t < nthreads; ++t) {
+        pthread_join(th[t], NULL);
+        failures += jobs[t].failures;
+    }
+    OK(failures == 0, "%s: %d threads x %d records, own contexts, concurrent create/free: %d mismatches", what, nthreads, iters,
+       failures);
+}
+
+/* records and AADs beyond the batch descriptor's 16-bit AAD field and the old 16 MiB record limit, as fusion takes them
+ * (its set_capacity grows the H table, lib/fusion.c:1018-1041, 1141-1145) */
+static void large_test(ptls_aead_algorithm_t *ours, ptls_aead_algorithm_t *ref, size_t len, size_t aadlen, const char *what)
+{
+    uint8_t key[32], iv[12];
+    rnd(key, sizeof(key)), rnd(iv, sizeof(iv));
+    uint8_t *text = malloc(len + 1), *aad = malloc(aadlen + 1), *a = malloc(len + 16), *b = malloc(len + 16), *dec = malloc(len + 1);
+    rnd(text, len), rnd(aad, aadlen);
+    ptls_aead_context_t *e = ptls_aead_new_direct(ours, 1, key, iv), *r = ptls_aead_new_direct(ref, 1, key, iv),
+                        *d = ptls_aead_new_direct(ours, 0, key, iv);
+    ptls_aead_encrypt(e, a, text, len, 77, aad, aadlen);
+    ptls_aead_encrypt(r, b, text, len, 77, aad, aadlen);
+    OK(memcmp(a, b, len + 16) == 0, "%s: sealed equal to fusion (len=%zu aad=%zu)", what, len, aadlen);
+    OK(ptls_aead_decrypt(d, dec, b, len + 16, 77, aad, aadlen) == len && memcmp(dec, text, len) == 0, "%s: opens fusion's", what);
+    b[len / 2] ^= 1;
+    OK(ptls_aead_decrypt(d, dec, b, len + 16, 77, aad, aadlen) == SIZE_MAX, "%s: tamper rejected", what);
+    ptls_aead_free(e), ptls_aead_free(r), ptls_aead_free(d);
+    free(text), free(aad), free(a), free(b), free(dec);
+}
+
+/* run as `test_vtable failclosed` with PTLS_MI355X_MAX_STAGE_BYTES=65536: a seal the engine cannot perform leaves zeros
+ * in the output, never the plaintext (sealing in place), and the matching open fails */
+static int failclosed_main(void)
+{
+    uint8_t key[16] = {1}, iv[12] = {2};
+    size_t len = 100000;
+    uint8_t *buf = malloc(len + 16), *zero = calloc(1, len + 16), aad[13] = {3};
+    memset(buf, 0x5a, len);
+    ptls_aead_context_t *e = ptls_aead_new_direct(&ptls_mi355x_aes128gcm, 1, key, iv);
+    OK(e != NULL, "failclosed: context");
+    ptls_aead_encrypt(e, buf, buf, len, 1, aad, sizeof(aad)); /* in place, as QUIC stacks seal */
+    OK(memcmp(buf, zero, len + 16) == 0, "failclosed: output zeroed, plaintext gone");
+    OK(strstr(ptls_mi355x_last_error(), "PTLS_MI355X_MAX_STAGE_BYTES") != NULL, "failclosed: error reported (%s)",
+       ptls_mi355x_last_error());
+    ptls_iovec_t vec[2] = {{buf, len / 2}, {buf + len / 2, len / 2}};
+    memset(buf, 0x5a, len);
+    ptls_aead_encrypt_v(e, buf, vec, 2, 1, aad, sizeof(aad));
+    OK(memcmp(buf, zero, len + 16) == 0, "failclosed: encrypt_v output zeroed");
+    OK(ptls_aead_decrypt(e, buf, buf, len + 16, 1, aad, sizeof(aad)) == SIZE_MAX, "failclosed: decrypt fails");
+    /* small records still work on the same context */
+    uint8_t small[64] = {9}, out[80], ref_out[80];
+    ptls_aead_context_t *r = ptls_aead_new_direct(&ptls_fusion_aes128gcm, 1, key, iv);
+    ptls_aead_encrypt(e, out, small, sizeof(small), 2, aad, sizeof(aad));
+    ptls_aead_encrypt(r, ref_out, small, sizeof(small), 2, aad, sizeof(aad));
+    OK(memcmp(out, ref_out, sizeof(out)) == 0, "failclosed: small record after a failure equals fusion");
+    ptls_aead_free(e), ptls_aead_free(r);
+    free(buf), free(zero);
+    printf("1..%d\n# %d failed\n", ntest, nfail);
+    return nfail == 0 ? 0 : 1;
+}
+
+int main(int argc, char **argv)
 {
     if (!ptls_fusion_is_supported_by_cpu()) {
         printf("1..0 # SKIP fusion not supported by this CPU\n");
         return 0;
     }
+    if (argc > 1 && strcmp(argv[1], "failclosed") == 0)
+        return failclosed_main();
     OK(strcmp(ptls_mi355x_aes128gcm.name, ptls_fusion_aes128gcm.name) == 0 && ptls_mi355x_aes128gcm.key_size == 16 &&
            ptls_mi355x_aes128gcm.iv_size == 12 && ptls_mi355x_aes128gcm.tag_size == 16 &&
            ptls_mi355x_aes128gcm.confidentiality_limit == ptls_fusion_aes128gcm.confidentiality_limit &&
@@ -292,6 +428,11 @@ int main(void)
     quiclb_test();
     tls12_test(&ptls_mi355x_non_temporal_aes128gcm, &ptls_non_temporal_aes128gcm, &ptls_openssl_sha256, "tls12 aes128gcm wire == fusion");
     tls12_test(&ptls_mi355x_non_temporal_aes256gcm, &ptls_non_temporal_aes256gcm, &ptls_openssl_sha384, "tls12 aes256gcm wire == fusion");
+    threads_test(&ptls_mi355x_aes128gcm, &ptls_fusion_aes128gcm, 8, 60, "aes128gcm threads");
+    threads_test(&ptls_mi355x_aes256gcm, &ptls_fusion_aes256gcm, 8, 30, "aes256gcm threads");
+    large_test(&ptls_mi355x_aes128gcm, &ptls_fusion_aes128gcm, 17u << 20, 13, "17 MiB record");
+    large_test(&ptls_mi355x_aes256gcm, &ptls_fusion_aes256gcm, 3000, 70 << 10, "70 KiB AAD");
+    large_test(&ptls_mi355x_aes128gcm, &ptls_fusion_aes128gcm, 1 << 20, (1 << 17) + 3, "1 MiB record, 128 KiB AAD");
     printf("1..%d\n# %d failed\n", ntest, nfail);
     return nfail == 0 ? 0 : 1;
 }

@@ -1,0 +1,266 @@
+"""Context lifecycle, concurrency and the per-record path's edges, through the engine's C ABI, bit-exact vs lib/fusion.c.
+
+  * contexts are independent (SURVEY 8(b) Threading, lib/picotls.c:6553-6568): threads with their own contexts seal and
+    open concurrently while others are created and freed;
+  * teardown is stream-ordered: freeing a keyset right after launching a batch on it leaves that batch intact, and the
+    slab entry it frees is only reused once cleared;
+  * records and AADs beyond the descriptor's 16-bit AAD field (flags carries bits 16..31) and the per-record path's
+    gather (encrypt_v) and fused header protection (encrypt_s);
+  * the batch calls on pinned host arenas for a many-key keyset in random key order and for TLS 1.3 records.
+"""
+import os
+import threading
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import picotls_amd as pa  # noqa: E402
+from oracle import FusionRef  # noqa: E402
+from picotls_amd.records import RecordBatch  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+HAVE_REF = os.path.exists(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
+                                       "libfusion_ref.so"))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def engine():
+    assert torch.cuda.is_available(), "no GPU visible"
+    pa.load_library()
+    assert pa.is_supported(), "engine reports no gfx950 device"
+
+
+@pytest.fixture(scope="module")
+def ref():
+    if not HAVE_REF:
+        pytest.skip("oracle/_ref/libfusion_ref.so not shipped")
+    return FusionRef()
+
+
+def pinned(a):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).pin_memory()
+
+
+def test_threads_with_own_contexts_and_churn(ref):
+    # 8 threads (ctypes drops the GIL inside each engine call): each owns a send and a receive context and, every few
+    # records, creates, uses and frees a short-lived one; everything equals fusion
+    errors = []
+
+    def worker(t):
+        rng = np.random.default_rng(1000 + t)
+        ks_size = 16 if t % 2 == 0 else 32
+        alg = pa.aes128gcm if ks_size == 16 else pa.aes256gcm
+        key, iv = rng.bytes(ks_size), rng.bytes(12)
+        enc, dec = pa.aead_new_direct(alg, True, key, iv), pa.aead_new_direct(alg, False, key, iv)
+        try:
+            for i in range(40):
+                ln, al = int(rng.integers(0, 3000)), int(rng.integers(0, 40))
+                pt, aad, seq = rng.bytes(ln), rng.bytes(al), int(rng.integers(0, 2**62))
+                want = ref.seal(key, iv, seq, aad, pt)
+                if enc.encrypt(pt, seq, aad) != want or dec.decrypt(want, seq, aad) != pt:
+                    errors.append((t, i))
+                if i % 5 == 0:
+                    k2, v2 = rng.bytes(ks_size), rng.bytes(12)
+                    tmp = pa.aead_new_direct(alg, True, k2, v2)
+                    if tmp.encrypt(pt, seq, aad) != ref.seal(k2, v2, seq, aad, pt):
+                        errors.append((t, i, "tmp"))
+                    tmp.free()
+        finally:
+            enc.free()
+            dec.free()
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert errors == []
+
+
+def test_free_right_after_launch_is_ordered(ref):
+    # keyset_free does not wait on the host: it orders the clearing of the key material after the keyset's launches on
+    # every stream. A batch launched on a side stream and freed at once still seals correctly, and keysets made right
+    # after (reusing the device's entry pool) are correct too.
+    rng = np.random.default_rng(77)
+    n = 20000
+    b = RecordBatch.build(np.full(n, 4096), 13, seqs=np.arange(n, dtype=np.uint64))
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(b.aad_bytes), np.uint8)
+    dev = torch.device("cuda:0")
+    d_recs, d_pt, d_aad = (torch.from_numpy(x.view(np.uint8).copy()).to(dev) for x in (b.seal, pt, aad))
+    side = torch.cuda.Stream(dev)
+    outs = []
+    for r in range(3):
+        key, iv = rng.bytes(16), rng.bytes(12)
+        ks = pa.Keyset(key, iv, 16)
+        d_out = torch.zeros(b.sealed_bytes, dtype=torch.uint8, device=dev)
+        side.wait_stream(torch.cuda.current_stream())  # the inputs and the zeroed output are ready
+        pa.seal_batch(ks, d_recs.data_ptr(), n, d_pt.data_ptr(), d_aad.data_ptr(), d_out.data_ptr(), side.cuda_stream)
+        ks.free()  # immediately, with the batch most likely still running
+        outs.append((key, iv, d_out))
+        # a per-record context created now may take a freshly freed entry only after its clearing completed
+        ctx = pa.aead_new_direct(pa.aes128gcm, True, rng.bytes(16), rng.bytes(12))
+        ctx.encrypt(b"x" * 100, 1, b"")
+        ctx.free()
+    side.synchronize()
+    for key, iv, d_out in outs:
+        want = np.zeros(b.sealed_bytes, np.uint8)
+        ref.run_batch(True, np.frombuffer(key, np.uint8), np.frombuffer(iv, np.uint8), 16, b.seal, pt, aad, want, nthreads=8)
+        assert np.array_equal(d_out.cpu().numpy(), want)
+
+
+def test_context_churn_reuses_entries_correctly(ref):
+    # thousands of one-key contexts created and freed in a row (entries come back to the pool after clearing): every
+    # context seals with its own key
+    rng = np.random.default_rng(78)
+    for i in range(3000):
+        key, iv = rng.bytes(16), rng.bytes(12)
+        ctx = pa.aead_new_direct(pa.aes128gcm, True, key, iv)
+        if i % 100 == 0:
+            pt = rng.bytes(int(rng.integers(0, 200)))
+            assert ctx.encrypt(pt, i, b"h") == ref.seal(key, iv, i, b"h", pt), i
+        ctx.free()
+
+
+@pytest.mark.parametrize("aadlen", [65535, 65536, 70 << 10, (1 << 20) + 5])
+def test_large_aad_batch_via_flags(ref, aadlen):
+    # the AAD length's bits 16..31 travel in flags (PTLS_MI355X_RECORD_AAD_LEN); batch seal and open against fusion
+    rng = np.random.default_rng(aadlen)
+    lens = np.array([0, 1, 1500, 16384, 100000])
+    n = len(lens)
+    b = RecordBatch.build(lens, 0, seqs=rng.integers(0, 2**40, n, dtype=np.uint64))
+    recs = b.seal.copy()
+    recs["aad_off"] = np.arange(n) * ((aadlen + 15) // 16 * 16)
+    recs["aad_len"] = aadlen & 0xFFFF
+    recs["flags"] = aadlen >> 16
+    key, iv = rng.bytes(32), rng.bytes(12)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(n * ((aadlen + 15) // 16 * 16)), np.uint8)
+    ks = pa.Keyset(key, iv, 32)
+    from gpu_util import gpu_open, gpu_seal
+
+    sealed = gpu_seal(ks, recs, pt, aad, b.sealed_bytes)
+    for i, r in enumerate(recs):
+        a0 = int(r["aad_off"])
+        want = ref.seal(key, iv, int(r["seq"]), aad[a0:a0 + aadlen].tobytes(),
+                        pt[int(r["in_off"]):int(r["in_off"]) + int(r["len"])].tobytes())
+        assert sealed[int(r["out_off"]):int(r["out_off"]) + int(r["len"]) + 16].tobytes() == want, i
+    orecs = recs.copy()
+    orecs["in_off"], orecs["out_off"] = b.open["in_off"], b.open["out_off"]
+    back, ok = gpu_open(ks, orecs, sealed, aad, b.pt_bytes)
+    assert ok.all()
+    for r in orecs:
+        assert np.array_equal(back[int(r["out_off"]):int(r["out_off"]) + int(r["len"])],
+                              pt[int(r["out_off"]):int(r["out_off"]) + int(r["len"])])
+    ks.free()
+
+
+def test_per_record_large_aad_and_record(ref):
+    rng = np.random.default_rng(79)
+    for key_size, ln, al in [(16, 3000, 70 << 10), (32, 17 << 20, 13), (16, 5, 200000)]:
+        key, iv = rng.bytes(key_size), rng.bytes(12)
+        alg = pa.aes128gcm if key_size == 16 else pa.aes256gcm
+        ctx = pa.aead_new_direct(alg, True, key, iv)
+        pt, aad = rng.bytes(ln), rng.bytes(al)
+        want = ref.seal(key, iv, 9, aad, pt)
+        assert ctx.encrypt(pt, 9, aad) == want
+        assert ctx.decrypt(want, 9, aad) == pt
+        ctx.free()
+
+
+def test_encrypt_v_and_fused_header_protection(ref):
+    rng = np.random.default_rng(80)
+    key, iv, hpkey = rng.bytes(16), rng.bytes(12), rng.bytes(16)
+    ctx = pa.aead_new_direct(pa.aes128gcm, True, key, iv)
+    hp = pa.CtrCipher(hpkey)
+    for parts in ([0], [5, 0, 7], [1] * 40, [16384, 1], [3, 1200, 0, 9]):
+        vecs = [rng.bytes(p) for p in parts]
+        aad = rng.bytes(5)
+        assert ctx.encrypt_v(vecs, 42, aad) == ref.seal(key, iv, 42, aad, b"".join(vecs))
+    for ln in (1, 4, 20, 1200):
+        pt, aad = rng.bytes(ln), rng.bytes(13)
+        sample_off = min(2, ln)  # the sample may reach into the tag
+        sealed, mask = ctx.encrypt_s(pt, 7, aad, hp, sample_off)
+        want, want_mask = ref.seal_with_hp(key, iv, 7, aad, pt, hpkey, sample_off)
+        assert sealed == want and mask == want_mask, ln
+    ctx.free()
+
+
+def test_many_key_random_order_on_pinned_host_arenas(ref):
+    # many-key keyset, records in random key order (device grouping reads the host-resident descriptors), every arena,
+    # the descriptors and the ok bytes in pinned host memory
+    rng = np.random.default_rng(81)
+    n, nkeys = 4000, 333
+    lens = rng.integers(0, 6000, n)
+    key_idx = rng.integers(0, nkeys, n)
+    b = RecordBatch.build(lens, rng.integers(0, 30, n), seqs=rng.integers(0, 2**48, n, dtype=np.uint64), key_idx=key_idx)
+    keys, ivs = np.frombuffer(rng.bytes(nkeys * 16), np.uint8), np.frombuffer(rng.bytes(nkeys * 12), np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(max(b.aad_bytes, 1)), np.uint8)
+    h_seal, h_open, h_pt, h_aad = pinned(b.seal), pinned(b.open), pinned(pt), pinned(aad)
+    h_sealed = torch.zeros(b.sealed_bytes, dtype=torch.uint8).pin_memory()
+    ks = pa.Keyset(keys, ivs, 16)
+    s = torch.cuda.current_stream().cuda_stream
+    pa.seal_batch(ks, h_seal.data_ptr(), n, h_pt.data_ptr(), h_aad.data_ptr(), h_sealed.data_ptr(), s)
+    torch.cuda.synchronize()
+    want = np.zeros(b.sealed_bytes, np.uint8)
+    ref.run_batch(True, keys, ivs, 16, b.seal, pt, aad, want, nthreads=8)
+    assert np.array_equal(h_sealed.numpy(), want)
+    h_back = torch.zeros(b.pt_bytes, dtype=torch.uint8).pin_memory()
+    h_ok = torch.full((n,), 0xAA, dtype=torch.uint8).pin_memory()
+    h_sealed[int(b.seal[17]["out_off"])] ^= 1
+    pa.open_batch(ks, h_open.data_ptr(), n, h_sealed.data_ptr(), h_aad.data_ptr(), h_back.data_ptr(), h_ok.data_ptr(), s)
+    torch.cuda.synchronize()
+    want_ok = np.ones(n, np.uint8)
+    want_ok[17] = 0
+    assert np.array_equal(h_ok.numpy(), want_ok)
+    ks.free()
+
+
+def test_tls_records_on_pinned_host_arenas(ref):
+    # TLS 1.3 framing + the unpad kernel with wire records, plaintext, ok bytes and results in pinned host memory
+    rng = np.random.default_rng(82)
+    n = 500
+    lens = rng.integers(0, 16385, n)
+    b = RecordBatch.build(lens, 0, seqs=np.arange(n, dtype=np.uint64))
+    seal = b.seal.copy()
+    seal["flags"] = 23
+    wire_slot = (lens + 22 + 15) // 16 * 16
+    wire_off = np.concatenate([[0], np.cumsum(wire_slot)[:-1]]).astype(np.uint64)
+    seal["out_off"] = wire_off
+    key, iv = rng.bytes(16), rng.bytes(12)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    h_seal, h_pt = pinned(seal), pinned(pt)
+    h_wire = torch.zeros(int(wire_slot.sum()), dtype=torch.uint8).pin_memory()
+    ks = pa.Keyset(key, iv, 16)
+    s = torch.cuda.current_stream().cuda_stream
+    pa.seal_tls_records(ks, h_seal.data_ptr(), n, h_pt.data_ptr(), h_wire.data_ptr(), s)
+    torch.cuda.synchronize()
+    wire = h_wire.numpy()
+    for i in range(0, n, 37):
+        ln, o = int(lens[i]), int(wire_off[i])
+        inner = pt[int(b.seal[i]["in_off"]):int(b.seal[i]["in_off"]) + ln].tobytes() + b"\x17"
+        hdr = bytes([23, 3, 3, (ln + 17) >> 8, (ln + 17) & 0xFF])
+        assert wire[o:o + 5].tobytes() == hdr
+        assert wire[o + 5:o + 22 + ln].tobytes() == ref.seal(key, iv, i, hdr, inner), i
+    # the opened plaintext of record i is len + 1 bytes (the inner type follows the content): slots of their own
+    back_b = RecordBatch.build(lens + 1, 0)
+    opn = seal.copy()
+    opn["in_off"], opn["out_off"], opn["len"] = wire_off, back_b.seal["in_off"], lens + 1
+    h_open = pinned(opn)
+    h_back = torch.zeros(back_b.pt_bytes, dtype=torch.uint8).pin_memory()
+    h_ok = torch.zeros(n, dtype=torch.uint8).pin_memory()
+    h_res = torch.zeros(n * 8, dtype=torch.uint8).pin_memory()
+    pa.open_tls_records(ks, h_open.data_ptr(), n, h_wire.data_ptr(), h_back.data_ptr(), h_ok.data_ptr(), h_res.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert h_ok.numpy().all()
+    res = h_res.numpy().view(pa.TLS_RESULT_DTYPE)
+    assert np.array_equal(res["plain_len"], lens) and (res["content_type"] == 23).all() and (res["status"] == 0).all()
+    back = h_back.numpy()
+    for i in range(0, n, 41):
+        o, p0, ln = int(back_b.seal[i]["in_off"]), int(b.seal[i]["in_off"]), int(lens[i])
+        assert np.array_equal(back[o:o + ln], pt[p0:p0 + ln])
+    ks.free()

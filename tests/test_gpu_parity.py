@@ -589,6 +589,37 @@ def test_picotls_vtable_pairs():
     assert "not ok" not in r.stdout
 
 
+@pytest.mark.parametrize("copy_path", [False, True])
+def test_picotls_vtable_fail_closed(copy_path):
+    # an engine failure inside ptls_aead_encrypt (here: a record above the staging cap set for this process) leaves
+    # zeros in the output, never the plaintext (sealed in place), and the process keeps working; the same binary also
+    # checks that ptls_mi355x_last_error() names the cause. copy_path: the staging round trip through device memory
+    # (PTLS_MI355X_STAGE_COPY=1) instead of the mapped pinned buffer.
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "_bin", "test_vtable")
+    if not os.path.exists(exe):
+        pytest.skip("tests/c/_bin/test_vtable not built (needs picotls headers at build time)")
+    env = dict(os.environ, PTLS_MI355X_MAX_STAGE_BYTES="65536")
+    if copy_path:
+        env["PTLS_MI355X_STAGE_COPY"] = "1"
+    r = subprocess.run([exe, "failclosed"], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    assert "not ok" not in r.stdout
+
+
+def test_picotls_vtable_pairs_copy_path():
+    # the whole vtable suite with the staging round trip copying through device memory (PTLS_MI355X_STAGE_COPY=1)
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "_bin", "test_vtable")
+    if not os.path.exists(exe):
+        pytest.skip("tests/c/_bin/test_vtable not built (needs picotls headers at build time)")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600, env=dict(os.environ, PTLS_MI355X_STAGE_COPY="1"))
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    assert "not ok" not in r.stdout
+
+
 @pytest.mark.parametrize("key_size", [16, 32])
 def test_per_record_path_every_unit_size_vs_fusion(ref, key_size):
     # the per-record path (ptls_aead_encrypt / decrypt through the vtable = a launch of one record) cuts the record into
@@ -627,11 +658,12 @@ def test_invalid_descriptor_rejected(ref, schedule):
     aad = np.frombuffer(rng.bytes(b.aad_bytes), np.uint8)
     expect = np.zeros(b.sealed_bytes, np.uint8)
     ref.run_batch(True, keys, ivs, 16, b.seal, pt, aad, expect, nthreads=2)
-    bad = [3, 17, 39, 25]
+    bad = [3, 17, 39, 25, 8]
     seal, opn = b.seal.copy(), b.open.copy()
-    for i, v in zip(bad, [(1 << 24) + 1, 0xFFFFFFFF, 0xFFFFFFF0]):
+    for i, v in zip(bad, [(1 << 30) + 1, 0xFFFFFFFF, 0xFFFFFFF0]):  # PTLS_MI355X_MAX_RECORD_LEN = 2^30
         seal[i]["len"] = opn[i]["len"] = v
     seal[25]["key_idx"] = opn[25]["key_idx"] = 5  # a one-key keyset: key 5 does not exist
+    seal[8]["flags"] = opn[8]["flags"] = 0x4001  # AAD length above PTLS_MI355X_MAX_AAD_LEN (bits 16..31 in flags)
     ks = pa.Keyset(keys, ivs, 16)
     ks.set_schedule(schedule)
     sealed = gpu_seal(ks, seal, pt, aad, b.sealed_bytes, out_fill=0xEE)
