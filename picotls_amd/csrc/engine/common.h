@@ -61,6 +61,10 @@ static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 #define ENGINE_FAST_STEP 1         // wave-uniform fast path for steps where every lane holds a full text block
 #endif
 
+#ifndef ALIGN_MIN_STEPS
+#define ALIGN_MIN_STEPS 64         // whole records of this many steps may take one more step to align their stores
+#endif
+
 #define ENGINE_G 8                 // lanes per record
 #ifndef ENGINE_NB
 #define ENGINE_NB 1                // AES-CTR blocks per lane per step (independent chains in flight)

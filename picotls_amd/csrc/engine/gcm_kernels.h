@@ -26,8 +26,7 @@ __device__ __forceinline__ bool record_ok(const BatchArgs &args, const ptls_mi35
 // Seals / opens one whole record per G-lane group.
 template <int NR, bool OPEN, int NB>
 __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u8 *lds, const u32 (&rk)[NR + 1][4], u32 iv0,
-                                              u32 iv1, u32 iv2, u64 rec, bool valid, u32 j, u32 laneoff, u32 tsel_horner,
-                                              u32 tsel_last)
+                                              u32 iv1, u32 iv2, u64 rec, bool valid, u32 j, u32 laneoff, u32 tsel_horner)
 {
     ptls_mi355x_record_t r = {};
     if (valid)
@@ -39,8 +38,8 @@ __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u
     }
     const u32 K = valid ? gcm_steps<OPEN, 0>(r) : 0;
     u32x4 acc, ek0;
-    gcm_segment<NR, OPEN, NB>(args, lds, rk, iv0, iv1, iv2, r, valid, 0, K, j, laneoff, tsel_horner, tsel_last, acc, ek0,
-                              true, rec);
+    gcm_segment<NR, OPEN, NB>(args, lds, rk, iv0, iv1, iv2, r, valid, 0, K, j, laneoff, tsel_horner, acc, ek0, true, rec,
+                              true);
 }
 
 // Persistent kernel: workgroup w owns the contiguous record range [n*w/grid, n*(w+1)/grid) and walks it in key runs
@@ -67,7 +66,6 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     const u32 wave = threadIdx.x >> 6;
     const u32 waves_per_wg = blockDim.x >> 6;
     const u32 tsel_horner = 0x10000u + (u32)(G - 1) * GHASH_TABLE_BYTES;
-    const u32 tsel_last = 0x10000u + (u32)(G - 1 - j) * GHASH_TABLE_BYTES;
 
     const u64 n = args.nrecs;
     const u64 beg = n * blockIdx.x / gridDim.x, end = n * (blockIdx.x + 1) / gridDim.x;
@@ -115,7 +113,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         const u64 ngroups = (run_end - pos + RPW - 1) / RPW;
         for (u64 grp = wave; grp < ngroups; grp += waves_per_wg) {
             const u64 rec = pos + grp * RPW + slot;
-            process_group<NR, OPEN, ENGINE_NB>(args, lds, rk, iv0, iv1, iv2, rec, rec < run_end, j, laneoff, tsel_horner, tsel_last);
+            process_group<NR, OPEN, ENGINE_NB>(args, lds, rk, iv0, iv1, iv2, rec, rec < run_end, j, laneoff, tsel_horner);
         }
         pos = run_end;
     }
@@ -316,7 +314,6 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     const u32 laneoff = (lane & 31) * 4;
     const u32 wave = threadIdx.x >> 6;
     const u32 tsel_horner = 0x10000u + (u32)(G - 1) * GHASH_TABLE_BYTES;
-    const u32 tsel_last = 0x10000u + (u32)(G - 1 - j) * GHASH_TABLE_BYTES;
     const u32 tsel_chunk = 0x10000u + 8u * GHASH_TABLE_BYTES;
     // unit length in steps (a power of two <= CHUNK_STEPS) and the key element of its combine power H^(G * ustep)
     const u32 ustep = 1u << args.unit_log2;
@@ -447,8 +444,8 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             if (!live)
                 m_lo = m_hi = 0;
             u32x4 acc, ek0;
-            gcm_segment<NR, OPEN, 1, FRAME>(args, lds, rk, iv0, iv1, iv2, r, live, m_lo, m_hi, j, laneoff, tsel_horner,
-                                     tsel_last, acc, ek0, unc == 1, rid);
+            gcm_segment<NR, OPEN, 1, FRAME>(args, lds, rk, iv0, iv1, iv2, r, live, m_lo, m_hi, j, laneoff, tsel_horner, acc, ek0,
+                                            unc == 1, rid, whole);
             if (live && unc > 1) {  // uniform over the group
                 u32 last = 0;
                 if (j == G - 1) {

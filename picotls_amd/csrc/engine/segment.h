@@ -5,14 +5,22 @@
 
 // GHASH/CTR work of one G-lane group on steps [m_lo, m_hi) of record r's stream (see file header): lane j owns stream
 // positions j + G*m and runs them NB at a time. The NB AES-CTR blocks of a step are independent (NB x 16 LDS lookups
-// per round in flight); their GHASH folds stay sequential (Horner with H^G, the segment's last step with H^(G-j)).
-// On return every lane of the group holds the segment's GHASH partial sum(X_i * H^(end - i)) and the length lane
-// (lane G-1, when the segment holds the length block) holds E(K, J0) in ek0. Invalid groups pass m_lo == m_hi.
+// per round in flight); their GHASH folds stay sequential (Horner with H^G; each lane's last position in the segment
+// with H^(end - position), from its own table). On return every lane of the group holds the segment's GHASH partial
+// sum(X_i * H^(end - i)) and the length lane (lane (N - 1) mod G, when the segment holds the length block) holds
+// E(K, J0) in ek0. Invalid groups pass m_lo == m_hi.
+//
+// Stream layout. Units of the chunked schedule end on step boundaries, so their stream [zero padding | AAD | text |
+// length] is front-padded to a multiple of G positions (N = G * K). A whole record (ALIGNED: the lockstep kernel and the
+// chunked kernel's whole-record runs) instead takes the front padding that puts its text blocks on 128-byte lines of the
+// output: the group then stores one full line per step instead of parts of two (the parts of two cost 14.5 % more HBM
+// writes and 2 % of seal time on 16 KiB records, profiles/r2_write_align.txt). Its stream ends where it ends (N any):
+// lanes past the length block in the last step are idle, and each lane's last position p multiplies by H^(N - p), 1..G.
 template <int NR, bool OPEN, int NB, int FRAME = 0>
 __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 *lds, const u32 (&rk)[NR + 1][4], u32 iv0,
                                             u32 iv1, u32 iv2, const ptls_mi355x_record_t &r, bool valid, u32 m_lo,
-                                            u32 m_hi, u32 j, u32 laneoff, u32 tsel_horner, u32 tsel_last, u32x4 &acc,
-                                            u32x4 &ek0, bool finish, u64 rec)
+                                            u32 m_hi, u32 j, u32 laneoff, u32 tsel_horner, u32x4 &acc, u32x4 &ek0, bool finish,
+                                            u64 rec, bool aligned)
 {
     constexpr int G = ENGINE_G;
     constexpr bool SEAL_FRAME = FRAME == 1 && !OPEN, OPEN_FRAME = FRAME == 1 && OPEN, TLS12 = FRAME == 2;
@@ -21,8 +29,34 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     const u32 Lsrc = SEAL_FRAME ? L - 1 : L;
     const u32 na = (A + 15) >> 4, nb = (L + 15) >> 4;
     const u32 total = na + nb + 1;
-    const u32 K = (total + G - 1) / G;
-    const int P = (int)(K * G) - (int)total;
+    const uint8_t *src = args.in + r.in_off + frame_in_skip<OPEN, FRAME>();
+    uint8_t *dst = args.out + r.out_off + frame_out_skip<OPEN, FRAME>();
+    int P;
+    u32 N;
+    if (aligned) {  // text block b at position P + na + b, and (dst / 16 + b) mod G == that position mod G
+        const u32 K0 = (total + G - 1) / G;
+        P = (int)(((u32)((uintptr_t)dst >> 4) - na) & (G - 1));
+        // ... unless that costs a record shorter than ALIGN_MIN_STEPS steps one more step (its wave would take it too:
+        // -6 % on 1200-byte records), which keeps the padding of a multiple of G positions
+        if ((u32)P + total > K0 * G && K0 < ALIGN_MIN_STEPS)
+            P = (int)(K0 * G - total);
+        N = (u32)P + total;
+        if (valid)
+            m_hi = (N + G - 1) / G;
+    } else {
+        const u32 K = (total + G - 1) / G;
+        P = (int)(K * G) - (int)total;
+        N = K * G;
+    }
+    // this lane's last step in the segment and its power there: at the record's end H^(N - p) for its last position p,
+    // at a unit's end (a step boundary) H^(G - j)
+    const bool at_end = aligned;
+    const int m_last = !valid ? -1 : at_end ? ((int)N - 1 - (int)j) >> 3 : (int)m_hi - 1;
+    const u32 tsel_last = 0x10000u + (at_end ? N - 1 - (8u * (u32)m_last + j) : (u32)(G - 1) - j) * GHASH_TABLE_BYTES;
+    // the first step in which some lane of the group is at its last position (the steady range ends before it)
+    const int m_first_last = at_end ? ((int)N - G) >> 3 : (int)m_hi - 1;
+    const u32 jl = (N - 1) & (G - 1);  // the length block's lane
+    static_assert(G == 8, "m_last uses a shift by 3");
 
     const u32 Smax = wave_max_per8(m_hi - m_lo);  // m_lo, m_hi are uniform within a group
 
@@ -37,8 +71,6 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     const u32 n0 = iv0 ^ rk[0][0];
     const u32 n1 = iv1 ^ nw1 ^ rk[0][1];
     const u32 n2 = iv2 ^ nw2 ^ rk[0][2];
-    const uint8_t *src = args.in + r.in_off + frame_in_skip<OPEN, FRAME>();
-    uint8_t *dst = args.out + r.out_off + frame_out_skip<OPEN, FRAME>();
     const uint8_t *aadp = OPEN_FRAME ? args.in + r.in_off : args.aad + r.aad_off;
 
     acc = u32x4{0, 0, 0, 0};
@@ -164,7 +196,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     const int ms = (D0 + G - 1) / G;    // first step whose 8 positions are all >= D0
     const int me = nbf + D0 >= G ? (nbf + D0 - G) / G : -1;  // last step whose 8 positions are all full text
     int sa = max(ms, (int)m_lo) - (int)m_lo;
-    int sb = min(me - 1, (int)m_hi - 2) + 1 - (int)m_lo;
+    int sb = min(me - 1, m_first_last - 1) + 1 - (int)m_lo;
     if (!valid || m_hi <= m_lo)
         sa = 1, sb = 0;
     sa = wave_smax_per8(sa);
@@ -204,8 +236,8 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         // scheduling fence: keeps the 32 table loads of this fold from being hoisted next to the other work (that
         // hoisting spills them to scratch)
         __builtin_amdgcn_sched_barrier(0);
-        const u32x4 prod = gmul_tab(lds, acc ^ X, m0 + 1 == m_hi ? tsel_last : tsel_horner);
-        if (m0 < m_hi)
+        const u32x4 prod = gmul_tab(lds, acc ^ X, (int)m0 == m_last ? tsel_last : tsel_horner);
+        if ((int)m0 <= m_last)
             acc = prod;
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -217,7 +249,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         acc[c] = dpp_xor8(acc[c]);
     // whole record (finish): tag = GHASH ^ E(K, J0), written after the ciphertext (seal) or compared with the
     // received one (open)
-    if (finish && valid && j == G - 1) {
+    if (finish && valid && j == jl) {
         const u32x4 tag = acc ^ ek0;
         if (OPEN) {
             const u32x4 rt = *(const u32x4_u *)(src + L);

@@ -42,11 +42,16 @@ def main():
     d_aad = torch.from_numpy(wl.aad_arena(b, 0)).to(dev)
     d_out = torch.zeros(out_bytes, dtype=torch.uint8, device=dev)
     s = torch.cuda.current_stream().cuda_stream
-    for _ in range(a.reps):
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(a.reps + 1)]
+    ev[0].record()
+    for i in range(a.reps):
         pa.seal_batch(ks, d_recs.data_ptr(), b.n, d_pt.data_ptr(), d_aad.data_ptr(), d_out.data_ptr(), s)
+        ev[i + 1].record()
     torch.cuda.synchronize()
+    ms = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(1, a.reps))  # the first launch warms up
     ks.free()
-    print(f"write_align: layout={a.layout} records={b.n} algorithmic writes per launch {b.n * 16400} B")
+    print(f"write_align: layout={a.layout} records={b.n} algorithmic writes per launch {b.n * 16400} B, "
+          f"seal median {ms[len(ms) // 2]:.3f} ms over {len(ms)} launches")
 
 
 if __name__ == "__main__":
