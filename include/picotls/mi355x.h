@@ -127,6 +127,17 @@ int ptls_mi355x_keyset_set_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, const vo
 int ptls_mi355x_keyset_set_schedule(ptls_mi355x_keyset_t *ks, int schedule);
 
 /**
+ * Constant-time LDS access (no reference counterpart: fusion's AES-NI / PCLMUL code is constant-time by construction).
+ * The AES T-table lookups and the GHASH Horner steps have bank-conflict patterns that do not depend on keys or data; by
+ * default the GHASH multiply of each lane's last block position (from a per-lane table of H^1..H^8) and the unit
+ * combine do, in 0.5 % of the kernel's LDS cycles. With on != 0 the keyset's batches and per-record
+ * calls use the variant in which every LDS access has a data-independent pattern (SQ_LDS_BANK_CONFLICT equal for any
+ * key and payload), at 2-10 % of throughput. The environment variable PTLS_MI355X_CONSTANT_TIME=1 (read when a device
+ * is first used) sets it for every keyset, including those behind the picotls objects. Returns 0, or -1.
+ */
+int ptls_mi355x_keyset_set_constant_time(ptls_mi355x_keyset_t *ks, int on);
+
+/**
  * Seals nrecs records in one launch. Asynchronous on `stream`. recs, in, aad, out (and ok, results of the calls below)
  * are addresses the device can access: device memory, host memory from hipHostMalloc (its address is the device
  * address), or host memory registered with hipHostRegister passed as the address hipHostGetDevicePointer returns for it

@@ -40,6 +40,7 @@ ABI_FUNCTIONS = (
     "ptls_mi355x_keyset_set_iv",
     "ptls_mi355x_keyset_update",
     "ptls_mi355x_keyset_set_schedule",
+    "ptls_mi355x_keyset_set_constant_time",
     "ptls_mi355x_seal_batch",
     "ptls_mi355x_open_batch",
     "ptls_mi355x_seal_tls_records",
@@ -89,6 +90,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.ptls_mi355x_keyset_set_iv.argtypes = [vp, sz, vp]
     lib.ptls_mi355x_keyset_update.argtypes = [vp, vp, vp, vp, sz]
     lib.ptls_mi355x_keyset_set_schedule.argtypes = [vp, ci]
+    lib.ptls_mi355x_keyset_set_constant_time.argtypes = [vp, ci]
     lib.ptls_mi355x_seal_batch.argtypes = [vp, vp, sz, vp, vp, vp, vp]
     lib.ptls_mi355x_open_batch.argtypes = [vp, vp, sz, vp, vp, vp, vp, vp]
     lib.ptls_mi355x_ecb_batch.argtypes = [vp, vp, vp, vp, sz, vp]
@@ -181,6 +183,11 @@ class Keyset:
             raise ValueError("keys must be n*key_size bytes and ivs n*12 bytes")
         if load_library().ptls_mi355x_keyset_update(self.handle, _buf(idx), _buf(k), _buf(v), idx.size) != 0:
             raise _err("keyset_update")
+
+    def set_constant_time(self, on: bool = True) -> None:
+        """Constant-time GHASH variant (ptls_mi355x_keyset_set_constant_time)."""
+        if load_library().ptls_mi355x_keyset_set_constant_time(self.handle, 1 if on else 0) != 0:
+            raise _err("set_constant_time")
 
     SCHEDULES = {"auto": 0, "lockstep": 1, "chunked": 2}
 

@@ -115,6 +115,7 @@ struct DeviceState {
                                   // per-record round trips) are dispatched ahead of bulk batches on ordinary streams
     bool force_copy = false;      // PTLS_MI355X_STAGE_COPY=1: the staging round trip copies instead of mapping
     size_t stage_limit = 0;       // PTLS_MI355X_MAX_STAGE_BYTES: the largest staging buffer one call may use
+    bool ct_default = false;      // PTLS_MI355X_CONSTANT_TIME=1: new keysets use the constant-time GHASH variant
     std::mutex mu;                // the pools below
     Stager *stagers[STAGE_CLASSES] = {};
     std::vector<KeyEntry *> slots;
@@ -132,7 +133,9 @@ static int set_kernel_attrs(void)
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<14, false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<14, true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
 #define CHUNKED_ATTR(nr, open, frame)                                                                                  \
-    HIP_TRY(hipFuncSetAttribute((const void *)gcm_chunked_kernel<nr, open, frame>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_chunked_kernel<nr, open, frame, false>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                CLDS_ALLOC));                                                                              \
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_chunked_kernel<nr, open, frame, true>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                 CLDS_ALLOC))
     CHUNKED_ATTR(10, false, 0);
     CHUNKED_ATTR(10, true, 0);
@@ -177,6 +180,8 @@ static DeviceState *device_state(int dev)
     ds->device = dev;
     const char *copy = getenv("PTLS_MI355X_STAGE_COPY"), *limit = getenv("PTLS_MI355X_MAX_STAGE_BYTES");
     ds->force_copy = copy != nullptr && strcmp(copy, "1") == 0;
+    const char *ct = getenv("PTLS_MI355X_CONSTANT_TIME");
+    ds->ct_default = ct != nullptr && strcmp(ct, "1") == 0;
     ds->stage_limit = limit != nullptr ? (size_t)strtoull(limit, nullptr, 0) : (size_t)4096 << (STAGE_CLASSES - 1);
     int least = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &ds->priority) != hipSuccess)
@@ -345,6 +350,7 @@ struct st_ptls_mi355x_keyset_t {
     KeyEntry *d_keys;
     bool slot;  // d_keys is one entry of the device's slab (one-key keysets)
     int schedule;
+    bool ct;                           // constant-time GHASH (ptls_mi355x_keyset_set_constant_time)
     hipEvent_t ready;                  // the last setup / update / set_iv of the entries
     std::atomic<bool> ready_seen;      // ... known to be complete: launches need not wait for it
     std::vector<uint8_t> ivs;          // the static IVs (do_get_iv reads these; the device copy is what seals use)
@@ -451,6 +457,7 @@ ptls_mi355x_keyset_t *ptls_mi355x_keyset_new(const void *keys, const void *ivs, 
     ks->ds = ds;
     ks->device = ds->device;
     ks->nkeys = nkeys, ks->key_size = key_size, ks->nr = key_size == 16 ? 10 : 14;
+    ks->ct = ds->ct_default;
     ks->ready_seen.store(false);
     ks->ivs.assign((const uint8_t *)ivs, (const uint8_t *)ivs + nkeys * 12);
     if ((ks->ready = event_get(ds)) == nullptr) {
@@ -601,6 +608,14 @@ int ptls_mi355x_keyset_set_schedule(ptls_mi355x_keyset_t *ks, int schedule)
     return 0;
 }
 
+int ptls_mi355x_keyset_set_constant_time(ptls_mi355x_keyset_t *ks, int on)
+{
+    if (ks == NULL)
+        return fail("%s", "set_constant_time: invalid arguments");
+    ks->ct = on != 0;
+    return 0;
+}
+
 size_t ptls_mi355x_keyset_size(const ptls_mi355x_keyset_t *ks) { return ks->nkeys; }
 size_t ptls_mi355x_keyset_key_size(const ptls_mi355x_keyset_t *ks) { return ks->key_size; }
 
@@ -636,11 +651,21 @@ int ptls_mi355x_keyset_set_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, const vo
 // 784 vs 751 on 1200 B), and its chunked runs balance mixed lengths and short key runs.
 static bool use_chunked(int schedule) { return schedule != PTLS_MI355X_SCHEDULE_LOCKSTEP; }
 
-// The GCM kernel launch of a batch over `nkeys` entries at `keys` (no key grouping, no keyset bookkeeping).
-static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int schedule, bool open, const ptls_mi355x_record_t *recs,
-                      size_t nrecs, const void *in, const void *aad, void *out, uint8_t *ok, hipStream_t s, int frame,
-                      u32 unit_log2, const ptls_mi355x_record_t *grouped = nullptr, const u32 *perm = nullptr,
-                      const u32 *perm_on = nullptr)
+template <int NR, bool OPEN, int FRAME>
+static void launch_chunked(bool ct, unsigned grid, hipStream_t s, const BatchArgs &a)
+{
+    if (ct)
+        gcm_chunked_kernel<NR, OPEN, FRAME, true><<<grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
+    else
+        gcm_chunked_kernel<NR, OPEN, FRAME, false><<<grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
+}
+
+// The GCM kernel launch of a batch over `nkeys` entries at `keys` (no key grouping, no keyset bookkeeping). ct: the
+// constant-time GHASH variant of the chunked kernel (the lockstep schedule is not offered in that mode).
+static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int schedule, bool ct, bool open,
+                      const ptls_mi355x_record_t *recs, size_t nrecs, const void *in, const void *aad, void *out, uint8_t *ok,
+                      hipStream_t s, int frame, u32 unit_log2, const ptls_mi355x_record_t *grouped = nullptr,
+                      const u32 *perm = nullptr, const u32 *perm_on = nullptr)
 {
     BatchArgs a = {keys, recs, (u64)nrecs, (const uint8_t *)in, (const uint8_t *)aad, (uint8_t *)out, ok,
                    nkeys > 1 ? 1u : 0u, nkeys, unit_log2, grouped, perm, perm_on};
@@ -653,7 +678,7 @@ static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int sche
         grid = (groups + 3) / 4;
     if (grid < 1)
         grid = 1;
-#define CHUNKED_LAUNCH(nr_, op, frame_) gcm_chunked_kernel<nr_, op, frame_><<<(unsigned)grid, ENGINE_WG, CLDS_ALLOC, s>>>(a)
+#define CHUNKED_LAUNCH(nr_, op, frame_) launch_chunked<nr_, op, frame_>(ct, (unsigned)grid, s, a)
 #define CHUNKED_BY_KEY(frame_)                                                                                          \
     do {                                                                                                                \
         if (nr == 10) {                                                                                                 \
@@ -672,7 +697,7 @@ static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int sche
         CHUNKED_BY_KEY(1);
     else if (frame == 2)
         CHUNKED_BY_KEY(2);
-    else if (use_chunked(schedule))
+    else if (ct || use_chunked(schedule))
         CHUNKED_BY_KEY(0);
     else if (nr == 10) {
         if (open)
@@ -735,13 +760,13 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
         key_scan_kernel<<<1, 1024, 0, s>>>(cnt, (u32)nb, nrecs, ctl);
         ptls_mi355x_record_t *grouped = (ptls_mi355x_record_t *)(ctl + ((2 + nb + nrecs + 1) & ~(size_t)1));
         key_scatter_kernel<<<gh, 256, 0, s>>>(recs, nrecs, (u32)ks->nkeys, cnt, perm, grouped, ctl);
-        ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, open, recs, nrecs, in, aad, out, ok, s, frame,
-                         CHUNK_LOG2, grouped, perm, ctl + 1);
+        ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, ks->ct, open, recs, nrecs, in, aad, out, ok, s,
+                         frame, CHUNK_LOG2, grouped, perm, ctl + 1);
         if (ret == 0)
             HIP_TRY(hipEventRecord(ks->group_ev, s));
     } else {
-        ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, open, recs, nrecs, in, aad, out, ok, s,
-                         frame, CHUNK_LOG2);
+        ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, ks->ct, open, recs, nrecs, in, aad, out, ok,
+                         s, frame, CHUNK_LOG2);
     }
     if (ret != 0)
         return -1;
@@ -979,7 +1004,7 @@ static int single(ptls_mi355x_keyset_t *ks, size_t key_idx, bool open, void *out
     if (wait_ready(ks, s) != 0 || (hp_ks != NULL && wait_ready(hp_ks, s) != 0))
         return -1;
     if (call.roundtrip(off_out, [&] {
-            if (launch_gcm(ks->d_keys + key_idx, 1, ks->nr, ks->ds->ncu, ks->schedule, open, (const ptls_mi355x_record_t *)(d + off_rec),
+            if (launch_gcm(ks->d_keys + key_idx, 1, ks->nr, ks->ds->ncu, ks->schedule, ks->ct, open, (const ptls_mi355x_record_t *)(d + off_rec),
                            1, d + off_in, d + off_aad, d + off_out, d + off_ok, s, 0, unit_log2 < CHUNK_LOG2 ? unit_log2 : CHUNK_LOG2) != 0)
                 return -1;
             return hp_ks == NULL ? 0

@@ -297,7 +297,7 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
 // GHASH = sum_k P_k * H^(k * CHUNK_BLOCKS). The group that completes a record's last outstanding unit (LDS counter per
 // record) evaluates that sum by Horner with the H^CHUNK_BLOCKS table and finishes the tag, inside the unit loop.
 // Single-unit records finish inside their unit as in the lockstep kernel.
-template <int NR, bool OPEN, int FRAME>
+template <int NR, bool OPEN, int FRAME, bool CT = false>
 __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGINE_WAVES_PER_SIMD, ENGINE_WAVES_PER_SIMD))) void gcm_chunked_kernel(BatchArgs args)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -444,7 +444,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             if (!live)
                 m_lo = m_hi = 0;
             u32x4 acc, ek0;
-            gcm_segment<NR, OPEN, 1, FRAME>(args, lds, rk, iv0, iv1, iv2, r, live, m_lo, m_hi, j, laneoff, tsel_horner, acc, ek0,
+            gcm_segment<NR, OPEN, 1, FRAME, CT>(args, lds, rk, iv0, iv1, iv2, r, live, m_lo, m_hi, j, laneoff, tsel_horner, acc, ek0,
                                             unc == 1, rid, whole);
             if (live && unc > 1) {  // uniform over the group
                 u32 last = 0;
@@ -459,11 +459,13 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 if (last) {
                     // last unit of the record: GHASH = Horner over the partials with H^(G * ulen) = (H^(G * ustep))^mul
                     // (whole group)
+                    // (CT: each lane forms the whole product from the same table rows, instead of a share of it from
+                    // its own window rows)
                     u32x4 g = s_part[first];
                     for (u32 i = 1; i < unc; ++i) {
-                        g = gmul_group(lds, g, tsel_chunk, j);
+                        g = CT ? gmul_tab(lds, g, tsel_chunk) : gmul_group(lds, g, tsel_chunk, j);
                         for (u32 t = 1; t < mul; ++t)  // huge records only
-                            g = gmul_group(lds, g, tsel_chunk, j);
+                            g = CT ? gmul_tab(lds, g, tsel_chunk) : gmul_group(lds, g, tsel_chunk, j);
                         g ^= s_part[first + i];
                     }
                     const u32x4 tag = g;

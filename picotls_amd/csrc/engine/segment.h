@@ -16,7 +16,13 @@
 // output: the group then stores one full line per step instead of parts of two (the parts of two cost 14.5 % more HBM
 // writes and 2 % of seal time on 16 KiB records, profiles/r2_write_align.txt). Its stream ends where it ends (N any):
 // lanes past the length block in the last step are idle, and each lane's last position p multiplies by H^(N - p), 1..G.
-template <int NR, bool OPEN, int NB, int FRAME = 0>
+//
+// CT (constant-time LDS access): a lane's last multiply by its own power H^e, from its own table, reads another table
+// row than the lanes beside it, so its bank conflicts depend on the data (profiles/r2_ct_counters.txt). With CT, a step
+// in which any lane of the wave takes its last multiply runs four multiplies that every lane takes from the same table
+// (H^8, then H^4, H^2, H^1 on the bits of e, each kept or not per lane): every LDS access of the kernel then has a
+// conflict pattern that depends on the record layout only.
+template <int NR, bool OPEN, int NB, int FRAME = 0, bool CT = false>
 __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 *lds, const u32 (&rk)[NR + 1][4], u32 iv0,
                                             u32 iv1, u32 iv2, const ptls_mi355x_record_t &r, bool valid, u32 m_lo,
                                             u32 m_hi, u32 j, u32 laneoff, u32 tsel_horner, u32x4 &acc, u32x4 &ek0, bool finish,
@@ -52,7 +58,8 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     // at a unit's end (a step boundary) H^(G - j)
     const bool at_end = aligned;
     const int m_last = !valid ? -1 : at_end ? ((int)N - 1 - (int)j) >> 3 : (int)m_hi - 1;
-    const u32 tsel_last = 0x10000u + (at_end ? N - 1 - (8u * (u32)m_last + j) : (u32)(G - 1) - j) * GHASH_TABLE_BYTES;
+    const u32 e_last = at_end ? N - (8u * (u32)m_last + j) : (u32)G - j;  // 1..G
+    const u32 tsel_last = 0x10000u + (e_last - 1) * GHASH_TABLE_BYTES;
     // the first step in which some lane of the group is at its last position (the steady range ends before it)
     const int m_first_last = at_end ? ((int)N - G) >> 3 : (int)m_hi - 1;
     const u32 jl = (N - 1) & (G - 1);  // the length block's lane
@@ -236,7 +243,27 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         // scheduling fence: keeps the 32 table loads of this fold from being hoisted next to the other work (that
         // hoisting spills them to scratch)
         __builtin_amdgcn_sched_barrier(0);
-        const u32x4 prod = gmul_tab(lds, acc ^ X, (int)m0 == m_last ? tsel_last : tsel_horner);
+        const bool last_here = (int)m0 == m_last;
+        u32x4 prod;
+        if (CT && __any(last_here)) {
+            // H^8 (the Horner step, and a last power of 8), then H^4, H^2, H^1 kept on the bits of e_last; one
+            // multiply site in a loop, so the branch costs no more registers than a plain step
+            u32x4 t = acc ^ X;
+            prod = t;
+#pragma unroll 1
+            for (u32 it = 0; it < 4; ++it) {
+                const u32x4 q = gmul_tab(lds, t, 0x10000u + ((8u >> it) - 1u) * GHASH_TABLE_BYTES);
+                if (it == 0)
+                    prod = q;
+                else if (e_last & (8u >> it))
+                    t = q;
+            }
+            if (!last_here || e_last == (u32)G)
+                t = prod;
+            prod = t;
+        } else {
+            prod = gmul_tab(lds, acc ^ X, !CT && last_here ? tsel_last : tsel_horner);
+        }
         if ((int)m0 <= m_last)
             acc = prod;
         __builtin_amdgcn_sched_barrier(0);

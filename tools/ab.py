@@ -46,13 +46,16 @@ def main():
     d_aad = torch.from_numpy(wl.aad_arena(b, 0)).to(dev)
     d_pt = payload_torch(wl.seed, b.pt_bytes, dev)
     outs = {}
-    libs = [(p, bind(p)) for p in a.libs]
+    # a variant is a library path, optionally suffixed ":ct" (the same build with ptls_mi355x_keyset_set_constant_time)
+    libs = [(p, bind(p.split(":")[0])) for p in a.libs]
     kss = {}
     for p, lib in libs:
         kss[p] = ctypes.c_void_p(lib.ptls_mi355x_keyset_new(keys.ctypes.data, ivs.ctypes.data, wl.nkeys, wl.key_size))
         assert kss[p].value, p
         if a.schedule and hasattr(lib, "ptls_mi355x_keyset_set_schedule"):
             assert lib.ptls_mi355x_keyset_set_schedule(kss[p], a.schedule) == 0
+        if p.endswith(":ct"):
+            assert lib.ptls_mi355x_keyset_set_constant_time(kss[p], 1) == 0
     sealed = torch.empty(b.sealed_bytes, dtype=torch.uint8, device=dev)
     back = torch.empty(b.pt_bytes, dtype=torch.uint8, device=dev)
     ok = torch.empty(b.n, dtype=torch.uint8, device=dev)

@@ -3,7 +3,7 @@
 key and payload, so that rocprofv3 --pmc SQ_LDS_BANK_CONFLICT / SQ_WAIT_INST_LDS / SQ_LDS_IDX_ACTIVE / SQ_INSTS_LDS can
 be compared across keys and payloads. Identical shapes: record count, lengths, AAD, sequence numbers.
 
-    python tools/ct_probe.py --key-seed 1 --payload zero|random|ones [--workload tls16k --records 65536 --reps 3]
+    python tools/ct_probe.py --key-seed 1 --payload zero|random|ones [--ct] [--workload tls16k --records 65536 --reps 3]
 """
 import argparse
 import os
@@ -21,11 +21,16 @@ def main():
     p.add_argument("--workload", default="tls16k")
     p.add_argument("--records", type=int, default=65536)
     p.add_argument("--reps", type=int, default=3)
+    p.add_argument("--lib", default=None, help="engine build to probe (default: picotls_amd/_lib/libptls_mi355x.so)")
+    p.add_argument("--ct", action="store_true", help="the constant-time GHASH variant (ptls_mi355x_keyset_set_constant_time)")
     a = p.parse_args()
 
     import torch
 
     import picotls_amd as pa
+
+    if a.lib:
+        pa.load_library(a.lib)
     from picotls_amd.workloads import WORKLOADS, payload_torch
 
     wl = WORKLOADS[a.workload].scaled(a.records)
@@ -34,6 +39,8 @@ def main():
     keys = np.frombuffer(rng.bytes(wl.nkeys * wl.key_size), np.uint8)
     ivs = np.frombuffer(rng.bytes(wl.nkeys * 12), np.uint8)
     ks = pa.Keyset(keys, ivs, wl.key_size)
+    if a.ct:
+        ks.set_constant_time(True)
     dev = torch.device("cuda:0")
     if a.payload == "random":
         d_pt = payload_torch(wl.seed, b.pt_bytes, dev)
@@ -52,7 +59,7 @@ def main():
     torch.cuda.synchronize()
     assert bool(d_ok.min().item() == 1)
     ks.free()
-    print(f"ct_probe: key_seed={a.key_seed} payload={a.payload} workload={a.workload} records={b.n} ok")
+    print(f"ct_probe: key_seed={a.key_seed} payload={a.payload} workload={a.workload} records={b.n} ct={a.ct} ok")
 
 
 if __name__ == "__main__":
