@@ -1,10 +1,10 @@
-// Host unit test of the bitsliced AES core (picotls_amd/csrc/aes_bitsliced.h) against the oracle's AES
+// Host unit test of the bitsliced AES core (tools/mb/aes_bitsliced.h) against the oracle's AES
 // (oracle/gcm_ref.c): load/store round trip, and AES-128/256 of random 8-block batches. Exit status 0 = pass.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
-#include "../../picotls_amd/csrc/aes_bitsliced.h"
+#include "../../tools/mb/aes_bitsliced.h"
 
 extern "C" {
 int oracle_aes_expand(uint8_t *rk, const uint8_t *key, size_t key_size);

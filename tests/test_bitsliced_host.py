@@ -1,4 +1,4 @@
-"""Host unit test of the bitsliced AES core (picotls_amd/csrc/aes_bitsliced.h, the VALU-only AES evaluated against the
+"""Host unit test of the bitsliced AES core (tools/mb/aes_bitsliced.h, the VALU-only AES evaluated against the
 T-table rounds in DESIGN.md §5) against the oracle's AES: compiled with g++ and run on the CPU."""
 import os
 import shutil
@@ -24,7 +24,7 @@ def test_bitsliced_aes_matches_oracle(tmp_path):
 def test_sbox_circuit_generator_is_current():
     # the committed .inc is what the generator emits from the verified circuit
     gen = os.path.join(ROOT, "tools", "gen", "gen_bs_sbox.py")
-    inc = os.path.join(ROOT, "picotls_amd", "csrc", "aes_bs_sbox.inc")
+    inc = os.path.join(ROOT, "tools", "mb", "aes_bs_sbox.inc")
     before = open(inc).read()
     subprocess.run(["python3", gen], check=True, capture_output=True)
     assert open(inc).read() == before

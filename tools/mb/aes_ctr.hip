@@ -1,7 +1,7 @@
 // AES-CTR keystream microbenchmark: the engine's two AES implementations side by side on the same data.
 //   ctr_tt  LDS T-tables (the rounds of aesgcm_engine.hip: Te0/Te2 replicated over 32 banks, v_perm addressing), one
 //           block per lane per iteration
-//   ctr_bs  bitsliced (picotls_amd/csrc/aes_bitsliced.h), eight blocks per lane per iteration, VALU only; key
+//   ctr_bs  bitsliced (tools/mb/aes_bitsliced.h), eight blocks per lane per iteration, VALU only; key
 //           planes read with scalar loads
 // out[i] = in[i] ^ AES_K(nonce || BE32(i + 2)) for 16-byte blocks i (the GCM counter numbering). Both kernels must give
 // identical output (checked by tools/mb/aes_ctr.py). Build:
@@ -9,7 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "../../picotls_amd/csrc/aes_bitsliced.h"
+#include "aes_bitsliced.h"
 
 typedef uint32_t u32;
 typedef uint64_t u64;
