@@ -182,4 +182,5 @@ WORKLOADS = {
                           desc="4M mixed-length records 64 B-16 KiB, AES-256-GCM, one key"),
     "tls16k256": Workload("tls16k256", 1 << 20, 16384, 5, 32, tls_header_aad=True,
                           desc="1M x 16384 B TLS records, AES-256-GCM, one key"),
+    "u8k256": Workload("u8k256", 4 << 20, 8192, 13, 32, desc="4M x 8192 B records, AES-256-GCM, one key"),
 }
