@@ -6,7 +6,7 @@ bulk batches streaming on another stream?
 Interleaved A/B in one process: `reps` rounds of [bulk alone, bulk while a second thread creates, uses once and frees
 `contexts` contexts (bulk launches continue until the churn is done)]. Bulk = seal_batch over 256K x 16 KiB records
 (4 GiB), back to back on one stream, timed with HIP events. Prints one JSON line: bulk GiB/s alone and under churn, their
-ratio, and the churn thread's per-context costs (create, first seal, free) on an idle device and under the bulk load.
+ratio, and the churn thread's per-context costs (create, first seal, second seal, free) on an idle device and under the bulk load.
 
     python tools/lifecycle.py [--contexts 1000] [--reps 4] [--records 262144]
 """
@@ -63,8 +63,9 @@ def main():
     out = ctypes.create_string_buffer(1216)
 
     def churn(stats):
-        # one context per iteration: create, seal one 1200-byte record (the first use waits for its setup), free
-        t_new, t_first, t_free = [], [], []
+        # one context per iteration: create, seal one 1200-byte record (the first use waits for its setup), seal a
+        # second one (a context in use), free
+        t_new, t_first, t_second, t_free = [], [], [], []
         t00 = time.perf_counter()
         for n in range(a.contexts):
             t0 = time.perf_counter()
@@ -73,15 +74,19 @@ def main():
             assert h, pa._err("keyset_new")
             assert lib.ptls_mi355x_encrypt(ctypes.c_void_p(h), 0, out, pt, len(pt), n, None, 0) == 0
             t2 = time.perf_counter()
-            lib.ptls_mi355x_keyset_free(ctypes.c_void_p(h))
+            assert lib.ptls_mi355x_encrypt(ctypes.c_void_p(h), 0, out, pt, len(pt), n + 1, None, 0) == 0
             t3 = time.perf_counter()
+            lib.ptls_mi355x_keyset_free(ctypes.c_void_p(h))
+            t4 = time.perf_counter()
             t_new.append(t1 - t0)
             t_first.append(t2 - t1)
-            t_free.append(t3 - t2)
+            t_second.append(t3 - t2)
+            t_free.append(t4 - t3)
         us = lambda x, q: round(1e6 * float(np.percentile(x, q)), 1)  # noqa: E731
         stats.update({"contexts": a.contexts, "seconds": round(time.perf_counter() - t00, 4),
                       "new_us_p50": us(t_new, 50), "new_us_p99": us(t_new, 99),
                       "first_seal_us_p50": us(t_first, 50), "first_seal_us_p99": us(t_first, 99),
+                      "second_seal_us_p50": us(t_second, 50), "second_seal_us_p99": us(t_second, 99),
                       "free_us_p50": us(t_free, 50), "free_us_p99": us(t_free, 99)})
 
     def bulk_while(th):
