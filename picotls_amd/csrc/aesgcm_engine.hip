@@ -671,11 +671,10 @@ static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int sche
                    nkeys > 1 ? 1u : 0u, nkeys, unit_log2, grouped, perm, perm_on};
     if (a.aad == NULL)
         a.aad = a.in;
-    const u64 groups = (nrecs + (64 / ENGINE_G) - 1) / (64 / ENGINE_G);
-    // one persistent workgroup per CU; small batches use fewer workgroups so each still gets >= 4 record groups
+    // one persistent workgroup per CU. A batch with fewer records than CUs takes one workgroup per record.
     u64 grid = (u64)ncu;
-    if (grid > (groups + 3) / 4)
-        grid = (groups + 3) / 4;
+    if (grid > nrecs)
+        grid = nrecs;
     if (grid < 1)
         grid = 1;
 #define CHUNKED_LAUNCH(nr_, op, frame_) launch_chunked<nr_, op, frame_>(ct, (unsigned)grid, s, a)
@@ -714,6 +713,16 @@ static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int sche
 #undef CHUNKED_LAUNCH
     HIP_TRY(hipGetLastError());
     return 0;
+}
+
+// Unit length of a batch launch (chunked runs): 2 KiB units, except in a batch so small that a workgroup gets at most 8
+// records (fewer than 8 per CU): then shorter units, so that a workgroup's few records still fill its 128 groups (a
+// 16 KiB record is 128 steps: 8 records in 8-step units, 4 or fewer in 4-step units; a record's unit combine then
+// chains at most 32 partials). Lengths are on the device, so the rule goes by the record count alone.
+static u32 batch_unit_log2(size_t nrecs, int ncu)
+{
+    const size_t per_wg = (nrecs + (size_t)ncu - 1) / (size_t)ncu;
+    return per_wg > 8 ? CHUNK_LOG2 : per_wg > 4 ? 3u : 2u;
 }
 
 // A batch call on a keyset: waits for the keyset's setup, groups an ungrouped many-key batch by key on the device, launches,
@@ -761,12 +770,12 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
         ptls_mi355x_record_t *grouped = (ptls_mi355x_record_t *)(ctl + ((2 + nb + nrecs + 1) & ~(size_t)1));
         key_scatter_kernel<<<gh, 256, 0, s>>>(recs, nrecs, (u32)ks->nkeys, cnt, perm, grouped, ctl);
         ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, ks->ct, open, recs, nrecs, in, aad, out, ok, s,
-                         frame, CHUNK_LOG2, grouped, perm, ctl + 1);
+                         frame, batch_unit_log2(nrecs, ks->ds->ncu), grouped, perm, ctl + 1);
         if (ret == 0)
             HIP_TRY(hipEventRecord(ks->group_ev, s));
     } else {
         ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, ks->ct, open, recs, nrecs, in, aad, out, ok,
-                         s, frame, CHUNK_LOG2);
+                         s, frame, batch_unit_log2(nrecs, ks->ds->ncu));
     }
     if (ret != 0)
         return -1;
