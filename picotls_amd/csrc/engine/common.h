@@ -52,7 +52,7 @@ __constant__ SboxTable c_sbox = make_sbox();
 struct KeyEntry {
     u32 rk[15][4];  // round keys, LE column words; rounds 1..NR-1 stored rotated right by 8 bits (see aes_rounds_n)
     u32 iv[4];      // static IV as LE words (word 3 = 0)
-    u32 h[16][4];   // GHASH elements (LE words): [0..7] = H^1..H^8, [8] = H^CHUNK_BLOCKS, [9..11] = H^16, H^32, H^64
+    u32 h[16][4];   // GHASH elements (LE words): [0..7] = H^1..H^8, [8] = H^CHUNK_BLOCKS, [9..12] = H^16, H^32, H^64, H^128
                     // (the combine powers of smaller units), [12..15] = 0
 };
 static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
@@ -81,7 +81,9 @@ static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 // Chunked schedule (many-key batches): records are cut into units of at most CHUNK_BLOCKS GHASH-stream blocks, and
 // the per-unit GHASH partials are recombined with H^CHUNK_BLOCKS (one more 8 KiB table, LDS table slot 8).
 #ifndef CHUNK_BLOCKS
-#define CHUNK_BLOCKS 128  // 2 KiB units: 64K-key mixed +3 %, one-key mixed +7 % over 1 KiB units (interleaved A/B); 256: +1 % / +10 %
+// 2 KiB units: 64K-key mixed +3 %, one-key mixed +7 % over 1 KiB units (interleaved A/B, round 1). 4 KiB units (256,
+// round 2, profiles/r2_chunk_ab.txt): 64K-key mixed -2.3 %, random key order -1.5 %, one-key mixed +0.8 %
+#define CHUNK_BLOCKS 128
 #endif
 #define CHUNK_STEPS (CHUNK_BLOCKS / ENGINE_G)
 #define CHUNK_LOG2 (__builtin_ctz(CHUNK_STEPS))
@@ -114,7 +116,7 @@ static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 #define CLDS_ALLOC (CLDS_PART + 16 * CRUN_UNITS)
 static_assert(CLDS_ALLOC <= 160 * 1024, "chunked schedule LDS budget");
 static_assert(CHUNK_BLOCKS % ENGINE_G == 0, "units are whole steps");
-static_assert((CHUNK_STEPS & (CHUNK_STEPS - 1)) == 0 && CHUNK_STEPS <= 16, "unit lengths are powers of two up to 16 steps");
+static_assert((CHUNK_STEPS & (CHUNK_STEPS - 1)) == 0 && CHUNK_STEPS <= 32, "unit lengths are powers of two up to 32 steps");
 
 
 // ------------------------------------------------------------------------------------------------ small helpers

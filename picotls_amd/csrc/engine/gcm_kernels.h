@@ -317,7 +317,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     const u32 tsel_chunk = 0x10000u + 8u * GHASH_TABLE_BYTES;
     // unit length in steps (a power of two <= CHUNK_STEPS) and the key element of its combine power H^(G * ustep)
     const u32 ustep = 1u << args.unit_log2;
-    const u32 usrc = ustep == CHUNK_STEPS ? 8u : args.unit_log2 == 0 ? 7u : 8u + args.unit_log2;
+    const u32 usrc = ustep == CHUNK_STEPS ? 8u : args.unit_log2 == 0 ? 7u : 8u + args.unit_log2;  // [9..12]: H^16..H^128
 
     const u64 n = args.nrecs;
     const u64 beg = n * blockIdx.x / gridDim.x, end = n * (blockIdx.x + 1) / gridDim.x;

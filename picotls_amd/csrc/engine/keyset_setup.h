@@ -149,9 +149,9 @@ __device__ void setup_entry(const S &sb, const uint8_t *k, const uint8_t *v, Key
     }
     static_assert(CHUNK_BLOCKS >= 8 && (CHUNK_BLOCKS & (CHUNK_BLOCKS - 1)) == 0, "unit powers are squarings of H^8");
     for (int c = 0; c < 4; ++c)
-        out[8][c] = out[7][c];  // CHUNK_BLOCKS == 8
+        out[8][c] = out[7][c], out[12][c] = 0;  // CHUNK_BLOCKS == 8
 #pragma unroll
-    for (int n = 16; n <= (CHUNK_BLOCKS > 64 ? CHUNK_BLOCKS : 64); n *= 2) {
+    for (int n = 16; n <= (CHUNK_BLOCKS > 128 ? CHUNK_BLOCKS : 128); n *= 2) {
         const u32 q[4] = {p[0], p[1], p[2], p[3]};
         if (WAVE)
             gf_mul_be_wave(p, q);  // p = H^n
@@ -160,17 +160,17 @@ __device__ void setup_entry(const S &sb, const uint8_t *k, const uint8_t *v, Key
         if (n == CHUNK_BLOCKS)
             for (int c = 0; c < 4; ++c)
                 out[8][c] = bswap32(p[c]);
-        if (n <= 64)
+        if (n <= 128)
             for (int c = 0; c < 4; ++c)
-                out[n == 16 ? 9 : n == 32 ? 10 : 11][c] = bswap32(p[c]);
+                out[n == 16 ? 9 : n == 32 ? 10 : n == 64 ? 11 : 12][c] = bswap32(p[c]);
     }
     if (writer) {
 #pragma unroll
-        for (int n = 0; n < 12; ++n)
+        for (int n = 0; n < 13; ++n)
 #pragma unroll
             for (int c = 0; c < 4; ++c)
                 e->h[n][c] = out[n][c];
-        for (int n = 12; n < 16; ++n)
+        for (int n = 13; n < 16; ++n)
             for (int c = 0; c < 4; ++c)
                 e->h[n][c] = 0;
     }
