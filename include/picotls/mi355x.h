@@ -83,9 +83,10 @@ int ptls_mi355x_is_supported(void);
  *
  * Keysets are independent, like picotls contexts (lib/picotls.c:6553-6568): creating, rekeying or freeing one never
  * waits for the device as a whole, only (where stated) for that keyset's own work. A one-key keyset (what each
- * ptls_aead_new_direct on the MI355X objects makes) takes an entry from a per-device pool and one setup launch whose key
- * travels in the kernel arguments; the call does not wait for it (the keyset's first use does, on the GPU). A many-key
- * keyset waits until its key arrays have been copied to the device.
+ * ptls_aead_new_direct on the MI355X objects makes) takes an entry from a per-device pool; its setup launch (the key in
+ * the kernel arguments, held in host memory until then and cleared after) runs on the stream of its first use, ahead
+ * of that use, so creating one launches nothing. A many-key keyset waits until its key arrays have been copied to the
+ * device.
  */
 ptls_mi355x_keyset_t *ptls_mi355x_keyset_new(const void *keys, const void *ivs, size_t nkeys, size_t key_size);
 /**

@@ -353,6 +353,10 @@ struct st_ptls_mi355x_keyset_t {
     bool ct;                           // constant-time GHASH (ptls_mi355x_keyset_set_constant_time)
     hipEvent_t ready;                  // the last setup / update / set_iv of the entries
     std::atomic<bool> ready_seen;      // ... known to be complete: launches need not wait for it
+    // a one-key keyset's setup waits for its first use and runs on that use's stream (no cross-stream wait for the
+    // first seal of a context); until then the raw key stays here (cleared once launched)
+    std::atomic<bool> pending;
+    RawKey raw;
     std::vector<uint8_t> ivs;          // the static IVs (do_get_iv reads these; the device copy is what seals use)
     std::mutex mu;                     // launches from several threads: uses, group scratch
     std::vector<std::pair<hipStream_t, hipEvent_t>> uses;  // per stream: after this keyset's last launch on it
@@ -363,9 +367,33 @@ struct st_ptls_mi355x_keyset_t {
     hipEvent_t group_ev;
 };
 
+static int mark_ready(ptls_mi355x_keyset_t *ks, hipStream_t s);
+
+// launches a pending one-key setup on `s` (the stream of the keyset's first use, or the maintenance stream); returns 1
+// when it did (work on `s` is then ordered after it), 0 when there was none, -1 on failure
+static int setup_now(ptls_mi355x_keyset_t *ks, hipStream_t s)
+{
+    if (!ks->pending.load(std::memory_order_acquire))
+        return 0;
+    std::lock_guard<std::mutex> lk(ks->mu);
+    if (!ks->pending.load(std::memory_order_relaxed))
+        return 0;
+    keyset_setup_one_kernel<<<1, 64, 0, s>>>(ks->raw, ks->d_keys);
+    if (hipGetLastError() != hipSuccess)
+        return fail("%s", "keyset setup launch failed");
+    clear_memory(&ks->raw, sizeof(ks->raw));
+    if (mark_ready(ks, s) != 0)
+        return -1;
+    ks->pending.store(false, std::memory_order_release);
+    return 1;
+}
+
 // makes `s` wait for the keyset's last setup / update / set_iv, unless that is known to be complete
 static int wait_ready(ptls_mi355x_keyset_t *ks, hipStream_t s)
 {
+    const int now = setup_now(ks, s);
+    if (now != 0)
+        return now < 0 ? -1 : 0;
     if (ks->ready_seen.load(std::memory_order_acquire))
         return 0;
     hipError_t q = hipEventQuery(ks->ready);
@@ -397,6 +425,8 @@ static int note_use(ptls_mi355x_keyset_t *ks, hipStream_t s)
 // orders the maintenance stream after every launch that used the keyset and after its last setup
 static int maint_after_uses(ptls_mi355x_keyset_t *ks)
 {
+    if (setup_now(ks, ks->ds->maint) < 0)
+        return -1;
     std::lock_guard<std::mutex> lk(ks->mu);
     for (auto &u : ks->uses)
         HIP_TRY(hipStreamWaitEvent(ks->ds->maint, u.second, 0));
@@ -421,6 +451,7 @@ static void keyset_destroy(ptls_mi355x_keyset_t *ks)
     if (ks->group_ev != nullptr)
         (void)hipEventDestroy(ks->group_ev);
     clear_memory(ks->ivs.data(), ks->ivs.size());
+    clear_memory(&ks->raw, sizeof(ks->raw));
     delete ks;
 }
 
@@ -459,6 +490,7 @@ ptls_mi355x_keyset_t *ptls_mi355x_keyset_new(const void *keys, const void *ivs, 
     ks->nkeys = nkeys, ks->key_size = key_size, ks->nr = key_size == 16 ? 10 : 14;
     ks->ct = ds->ct_default;
     ks->ready_seen.store(false);
+    ks->pending.store(false);
     ks->ivs.assign((const uint8_t *)ivs, (const uint8_t *)ivs + nkeys * 12);
     if ((ks->ready = event_get(ds)) == nullptr) {
         fail("%s", "ptls_mi355x_keyset_new: event creation failed");
@@ -466,23 +498,17 @@ ptls_mi355x_keyset_t *ptls_mi355x_keyset_new(const void *keys, const void *ivs, 
         return NULL;
     }
     if (nkeys == 1) {
-        // a picotls context: a slab entry and one launch with the key in its arguments, nothing to wait for
+        // a picotls context: a slab entry, and the setup launch (the key in its arguments) deferred to the first use,
+        // on that use's stream (setup_now)
         if ((ks->d_keys = slot_get(ds)) == nullptr) {
             keyset_destroy(ks);
             return NULL;
         }
         ks->slot = true;
-        RawKey raw = {};
-        memcpy(raw.key, keys, key_size);
-        memcpy(raw.iv, ivs, 12);
-        raw.key_size = (u32)key_size;
-        keyset_setup_one_kernel<<<1, 64, 0, ds->setup>>>(raw, ks->d_keys);
-        clear_memory(&raw, sizeof(raw));
-        if (hipGetLastError() != hipSuccess || mark_ready(ks, ds->setup) != 0) {
-            fail("%s", "ptls_mi355x_keyset_new: setup launch failed");
-            keyset_destroy(ks);  // the entry is not returned to the pool: its state is unknown
-            return NULL;
-        }
+        memcpy(ks->raw.key, keys, key_size);
+        memcpy(ks->raw.iv, ivs, 12);
+        ks->raw.key_size = (u32)key_size;
+        ks->pending.store(true, std::memory_order_release);
         return ks;
     }
     // many keys: entries and the raw key material in stream-ordered memory on the setup stream. The caller's arrays are
@@ -564,6 +590,7 @@ void ptls_mi355x_keyset_free(ptls_mi355x_keyset_t *ks)
         return;
     DeviceScope scope(ks->device);
     DeviceState *ds = ks->ds;
+    ks->pending.store(false, std::memory_order_release);  // never used: its setup never ran (the raw key is cleared below)
     // key material is cleared (ptls_clear_memory, lib/fusion.c:1045) after the keyset's last launch, on the maintenance
     // stream; nothing here waits on the host
     bool ordered = maint_after_uses(ks) == 0;

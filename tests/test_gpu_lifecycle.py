@@ -125,6 +125,49 @@ def test_context_churn_reuses_entries_correctly(ref):
         ctx.free()
 
 
+def test_deferred_setup_on_every_kind_of_first_use(ref):
+    # a one-key keyset's setup runs on its first use's stream: whatever that first use is (a batch on a side stream, an
+    # IV change, a rekey, a per-record call, an ECB mask), the result equals fusion with the key and IV in force
+    rng = np.random.default_rng(79)
+    key, iv, iv2, key3, iv3 = rng.bytes(16), rng.bytes(12), rng.bytes(12), rng.bytes(16), rng.bytes(12)
+    lens = rng.integers(0, 3000, 40)
+    b = RecordBatch.build(lens, 13, seqs=np.arange(40, dtype=np.uint64))
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(b.aad_bytes), np.uint8)
+    side = torch.cuda.Stream()
+
+    def batch(ks, stream):
+        d_recs, d_pt, d_aad = (torch.from_numpy(x.view(np.uint8).copy()).cuda() for x in (b.seal, pt, aad))
+        d_out = torch.zeros(b.sealed_bytes, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        pa.seal_batch(ks, d_recs.data_ptr(), b.n, d_pt.data_ptr(), d_aad.data_ptr(), d_out.data_ptr(), stream.cuda_stream)
+        stream.synchronize()
+        return d_out.cpu().numpy()
+
+    def want(k, v):
+        out = np.zeros(b.sealed_bytes, np.uint8)
+        ref.run_batch(True, np.frombuffer(k, np.uint8), np.frombuffer(v, np.uint8), 16, b.seal, pt, aad, out)
+        return out
+
+    ks = pa.Keyset(key, iv, 16)  # first use: a batch on a side stream
+    assert np.array_equal(batch(ks, side), want(key, iv))
+    ks.free()
+    ks = pa.Keyset(key, iv, 16)  # first use: set_iv (on the maintenance stream), then a batch
+    ks.set_iv(iv2)
+    assert np.array_equal(batch(ks, side), want(key, iv2))
+    ks.free()
+    ks = pa.Keyset(key, iv, 16)  # first use: a rekey
+    ks.update([0], key3, iv3)
+    assert np.array_equal(batch(ks, torch.cuda.current_stream()), want(key3, iv3))
+    ks.free()
+    ctx = pa.aead_new_direct(pa.aes128gcm, True, key, iv)  # first use: a per-record seal
+    assert ctx.encrypt(b"x" * 100, 5, b"a") == ref.seal(key, iv, 5, b"a", b"x" * 100)
+    ctx.free()
+    hp = pa.CtrCipher(key)  # first use: an ECB block (header-protection mask)
+    assert hp.mask(bytes(range(16))) == ref.aesecb(key, bytes(range(16)))
+    hp.ks.free()
+
+
 @pytest.mark.parametrize("aadlen", [65535, 65536, 70 << 10, (1 << 20) + 5])
 def test_large_aad_batch_via_flags(ref, aadlen):
     # the AAD length's bits 16..31 travel in flags (PTLS_MI355X_RECORD_AAD_LEN); batch seal and open against fusion
