@@ -57,6 +57,15 @@ struct KeyEntry {
 };
 static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 
+// The lane index, computed where it is used: the asm is volatile, so the compiler neither hoists it nor keeps a value
+// derived from it live across the kernel's loops (such values were spilled to scratch and reloaded per unit and step).
+__device__ __forceinline__ u32 lane_here()
+{
+    u32 x;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(x));
+    return x;
+}
+
 #ifndef ENGINE_FAST_STEP
 #define ENGINE_FAST_STEP 1         // wave-uniform fast path for steps where every lane holds a full text block
 #endif

@@ -167,7 +167,7 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
 {
     constexpr u32 Q = CRUN_RECS / 64;
     lds_u32 *ubase = rs + RUN_UBASE_OFF, *done = rs + RUN_DONE_OFF, *front = rs + RUN_FRONT_OFF;
-    const u32 lane = threadIdx.x & 63;
+    const u32 lane = lane_here();
     const u32 log2 = args.unit_log2, ustep = 1u << log2;
     const u32 lim = (u32)min(end - p, (u64)CRUN_RECS);
     const u32 key = args.multi_key ? recs[p].key_idx : 0u;
@@ -390,6 +390,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
 
         // ---- units: each wave takes RPW consecutive units (one per group) at a time
         for (;;) {
+            const u32 lane = lane_here(), j = lane % G, slot = lane / G, laneoff = (lane & 31) * 4;
             u32 ub = 0;
             if (lane == 0)
                 ub = atomicAdd((u32 *)&rs[RC_NEXT], (u32)RPW);
