@@ -742,16 +742,6 @@ static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int sche
     return 0;
 }
 
-// Unit length of a batch launch (chunked runs): 2 KiB units, except in a batch so small that a workgroup gets at most 8
-// records (fewer than 8 per CU): then shorter units, so that a workgroup's few records still fill its 128 groups (a
-// 16 KiB record is 128 steps: 8 records in 8-step units, 4 or fewer in 4-step units; a record's unit combine then
-// chains at most 32 partials). Lengths are on the device, so the rule goes by the record count alone.
-static u32 batch_unit_log2(size_t nrecs, int ncu)
-{
-    const size_t per_wg = (nrecs + (size_t)ncu - 1) / (size_t)ncu;
-    return per_wg > 8 ? CHUNK_LOG2 : per_wg > 4 ? 3u : 2u;
-}
-
 // A batch call on a keyset: waits for the keyset's setup, groups an ungrouped many-key batch by key on the device, launches,
 // and records the use (teardown and rekey are ordered after it).
 static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
@@ -797,12 +787,12 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
         ptls_mi355x_record_t *grouped = (ptls_mi355x_record_t *)(ctl + ((2 + nb + nrecs + 1) & ~(size_t)1));
         key_scatter_kernel<<<gh, 256, 0, s>>>(recs, nrecs, (u32)ks->nkeys, cnt, perm, grouped, ctl);
         ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, ks->ct, open, recs, nrecs, in, aad, out, ok, s,
-                         frame, batch_unit_log2(nrecs, ks->ds->ncu), grouped, perm, ctl + 1);
+                         frame, CHUNK_LOG2, grouped, perm, ctl + 1);
         if (ret == 0)
             HIP_TRY(hipEventRecord(ks->group_ev, s));
     } else {
         ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, ks->ct, open, recs, nrecs, in, aad, out, ok,
-                         s, frame, batch_unit_log2(nrecs, ks->ds->ncu));
+                         s, frame, CHUNK_LOG2);
     }
     if (ret != 0)
         return -1;
@@ -1033,7 +1023,8 @@ static int single(ptls_mi355x_keyset_t *ks, size_t key_idx, bool open, void *out
         memcpy(h + off_hp, &e, sizeof(e));
     }
     // one record on one workgroup: shorter units put more of its waves to work (a unit step costs a lone wave ~2 us of
-    // latency, a unit combine ~0.15 us); steps / 2^k units balance the two
+    // latency, a unit combine ~0.15 us); steps / 2^k units balance the two (tools/latency.py). Long records pass
+    // CHUNK_LOG2: the kernel's scan then picks (run_unit_log2).
     const size_t steps = ((aadlen + 15) / 16 + (len + 15) / 16 + 1 + ENGINE_G - 1) / ENGINE_G;
     const u32 unit_log2 = steps <= 24 ? 0 : steps <= 96 ? 1 : steps <= 400 ? 2 : steps <= 1600 ? 3 : CHUNK_LOG2;
     const hipStream_t s = call.stream();

@@ -150,6 +150,7 @@ __device__ __forceinline__ unsigned long long stamp()
 #define RC_UNITS 4   // units in the run
 #define RC_HUGE 5    // records whose front unit goes first (longer than CHUNK_MAX_UNITS units)
 #define RC_CLAIM 6   // the first wave to find this run's queue empty scans the next run
+#define RC_LOG2 7    // the run's unit length: 2^RC_LOG2 steps (run_unit_log2)
 
 // Scans the run that starts at record p into one run-state buffer, with ONE wave and no workgroup barrier, so that it
 // runs while the other waves are still busy with the previous run (the end-of-run tail where they would otherwise
@@ -161,6 +162,22 @@ __device__ __forceinline__ unsigned long long stamp()
 // workgroup waits for: the critical path of a launch of one record) stops the loops at the run's last 64-record block
 // and skips the sort for a lone record; the scans in the run tails keep the plain loops, whose registers the unit loop
 // shares (the guarded form adds VGPR spills to the open kernel).
+// Unit length of a cut run (2^log2 steps, at most 2^cap) when the launch leaves it to the scan (args.unit_log2 ==
+// CHUNK_LOG2): the longest that still gives at least 64 units (half the workgroup's 128 groups; shorter units would
+// not shorten the run, only add per-unit work), but long enough that a record's unit combine chains at most 36
+// partials (a chain is serial, ~0.15 us a link; 36 admits a 16 KiB TLS record, 129 steps, in 4-step units). Big
+// batches keep 2 KiB units; a run of a few records -- a small batch -- is cut finer, so its records spread over the
+// waves. (A launch of one record passes its own length rule, single() in aesgcm_engine.hip.)
+__device__ __forceinline__ u32 run_unit_log2(u32 total_steps, u32 smax, u32 cap)
+{
+    u32 fill = 0, chain = 0;
+    while (fill < cap && (total_steps >> (fill + 1)) >= (u32)(ENGINE_WG / ENGINE_G / 2))
+        ++fill;
+    while (chain < cap && ((smax + (1u << chain) - 1) >> chain) > 36u)
+        ++chain;
+    return fill > chain ? fill : chain;
+}
+
 template <bool OPEN, int FRAME, bool FIRST = false>
 __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355x_record_t *__restrict__ recs, u64 p, u64 end,
                                       lds_u32 *rs)
@@ -168,7 +185,6 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
     constexpr u32 Q = CRUN_RECS / 64;
     lds_u32 *ubase = rs + RUN_UBASE_OFF, *done = rs + RUN_DONE_OFF, *front = rs + RUN_FRONT_OFF;
     const u32 lane = lane_here();
-    const u32 log2 = args.unit_log2, ustep = 1u << log2;
     const u32 lim = (u32)min(end - p, (u64)CRUN_RECS);
     const u32 key = args.multi_key ? recs[p].key_idx : 0u;
     if (key < args.nkeys)  // the key entry (round keys, IV, H powers) moves to LDS now, off the next run's critical path
@@ -187,13 +203,6 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
             if (!record_ok<FRAME>(args, r))  // rejected: one empty unit (see the unit loop)
                 r.len = 0, r.aad_len = 0, r.flags = 0;
             steps[q] = gcm_steps<OPEN, FRAME>(r);
-            // front-unit size bucket: 0 = a record too long for CHUNK_MAX_UNITS units (it takes units of a multiple
-            // length, unit_mul), else ustep + 1 - size of the record's first unit (1 = a full unit, ustep = one step)
-            const u32 mul = unit_mul(steps[q], log2);
-            nc[q] = (steps[q] + ustep - 1) >> log2;
-            if (mul > 1)  // rare: the only division
-                nc[q] = (steps[q] + mul * ustep - 1) / (mul * ustep);
-            bkt[q] = mul > 1 ? 0u : ustep + 1 - (steps[q] - (nc[q] - 1) * ustep);
         }
         const u64 kb = __ballot(other);
         if (kb != 0)
@@ -213,8 +222,26 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
     const bool whole = smax <= smin + UNIFORM_SLACK && end - p >= WHOLE_MIN_RECS;
     if (whole && !args.multi_key)
         n = (u32)min(end - p, (u64)WHOLE_RUN_RECS);
-    u32 units = n, nhuge = 0;
+    u32 units = n, nhuge = 0, log2 = args.unit_log2;
     if (!whole) {
+        u32 tot = 0;
+#pragma unroll
+        for (u32 q = 0; q < Q; ++q)
+            tot += q * 64 + lane < n ? steps[q] : 0u;
+        const u32 incl = wave_incl_sum(tot);
+        if (log2 == CHUNK_LOG2)
+            log2 = run_unit_log2((u32)__builtin_amdgcn_readlane((int)incl, 63), smax, CHUNK_LOG2);
+        const u32 ustep = 1u << log2;
+#pragma unroll
+        for (u32 q = 0; q < Q; ++q) {
+            // front-unit size bucket: 0 = a record too long for CHUNK_MAX_UNITS units (it takes units of a multiple
+            // length, unit_mul), else ustep + 1 - size of the record's first unit (1 = a full unit, ustep = one step)
+            const u32 mul = unit_mul(steps[q], log2);
+            nc[q] = (steps[q] + ustep - 1) >> log2;
+            if (mul > 1)  // rare: the only division
+                nc[q] = (steps[q] + mul * ustep - 1) / (mul * ustep);
+            bkt[q] = mul > 1 ? 0u : ustep + 1 - (steps[q] - (nc[q] - 1) * ustep);
+        }
         // unit prefix in record order; the first record whose units overflow the run's partial slots ends the run
         // (never the first record)
         u32 carry = 0, cut = n;
@@ -285,6 +312,7 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
         rs[RC_UNITS] = units;
         rs[RC_HUGE] = nhuge;
         rs[RC_CLAIM] = 0;
+        rs[RC_LOG2] = log2;
     }
 }
 
@@ -315,13 +343,10 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     const u32 wave = threadIdx.x >> 6;
     const u32 tsel_horner = 0x10000u + (u32)(G - 1) * GHASH_TABLE_BYTES;
     const u32 tsel_chunk = 0x10000u + 8u * GHASH_TABLE_BYTES;
-    // unit length in steps (a power of two <= CHUNK_STEPS) and the key element of its combine power H^(G * ustep)
-    const u32 ustep = 1u << args.unit_log2;
-    const u32 usrc = ustep == CHUNK_STEPS ? 8u : args.unit_log2 == 0 ? 7u : 8u + args.unit_log2;  // [9..12]: H^16..H^128
 
     const u64 n = args.nrecs;
     const u64 beg = n * blockIdx.x / gridDim.x, end = n * (blockIdx.x + 1) / gridDim.x;
-    u32 loaded_key = 0xffffffffu;
+    u32 loaded_key = 0xffffffffu, loaded_usrc = 0xffffffffu;
     // the descriptors in batch order, or (an ungrouped many-key batch) the key-grouped copy built on the device; ok
     // bytes go to the record's batch index either way
     const ptls_mi355x_record_t *recs = args.recs;
@@ -354,6 +379,10 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         const bool whole = __builtin_amdgcn_readfirstlane(rs[RC_WHOLE]);
         const u32 total_units = __builtin_amdgcn_readfirstlane(rs[RC_UNITS]);
         const u32 nhuge = __builtin_amdgcn_readfirstlane(rs[RC_HUGE]);
+        // the run's unit length in steps (a power of two <= CHUNK_STEPS) and the key element of its combine power
+        // H^(G * ustep): [7] = H^8, [9..12] = H^16..H^128, [8] = H^CHUNK_BLOCKS
+        const u32 ulog2 = __builtin_amdgcn_readfirstlane(rs[RC_LOG2]), ustep = 1u << ulog2;
+        const u32 usrc = ustep == CHUNK_STEPS ? 8u : ulog2 == 0 ? 7u : 8u + ulog2;
         const u32 nfull = total_units - run_n;
         const u64 run_end = pos + run_n;
         PROF_STAMP(t1);
@@ -371,10 +400,12 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         }
         typedef __attribute__((address_space(3))) const KeyEntry lds_key_t;
         lds_key_t *key = (lds_key_t *)(rs + RUN_KEY_OFF);  // staged by the scanner
-        if (key_idx != loaded_key) {
-            build_ghash_tables(lds, key, 9, usrc);  // H^1..H^8 and the unit combine power
+        if (key_idx != loaded_key || (!whole && usrc != loaded_usrc)) {
+            // H^1..H^8 and the unit combine power (only the latter when just the unit length changed)
+            build_ghash_tables(lds, key, 9, usrc, key_idx != loaded_key ? 0u : 8u);
             __syncthreads();
             loaded_key = key_idx;
+            loaded_usrc = usrc;
             if (threadIdx.x == 0)
                 PROF_ADD(7, 1);
         }
@@ -435,7 +466,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             }
             const u32 steps = gcm_steps<OPEN, FRAME>(r);
             // unit [m_lo, m_hi) of the record's steps (whole mode: the record); huge records take longer units
-            const u32 mul = whole ? 1u : unit_mul(steps, args.unit_log2);
+            const u32 mul = whole ? 1u : unit_mul(steps, ulog2);
             u32 m_hi = steps, m_lo = 0;
             if (!whole) {
                 const u32 ulen = mul * ustep;

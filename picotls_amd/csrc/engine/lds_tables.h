@@ -35,9 +35,9 @@ __device__ void build_aes_tables(lds_u8 *lds)
 // order, and entry n ^ c = e(n) ^ e(c): at store n a lane writes slot n ^ (p mod 16), spreading a wave's 16-byte stores
 // over the bank groups. A few hundred VALU operations per thread: the build is a small part of a launch of one record.
 template <typename KeyPtr>  // a KeyEntry in global memory, or its copy staged in LDS (the chunked kernel)
-__device__ void build_ghash_tables(lds_u8 *lds, KeyPtr key, u32 ntables = ENGINE_G, u32 src8 = 8)
+__device__ void build_ghash_tables(lds_u8 *lds, KeyPtr key, u32 ntables = ENGINE_G, u32 src8 = 8, u32 first = 0)
 {
-    for (u32 idx = threadIdx.x; idx < ntables * 32; idx += blockDim.x) {
+    for (u32 idx = first * 32 + threadIdx.x; idx < ntables * 32; idx += blockDim.x) {
         const u32 t = idx >> 5, p = idx & 31;
         const auto *h = key->h[t == 8 ? src8 : t];  // table 8: the unit combine power (chunked kernel)
         u32 b0 = bswap32(h[0]), b1 = bswap32(h[1]), b2 = bswap32(h[2]), b3 = bswap32(h[3]);

@@ -52,7 +52,7 @@ struct BatchArgs {
     uint8_t *ok;
     u32 multi_key;  // 0: every record uses key 0 (no key-run scan)
     u32 nkeys;      // records whose key_idx >= nkeys are skipped (open: ok = 0)
-    u32 unit_log2;  // chunked kernel: units of 2^unit_log2 steps (<= CHUNK_STEPS; smaller for a launch of one record)
+    u32 unit_log2;  // chunked kernel: units of 2^unit_log2 steps; CHUNK_LOG2 = each run's scan picks (run_unit_log2)
     // chunked kernel, ungrouped many-key batches (key_*_kernel): when *perm_on != 0 the kernel walks `grouped` (the
     // descriptors in key order) and perm[i] is the batch index of grouped[i] (for the ok bytes)
     const ptls_mi355x_record_t *grouped;
