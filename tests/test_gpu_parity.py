@@ -213,6 +213,38 @@ def test_random_batch_vs_fusion(ref, key_size, nkeys, sort_keys, schedule):
     assert not back[~m].any()  # nothing outside the records was written
 
 
+@pytest.mark.parametrize("key_size", [16, 32])
+def test_unit_length_changes_between_runs_vs_fusion(ref, key_size):
+    # every workgroup (600 records of a 256 x 600 batch) walks a block of 300 short records then 300 long ones, so its
+    # runs get different unit lengths from their scans (run_unit_log2: 8-step, 1-step, then 16-step units) and the
+    # combine table is rebuilt under one key between runs; plus a small batch of long records (4-step units, chains of
+    # up to 36 partials)
+    rng = np.random.default_rng(4242 + key_size)
+    blocks = []
+    for _ in range(256):
+        blocks.append(rng.integers(64, 300, 300))
+        blocks.append(rng.integers(4000, 16385, 300))
+    for lens, ns in ((np.concatenate(blocks), 256 * 600), (rng.integers(16000, 16500, 90), 90)):
+        b = RecordBatch.build(lens[:ns], rng.integers(0, 30, ns), seqs=rng.integers(0, 2**40, ns, dtype=np.uint64))
+        keys, ivs = np.frombuffer(rng.bytes(key_size), np.uint8), np.frombuffer(rng.bytes(12), np.uint8)
+        pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+        aad = np.frombuffer(rng.bytes(max(b.aad_bytes, 1)), np.uint8)
+        ks = pa.Keyset(keys, ivs, key_size)
+        sealed = gpu_seal(ks, b.seal, pt, aad, b.sealed_bytes)
+        expect = np.zeros(b.sealed_bytes, np.uint8)
+        ref.run_batch(True, keys, ivs, key_size, b.seal, pt, aad, expect, nthreads=8)
+        assert np.array_equal(sealed, expect)
+        bad = expect.copy()
+        victims = rng.choice(ns, 5, replace=False)
+        for v in victims:
+            bad[int(b.seal[v]["out_off"]) + int(b.seal[v]["len"])] ^= 1
+        back, ok = gpu_open(ks, b.open, bad, aad, b.pt_bytes)
+        assert sorted(np.nonzero(ok != 1)[0].tolist()) == sorted(victims.tolist())
+        m = record_mask(b.seal, b.pt_bytes)
+        assert np.array_equal(back[m], pt[m])
+        ks.free()
+
+
 @pytest.mark.parametrize("schedule", SCHEDULES)
 def test_every_length_0_to_300_vs_oracle(oracle, schedule):
     # all stream layouts around the G-lane boundaries (partial blocks, AAD-only, empty records)
