@@ -228,9 +228,9 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
 #pragma unroll
         for (u32 q = 0; q < Q; ++q)
             tot += q * 64 + lane < n ? steps[q] : 0u;
-        const u32 incl = wave_incl_sum(tot);
+        const u32 tot_incl = wave_incl_sum(tot);
         if (log2 == CHUNK_LOG2)
-            log2 = run_unit_log2((u32)__builtin_amdgcn_readlane((int)incl, 63), smax, CHUNK_LOG2);
+            log2 = run_unit_log2((u32)__builtin_amdgcn_readlane((int)tot_incl, 63), smax, CHUNK_LOG2);
         const u32 ustep = 1u << log2;
 #pragma unroll
         for (u32 q = 0; q < Q; ++q) {
@@ -336,10 +336,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     constexpr int G = ENGINE_G;
     constexpr int RPW = 64 / G;
 
-    const u32 lane = threadIdx.x & 63;
-    const u32 j = lane % G;
-    const u32 slot = lane / G;
-    const u32 laneoff = (lane & 31) * 4;
+    // (the lane index and what derives from it are computed in the unit loop, lane_here())
     const u32 wave = threadIdx.x >> 6;
     const u32 tsel_horner = 0x10000u + (u32)(G - 1) * GHASH_TABLE_BYTES;
     const u32 tsel_chunk = 0x10000u + 8u * GHASH_TABLE_BYTES;
@@ -516,7 +513,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         // the run's units are all handed out: the first wave to get here scans the next run into the other buffer
         // while the rest finish theirs
         u32 claim = 0;
-        if (lane == 0)
+        if (lane_here() == 0)
             claim = atomicAdd((u32 *)&rs[RC_CLAIM], 1u) == 0;
         if (__builtin_amdgcn_readfirstlane(claim) && run_end < end)
             scan_run<OPEN, FRAME>(args, recs, run_end, end, rs_next);
@@ -524,7 +521,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         __syncthreads();  // the run's tables, partials and counters are free again
         PROF_STAMP(t3);
 #if ENGINE_PROFILE
-        if (lane == 0)
+        if (lane_here() == 0)
             PROF_ADD(4, t3 - tw);
         if (threadIdx.x == 0) {
             PROF_ADD(0, t1 - t0);
