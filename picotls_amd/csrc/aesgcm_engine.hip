@@ -618,10 +618,16 @@ void ptls_mi355x_keyset_free(ptls_mi355x_keyset_t *ks)
 int ptls_mi355x_debug_profile(unsigned long long *out, int reset)
 {
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(g_prof)));
+    static unsigned long long rows[PROF_ROWS][16];
+    HIP_TRY(hipMemcpyFromSymbol(rows, HIP_SYMBOL(g_prof), sizeof(g_prof)));
+    for (int i = 0; i < 16; ++i) {
+        out[i] = 0;
+        for (int r = 0; r < PROF_ROWS; ++r)
+            out[i] += rows[r][i];
+    }
     if (reset) {
-        static const unsigned long long z[16] = {};
-        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));
+        memset(rows, 0, sizeof(rows));
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), rows, sizeof(g_prof)));
     }
     return 0;
 }

@@ -120,13 +120,16 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
 }
 
 // Diagnostic build only (-DENGINE_PROFILE=1): s_memtime stamps of the chunked kernel's phases, summed over runs and
-// workgroups: [0] run setup, [1] GHASH table build, [2] unit loop, [3] kernel prologue (AES tables), [4] wave idle at the unit-loop barrier,
+// workgroups: [0] run setup, [1] GHASH table build, [2] unit loop, [3] kernel prologue (AES tables, first scan), [4] wave idle at the unit-loop barrier,
 // [5] units, [6] runs, [7] table builds.
 #ifndef ENGINE_PROFILE
 #define ENGINE_PROFILE 0
 #endif
 #if ENGINE_PROFILE
-__device__ unsigned long long g_prof[16];
+// one row of counters per workgroup (blockIdx.x mod PROF_ROWS): the rows are summed on the host, so the counter
+// atomics of 256 workgroups do not queue on one address inside the phases they measure
+#define PROF_ROWS 1024
+__device__ unsigned long long g_prof[PROF_ROWS][16];
 __device__ __forceinline__ unsigned long long stamp()
 {
     unsigned long long t;
@@ -136,7 +139,7 @@ __device__ __forceinline__ unsigned long long stamp()
     return t;
 }
 #define PROF_STAMP(v) const unsigned long long v = stamp()
-#define PROF_ADD(i, x) atomicAdd(&g_prof[i], (unsigned long long)(x))
+#define PROF_ADD(i, v) atomicAdd(&g_prof[blockIdx.x % PROF_ROWS][i], (unsigned long long)(v))
 #else
 #define PROF_STAMP(v)
 #define PROF_ADD(i, x)
@@ -159,8 +162,8 @@ __device__ __forceinline__ unsigned long long stamp()
 // Outputs: ctl[RC_*], ubase[0..n] (prefix of unit counts), front[] (records ordered [very long][the others by
 // front-unit size, largest first]; the kernel numbers units [their front units][all full units][the other front
 // units]) and done[0..n) = 0. All lanes of the wave must be active. FIRST (a launch's first run, which the whole
-// workgroup waits for: the critical path of a launch of one record) stops the loops at the run's last 64-record block
-// and skips the sort for a lone record; the scans in the run tails keep the plain loops, whose registers the unit loop
+// workgroup waits for: the critical path of a launch of one record) stops the loops at the run's last 64-record block,
+// skips the sort for a lone record and ranks a run of at most 64 records directly; the scans in the run tails keep the plain loops, whose registers the unit loop
 // shares (the guarded form adds VGPR spills to the open kernel).
 // Unit length of a cut run (2^log2 steps, at most 2^cap) when the launch leaves it to the scan (args.unit_log2 ==
 // CHUNK_LOG2): the longest that still gives at least 64 units (half the workgroup's 128 groups; shorter units would
@@ -265,6 +268,20 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
             nhuge = __builtin_amdgcn_readfirstlane(bkt[0]) == 0;
             if (lane == 0)
                 front[0] = 0;
+        } else if (FIRST && n <= 64) {
+            // a small first run (a small batch, one record per lane): each lane ranks its record by (bucket, index)
+            // against the others, n readlanes instead of the sort's 2 x (CHUNK_STEPS + 1) ballot passes
+            const u32 mine = bkt[0];
+            u32 rank = 0, huge = 0;
+#pragma unroll 1
+            for (u32 i = 0; i < n; ++i) {
+                const u32 bi = (u32)__builtin_amdgcn_readlane((int)bkt[0], (int)i);
+                rank += bi < mine || (bi == mine && i < lane) ? 1u : 0u;
+                huge += bi == 0 ? 1u : 0u;
+            }
+            nhuge = __builtin_amdgcn_readfirstlane(huge);
+            if (lane < n)
+                front[rank] = lane;
         } else {
             // counting sort of the records by front-unit bucket: lane b counts bucket b, then an exclusive scan over
             // lanes
@@ -352,15 +369,22 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         recs = args.grouped, perm = args.perm;
     auto ok_at = [&](u64 i) -> u64 { return perm != nullptr ? (u64)perm[i] : i; };
 
-    build_aes_tables(lds);
-    PROF_STAMP(ta);
-    // the first run's state (later runs are scanned during the previous run's tail)
-    if (wave == 0 && beg < end)
-        scan_run<OPEN, FRAME, true>(args, recs, beg, end, (lds_u32 *)(lds + CLDS_RUN0));
+    // the first run's state on wave 0 (later runs are scanned during the previous run's tail) while waves 1.. copy
+    // the AES tables
+    if (wave == 0) {
+        if (beg < end)
+            scan_run<OPEN, FRAME, true>(args, recs, beg, end, (lds_u32 *)(lds + CLDS_RUN0));
 #if ENGINE_PROFILE
-    if (threadIdx.x == 0)
-        PROF_ADD(8, ta - tk), PROF_ADD(9, stamp() - ta), PROF_ADD(10, 1);
+        if (threadIdx.x == 0)
+            PROF_ADD(9, stamp() - tk), PROF_ADD(10, 1);
 #endif
+    } else {
+        build_aes_tables(lds, 64);
+#if ENGINE_PROFILE
+        if (threadIdx.x == 64)
+            PROF_ADD(8, stamp() - tk);
+#endif
+    }
     __syncthreads();
 
     u32 rb = 0;  // run-state buffer of the current run

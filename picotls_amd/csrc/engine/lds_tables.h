@@ -5,20 +5,68 @@
 
 // ------------------------------------------------------------------------------------------------ LDS tables
 
+#ifndef AES_TTAB_COPY
+#define AES_TTAB_COPY 1
+#endif
+
 // AES T-table: Te0 replicated into banks 0..31 (bytes 0..127 of row n), Te2 = rotl16(Te0) into bytes 128..255
-__device__ void build_aes_tables(lds_u8 *lds)
+constexpr u32 aes_ttab_word(const SboxTable &sb, u32 idx)
 {
+    const u32 s = sb.v[(idx >> 6) & 255];
+    const u32 s2 = ((s << 1) ^ ((s & 0x80) ? 0x1b : 0)) & 0xff;
+    const u32 te0 = s2 | s << 8 | s << 16 | (s2 ^ s) << 24;
+    return (idx & 63) < 32 ? te0 : ((te0 << 16) | (te0 >> 16));
+}
+
+// The whole 64 KiB LDS image of the table, derived at compile time into the code object: a launch copies it with
+// 16-byte loads (L2 hits after the first workgroup of an XCD) instead of deriving it
+struct alignas(16) AesTtabImage {
+    u32 v[256 * 64];
+};
+constexpr AesTtabImage make_aes_ttab()
+{
+    const SboxTable sb = make_sbox();
+    AesTtabImage t = {};
+    for (u32 idx = 0; idx < 256 * 64; ++idx)
+        t.v[idx] = aes_ttab_word(sb, idx);
+    return t;
+}
+__device__ const AesTtabImage g_aes_ttab = make_aes_ttab();
+
+// Threads [skip, blockDim.x) build it (skip: a multiple of 64; the chunked kernel's wave 0 scans meanwhile)
+__device__ void build_aes_tables(lds_u8 *lds, u32 skip = 0)
+{
+    const u32 tid = threadIdx.x - skip, nthr = blockDim.x - skip;
+#if AES_TTAB_COPY
+    const u32x4 *src = (const u32x4 *)g_aes_ttab.v;
+    lds_u32x4 *dst = (lds_u32x4 *)lds;
+    // every thread's loads are in flight before its first LDS write
+    for (u32 base = 0; base < 256 * 64 / 4; base += 4 * nthr) {
+        u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const u32 idx = base + tid + k * nthr;
+            v[k] = idx < 256 * 64 / 4 ? src[idx] : u32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const u32 idx = base + tid + k * nthr;
+            if (idx < 256 * 64 / 4)
+                dst[idx] = v[k];
+        }
+    }
+#else
     lds_u32 *t = (lds_u32 *)lds;
     // entry n = idx >> 6 is wave-uniform (blockDim.x is a multiple of 64): scalar S-box loads, 16 in flight per batch,
     // so a launch pays one memory latency here instead of one per loop trip (the per-record path is a launch of one)
-    for (u32 base = 0; base < 256 * 64; base += 16 * blockDim.x) {
+    for (u32 base = 0; base < 256 * 64; base += 16 * nthr) {
         u32 sv[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k)
-            sv[k] = c_sbox.v[__builtin_amdgcn_readfirstlane((base + threadIdx.x + k * blockDim.x) >> 6) & 255u];
+            sv[k] = c_sbox.v[__builtin_amdgcn_readfirstlane((base + tid + k * nthr) >> 6) & 255u];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            const u32 idx = base + threadIdx.x + k * blockDim.x, slot = idx & 63;
+            const u32 idx = base + tid + k * nthr, slot = idx & 63;
             const u32 s = sv[k];
             const u32 s2 = ((s << 1) ^ ((s & 0x80) ? 0x1b : 0)) & 0xff;
             const u32 te0 = s2 | s << 8 | s << 16 | (s2 ^ s) << 24;
@@ -26,6 +74,7 @@ __device__ void build_aes_tables(lds_u8 *lds)
                 t[idx] = slot < 32 ? te0 : ((te0 << 16) | (te0 >> 16));
         }
     }
+#endif
 }
 
 // GHASH window tables of one key: table t (element key->h[t]), window p (x^(4p)..x^(4p+3)), entry n (4-bit value,

@@ -781,11 +781,12 @@ def test_ungrouped_many_key_batch_regrouped_on_device(ref, nkeys, frac_bad):
 
 # n = 1, 2, 33: one workgroup or a few; n = 256 * k: k records per workgroup on a 256-CU MI355X (one persistent
 # workgroup per CU once a batch has >= 32 records per CU)
-@pytest.mark.parametrize("n", [1, 2, 33, 256 * 63, 256 * 64, 256 * 65, 256 * 129, 256 * 256])
+@pytest.mark.parametrize("n", [1, 2, 33, 300, 1000, 256 * 63, 256 * 64, 256 * 65, 256 * 129, 256 * 256])
 def test_first_run_sizes(ref, n):
     # a launch's first run is scanned by the guarded scan (scan_run<..., FIRST>): its loops stop at the run's last
-    # 64-record block and a lone record skips the front-unit sort; workgroup shares around those block edges, with
-    # mixed lengths so that runs are cut into units (not whole-record mode), one record longer than 1024 units
+    # 64-record block, a lone record skips the front-unit sort and a run of at most 64 records is ranked directly;
+    # workgroup shares around those edges, with mixed lengths so that runs are cut into units (not whole-record mode),
+    # one record longer than 1024 units
     rng = np.random.default_rng(640 + n)
     lens = rng.integers(0, 40000 if n < 64 else 3000, n)
     lens[int(rng.integers(0, n))] = (3 << 20) + 5

@@ -57,7 +57,7 @@ def main():
     for i, name in enumerate(["run setup", "table build", "unit loop", "prologue"]):
         print(f"  {name:12s} {p[i] / runs:10.0f} cycles/run  {100 * p[i] / max(tot, 1):5.1f} %")
     if p[10]:
-        print("  prologue split (cycles/workgroup, thread 0): tables (wave 1) %.0f | first run scan (wave 0) %.0f" %
+        print("  prologue split (cycles/workgroup): AES tables (waves 1-15) %.0f | first run scan (wave 0) %.0f" %
               (p[8] / p[10], p[9] / p[10]))
     waves = 16
     print(f"  wave idle at unit-loop barrier: {p[4] / runs / waves:.0f} cycles/run/wave "
