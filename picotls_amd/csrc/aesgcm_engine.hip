@@ -29,6 +29,7 @@
 
 #include <hip/hip_runtime.h>
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <new>
 #include <type_traits>
@@ -37,6 +38,7 @@
 #include <stdint.h>
 #include <string.h>
 #include <stdio.h>
+#include <sched.h>
 
 #include "picotls/mi355x.h"
 
@@ -107,6 +109,14 @@ struct PendingSlot {
     hipEvent_t cleared;
 };
 
+struct OneCall;
+struct Combiner {  // per-record calls of one kind waiting for a launch (submit)
+    std::mutex mu;
+    std::vector<OneCall *> q;
+    int inflight = 0;
+    size_t expect = 1;  // calls in the last batch: a caller that could lead waits briefly until as many have queued
+};
+
 struct DeviceState {
     int device = 0, ncu = 0;
     hipStream_t setup = nullptr;  // one-key and many-key setup launches (never waits on anything)
@@ -121,6 +131,8 @@ struct DeviceState {
     std::vector<KeyEntry *> slots;
     std::vector<PendingSlot> pending;
     std::vector<hipEvent_t> events;
+    int combine = 2;              // PTLS_MI355X_COMBINE: combined per-record launches in flight per kind (0: none)
+    Combiner comb[32];
 };
 
 static std::atomic<DeviceState *> g_devs[MAX_DEVICES];
@@ -182,6 +194,9 @@ static DeviceState *device_state(int dev)
     ds->force_copy = copy != nullptr && strcmp(copy, "1") == 0;
     const char *ct = getenv("PTLS_MI355X_CONSTANT_TIME");
     ds->ct_default = ct != nullptr && strcmp(ct, "1") == 0;
+    const char *comb = getenv("PTLS_MI355X_COMBINE");
+    if (comb != nullptr)
+        ds->combine = atoi(comb) < 0 ? 0 : atoi(comb);
     ds->stage_limit = limit != nullptr ? (size_t)strtoull(limit, nullptr, 0) : (size_t)4096 << (STAGE_CLASSES - 1);
     int least = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &ds->priority) != hipSuccess)
@@ -698,10 +713,12 @@ static void launch_chunked(bool ct, unsigned grid, hipStream_t s, const BatchArg
 static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int schedule, bool ct, bool open,
                       const ptls_mi355x_record_t *recs, size_t nrecs, const void *in, const void *aad, void *out, uint8_t *ok,
                       hipStream_t s, int frame, u32 unit_log2, const ptls_mi355x_record_t *grouped = nullptr,
-                      const u32 *perm = nullptr, const u32 *perm_on = nullptr)
+                      const u32 *perm = nullptr, const u32 *perm_on = nullptr, const ptls_mi355x_record_t *one = nullptr)
 {
     BatchArgs a = {keys, recs, (u64)nrecs, (const uint8_t *)in, (const uint8_t *)aad, (uint8_t *)out, ok,
-                   nkeys > 1 ? 1u : 0u, nkeys, unit_log2, grouped, perm, perm_on};
+                   nkeys > 1 ? 1u : 0u, nkeys, unit_log2, grouped, perm, perm_on, 0u, {}};
+    if (one != nullptr && nrecs == 1)  // the chunked kernel takes a lone record's descriptor from its arguments
+        a.one_inline = 1, a.one = *one;
     if (a.aad == NULL)
         a.aad = a.in;
     // one persistent workgroup per CU. A batch with fewer records than CUs takes one workgroup per record.
@@ -995,8 +1012,223 @@ struct StageCall {
 // after a synchronous call on `ks` completed on a stager stream, its setup is complete too
 static void seen_ready(ptls_mi355x_keyset_t *ks) { ks->ready_seen.store(true, std::memory_order_release); }
 
+// ---- per-record calls, combined across threads
+//
+// picotls' per-record calls are synchronous, so one thread's records can never share a launch -- but the calls of
+// several threads can. A call of a one-key keyset (a picotls context) goes to its device's combiner for its kind (seal
+// or open, AES-128 or -256, constant-time or not, header-protection key size): when fewer than `combine` launches of
+// that kind are in flight it takes every queued call, itself included, into one batch (flat combining); otherwise it
+// queues and waits until a batch that took it completes, or until a launch slot frees and it can take the queue
+// itself. A lone caller thus launches at once, as before, while N threads calling together share launches instead of
+// queueing theirs on the device's few hardware queues (tools/mt_records.py). The entries of one-key keysets live in
+// per-device slabs, so a combined batch addresses them as key indices from the lowest entry of the batch.
+// PTLS_MI355X_COMBINE=k sets the launches in flight per kind (default 2); 0 runs every call on its own.
+
+struct OneCall {
+    ptls_mi355x_keyset_t *ks;
+    size_t key_idx;
+    bool open;
+    void *output;
+    const ptls_mi355x_iovec_t *vec;
+    size_t incnt, len;
+    uint64_t seq;
+    const void *aad;
+    size_t aadlen;
+    int *verified;
+    ptls_mi355x_keyset_t *hp_ks;  // header-protection mask of the sealed output's sample (fusion's supp) when set
+    size_t hp_key_idx, sample_off;
+    void *mask;
+    int ret = -1;
+    char err[sizeof(g_err)] = {};
+    std::atomic<bool> done{false};
+    const KeyEntry *entry() const { return ks->d_keys + key_idx; }
+    const KeyEntry *hp_entry() const { return hp_ks->d_keys + hp_key_idx; }
+};
+
+#define COMBINE_MAX_CALLS 256               // calls per combined launch
+#define COMBINE_MAX_BYTES ((size_t)65536)   // larger records and AADs run on their own
+#ifndef COMBINE_WAIT_US
+#define COMBINE_WAIT_US 5                   // how long a call that could lead waits for the rest of the last batch's callers
+#endif
+
+// Runs the calls `c[0..n)` (all of one kind) as one batch through one staging buffer and sets each call's ret (and
+// err), then its done flag. Staging layout: [descriptors | hp entries | every call's input and AAD] is read by the
+// device, [every call's output | ok bytes | masks] written (the copy path moves the first part up, the second down).
+static void run_calls(DeviceState *ds, OneCall *const *c, size_t n)
+{
+    const OneCall &c0 = *c[0];
+    const bool open = c0.open, hp = c0.hp_ks != nullptr;
+    const int nr = c0.ks->nr, hp_nr = hp ? c0.hp_ks->nr : 0;
+    auto a16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    // the key indices of the batch: entries from the lowest one of the batch (all of them one-key slab entries when
+    // n > 1; a lone call uses its own keyset's entries as they are)
+    const KeyEntry *kbase = c0.entry(), *hbase = hp ? c0.hp_entry() : nullptr;
+    for (size_t i = 1; i < n; ++i) {
+        kbase = c[i]->entry() < kbase ? c[i]->entry() : kbase;
+        if (hp)
+            hbase = c[i]->hp_entry() < hbase ? c[i]->hp_entry() : hbase;
+    }
+    const size_t off_rec = 0, off_hp = a16(n * sizeof(ptls_mi355x_record_t)), off_data = off_hp + a16(n * sizeof(ptls_mi355x_hp_t));
+    size_t up = off_data;
+    for (size_t i = 0; i < n; ++i)
+        up += a16(c[i]->len + (open ? 16 : 0)) + a16(c[i]->aadlen);
+    size_t off_ok = up;
+    for (size_t i = 0; i < n; ++i)
+        off_ok += a16(c[i]->len + (open ? 0 : 16));
+    const size_t off_mask = off_ok + a16(n), total = off_mask + 16 * n;
+    int ret = -1;
+    {
+        StageCall call(ds);
+        if (call.acquire(total) == 0) {
+            uint8_t *h = call.host(), *d = call.dev();
+            const hipStream_t s = call.stream();
+            u32 nkeys = 1, hp_nkeys = 1;
+            size_t in_at = off_data, out_at = up;
+            ptls_mi355x_record_t first = {};
+            ret = 0;
+            for (size_t i = 0; i < n && ret == 0; ++i) {
+                const OneCall &x = *c[i];
+                const size_t kd = (size_t)(x.entry() - kbase);
+                const size_t inbytes = x.len + (open ? 16 : 0);
+                for (size_t v = 0, off = 0; v < x.incnt; off += x.vec[v].len, ++v)
+                    if (x.vec[v].len != 0)
+                        memcpy(h + in_at + off, x.vec[v].base, x.vec[v].len);
+                const size_t aad_at = in_at + a16(inbytes);
+                if (x.aadlen != 0)
+                    memcpy(h + aad_at, x.aad, x.aadlen);
+                const ptls_mi355x_record_t r = {in_at, out_at, x.seq, (u32)aad_at, (u32)x.len, (u32)kd, (uint16_t)x.aadlen,
+                                                (uint16_t)(x.aadlen >> 16)};
+                memcpy(h + off_rec + i * sizeof(r), &r, sizeof(r));
+                if (i == 0)
+                    first = r;
+                nkeys = (u32)kd + 1 > nkeys ? (u32)kd + 1 : nkeys;
+                if (hp) {
+                    const size_t hd = (size_t)(x.hp_entry() - hbase);
+                    const ptls_mi355x_hp_t e = {out_at + x.sample_off, (u32)hd, 0};
+                    memcpy(h + off_hp + i * sizeof(e), &e, sizeof(e));
+                    hp_nkeys = (u32)hd + 1 > hp_nkeys ? (u32)hd + 1 : hp_nkeys;
+                }
+                in_at = aad_at + a16(x.aadlen);
+                out_at += a16(x.len + (open ? 0 : 16));
+                if (wait_ready(x.ks, s) != 0 || (hp && wait_ready(x.hp_ks, s) != 0))
+                    ret = -1;
+            }
+            // one record on one workgroup: shorter units put more of its waves to work (a unit step costs a lone
+            // wave ~2 us of latency, a unit combine ~0.15 us); steps / 2^k units balance the two (tools/latency.py).
+            // Long records, and batches (one workgroup per record), pass CHUNK_LOG2: the kernel's scan then picks.
+            const size_t steps = ((c0.aadlen + 15) / 16 + (c0.len + 15) / 16 + 1 + ENGINE_G - 1) / ENGINE_G;
+            const u32 unit_log2 = n > 1 ? CHUNK_LOG2 : steps <= 24 ? 0 : steps <= 96 ? 1 : steps <= 400 ? 2 : steps <= 1600 ? 3 : CHUNK_LOG2;
+            if (ret == 0)
+                ret = call.roundtrip(up, [&] {
+                    if (launch_gcm(kbase, nkeys, nr, ds->ncu, c0.ks->schedule, c0.ks->ct, open, (const ptls_mi355x_record_t *)(d + off_rec),
+                                   n, d, d, d, d + off_ok, s, 0, unit_log2, nullptr, nullptr, nullptr, n == 1 ? &first : nullptr) != 0)
+                        return -1;
+                    return !hp ? 0 : launch_hp(hbase, hp_nkeys, hp_nr, ds->ncu, (const ptls_mi355x_hp_t *)(d + off_hp), n, d, d + off_mask, s);
+                });
+            if (ret == 0) {
+                out_at = up;
+                for (size_t i = 0; i < n; ++i) {
+                    OneCall &x = *c[i];
+                    seen_ready(x.ks);
+                    if (hp)
+                        seen_ready(x.hp_ks);
+                    const size_t outbytes = x.len + (open ? 0 : 16);
+                    if (outbytes != 0)
+                        memcpy(x.output, h + out_at, outbytes);
+                    if (open)
+                        *x.verified = h[off_ok + i];
+                    if (hp)
+                        memcpy(x.mask, h + off_mask + 16 * i, 16);
+                    out_at += a16(outbytes);
+                }
+            }
+        }
+    }
+    for (size_t i = 0; i < n; ++i) {
+        c[i]->ret = ret;
+        if (ret != 0)
+            memcpy(c[i]->err, g_err, sizeof(g_err));
+        c[i]->done.store(true, std::memory_order_release);
+    }
+}
+
+// the combiner of a call's kind (index into DeviceState::comb), or -1 when the call runs on its own
+static int combine_kind(const OneCall &c)
+{
+    if (!c.ks->slot || c.ks->schedule == PTLS_MI355X_SCHEDULE_LOCKSTEP || c.len > COMBINE_MAX_BYTES || c.aadlen > COMBINE_MAX_BYTES ||
+        (c.hp_ks != nullptr && !c.hp_ks->slot))
+        return -1;
+    return (c.open ? 1 : 0) | (c.ks->nr == 14 ? 2 : 0) | (c.ks->ct ? 4 : 0) | (c.hp_ks == nullptr ? 0 : c.hp_ks->nr == 14 ? 16 : 8);
+}
+
+static int submit(DeviceState *ds, OneCall *c)
+{
+    const int kind = ds->combine > 0 ? combine_kind(*c) : -1;
+    if (kind < 0) {
+        run_calls(ds, &c, 1);
+    } else {
+        Combiner &cb = ds->comb[kind];
+        std::vector<OneCall *> batch;
+        const auto t_enq = std::chrono::steady_clock::now();
+        std::unique_lock<std::mutex> lk(cb.mu);
+        cb.q.push_back(c);
+        while (!c->done.load(std::memory_order_acquire)) {
+            // a launch slot is free: take the queue -- unless fewer calls have queued than the last batch held and this
+            // call has waited less than COMBINE_WAIT_US: threads whose calls just completed are about to submit their
+            // next ones, and a batch taken at once would hold only the first of them (a lone caller never waits)
+            if (cb.inflight < ds->combine && !cb.q.empty() &&
+                (cb.q.size() >= cb.expect ||
+                 std::chrono::steady_clock::now() - t_enq >= std::chrono::microseconds(COMBINE_WAIT_US))) {
+                // as many queued calls as fit one staging buffer (each call's share is about its bytes up and down)
+                size_t take = 0, bytes = 0;
+                while (take < cb.q.size() && take < COMBINE_MAX_CALLS) {
+                    const OneCall &x = *cb.q[take];
+                    bytes += 2 * x.len + x.aadlen + 128;
+                    if (take > 0 && bytes > ds->stage_limit / 2)
+                        break;
+                    ++take;
+                }
+                batch.assign(cb.q.begin(), cb.q.begin() + (long)take);
+                cb.q.erase(cb.q.begin(), cb.q.begin() + (long)take);
+                ++cb.inflight;
+                cb.expect = take;
+                lk.unlock();
+                // a batch's calls must address their entries as u32 key indices from its lowest entry; a call of
+                // another slab further away than that runs on its own (never expected: slabs are 512 KiB apart)
+                auto near = [&](bool hp_entries) {
+                    const KeyEntry *lo = nullptr, *hi = nullptr;
+                    for (OneCall *x : batch) {
+                        const KeyEntry *e = hp_entries ? x->hp_entry() : x->entry();
+                        lo = lo == nullptr || e < lo ? e : lo, hi = hi == nullptr || e > hi ? e : hi;
+                    }
+                    return (size_t)(hi - lo) < ((size_t)1 << 30);
+                };
+                if (batch.size() == 1 || (near(false) && (batch[0]->hp_ks == nullptr || near(true)))) {
+                    run_calls(ds, batch.data(), batch.size());
+                } else {
+                    for (OneCall *x : batch)
+                        run_calls(ds, &x, 1);
+                }
+                lk.lock();
+                --cb.inflight;
+                continue;
+            }
+            lk.unlock();
+            for (int k = 0; k < 256 && !c->done.load(std::memory_order_acquire); ++k)
+                __builtin_ia32_pause();
+            if (!c->done.load(std::memory_order_acquire))
+                sched_yield();
+            lk.lock();
+        }
+    }
+    if (c->ret != 0)
+        return fail("%s", c->err);
+    return 0;
+}
+
 // one record on host buffers (input as iovecs), optionally with the header-protection mask of a sample of the sealed
-// output under hp_ks (fusion's supp, lib/fusion.c:425-430,636-651): a batch of one through a staging buffer
+// output under hp_ks (fusion's supp, lib/fusion.c:425-430,636-651): a batch of one through a staging buffer, or a
+// share of a batch combined with other threads' calls (submit)
 static int single(ptls_mi355x_keyset_t *ks, size_t key_idx, bool open, void *output, const ptls_mi355x_iovec_t *vec, size_t incnt,
                   size_t len, uint64_t seq, const void *aad, size_t aadlen, int *verified, ptls_mi355x_keyset_t *hp_ks = NULL,
                   size_t hp_key_idx = 0, size_t sample_off = 0, void *mask = NULL)
@@ -1008,53 +1240,11 @@ static int single(ptls_mi355x_keyset_t *ks, size_t key_idx, bool open, void *out
     if (hp_ks != NULL && (hp_key_idx >= hp_ks->nkeys || hp_ks->device != ks->device || sample_off + 16 > len + 16))
         return fail("%s", "single: invalid header-protection arguments");
     DeviceScope scope(ks->device);
-    const size_t inbytes = len + (open ? 16 : 0), outbytes = len + (open ? 0 : 16);
-    // staging: [in | aad | descriptor | hp entry] goes up, [out | ok | mask] comes back
-    const size_t off_in = 0, off_aad = (inbytes + 15) & ~(size_t)15, off_rec = off_aad + ((aadlen + 15) & ~(size_t)15),
-                 off_hp = off_rec + 48, off_out = off_hp + 16, off_ok = off_out + ((outbytes + 15) & ~(size_t)15),
-                 off_mask = off_ok + 16, total = off_mask + 16;
-    StageCall call(ks->ds);
-    if (call.acquire(total) != 0)
-        return -1;
-    const ptls_mi355x_record_t r = {0, 0, seq, 0, (u32)len, 0, (uint16_t)aadlen, (uint16_t)(aadlen >> 16)};
-    uint8_t *h = call.host(), *d = call.dev();
-    for (size_t i = 0, off = 0; i < incnt; off += vec[i].len, ++i)
-        if (vec[i].len != 0)
-            memcpy(h + off_in + off, vec[i].base, vec[i].len);
-    if (aadlen != 0)
-        memcpy(h + off_aad, aad, aadlen);
-    memcpy(h + off_rec, &r, sizeof(r));
-    if (hp_ks != NULL) {
-        const ptls_mi355x_hp_t e = {sample_off, 0, 0};  // key 0 of the one-entry view hp_ks->d_keys + hp_key_idx
-        memcpy(h + off_hp, &e, sizeof(e));
-    }
-    // one record on one workgroup: shorter units put more of its waves to work (a unit step costs a lone wave ~2 us of
-    // latency, a unit combine ~0.15 us); steps / 2^k units balance the two (tools/latency.py). Long records pass
-    // CHUNK_LOG2: the kernel's scan then picks (run_unit_log2).
-    const size_t steps = ((aadlen + 15) / 16 + (len + 15) / 16 + 1 + ENGINE_G - 1) / ENGINE_G;
-    const u32 unit_log2 = steps <= 24 ? 0 : steps <= 96 ? 1 : steps <= 400 ? 2 : steps <= 1600 ? 3 : CHUNK_LOG2;
-    const hipStream_t s = call.stream();
-    if (wait_ready(ks, s) != 0 || (hp_ks != NULL && wait_ready(hp_ks, s) != 0))
-        return -1;
-    if (call.roundtrip(off_out, [&] {
-            if (launch_gcm(ks->d_keys + key_idx, 1, ks->nr, ks->ds->ncu, ks->schedule, ks->ct, open, (const ptls_mi355x_record_t *)(d + off_rec),
-                           1, d + off_in, d + off_aad, d + off_out, d + off_ok, s, 0, unit_log2 < CHUNK_LOG2 ? unit_log2 : CHUNK_LOG2) != 0)
-                return -1;
-            return hp_ks == NULL ? 0
-                                 : launch_hp(hp_ks->d_keys + hp_key_idx, 1, hp_ks->nr, hp_ks->ds->ncu,
-                                             (const ptls_mi355x_hp_t *)(d + off_hp), 1, d + off_out, d + off_mask, s);
-        }) != 0)
-        return -1;
-    seen_ready(ks);
-    if (hp_ks != NULL)
-        seen_ready(hp_ks);
-    if (outbytes != 0)
-        memcpy(output, h + off_out, outbytes);
-    if (open)
-        *verified = h[off_ok];
-    if (hp_ks != NULL)
-        memcpy(mask, h + off_mask, 16);
-    return 0;
+    OneCall c;
+    c.ks = ks, c.key_idx = key_idx, c.open = open, c.output = output, c.vec = vec, c.incnt = incnt, c.len = len, c.seq = seq;
+    c.aad = aad, c.aadlen = aadlen, c.verified = verified, c.hp_ks = hp_ks, c.hp_key_idx = hp_key_idx;
+    c.sample_off = sample_off, c.mask = mask;
+    return submit(ks->ds, &c);
 }
 
 extern "C" {

@@ -122,7 +122,8 @@ __device__ __forceinline__ u32 lane_here()
 #define CLDS_RUN0 (LDS_BYTES + GHASH_TABLE_BYTES)
 #define CLDS_RUN1 (CLDS_RUN0 + 4 * RUN_WORDS)
 #define CLDS_PART (CLDS_RUN1 + 4 * RUN_WORDS)                    // 16 B per unit: GHASH partial
-#define CLDS_ALLOC (CLDS_PART + 16 * CRUN_UNITS)
+#define CLDS_ONE (CLDS_PART + 16 * CRUN_UNITS)                   // a lone record's descriptor (BatchArgs::one)
+#define CLDS_ALLOC (CLDS_ONE + 48)
 static_assert(CLDS_ALLOC <= 160 * 1024, "chunked schedule LDS budget");
 static_assert(CHUNK_BLOCKS % ENGINE_G == 0, "units are whole steps");
 static_assert((CHUNK_STEPS & (CHUNK_STEPS - 1)) == 0 && CHUNK_STEPS <= 32, "unit lengths are powers of two up to 32 steps");

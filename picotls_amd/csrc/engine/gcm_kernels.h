@@ -367,6 +367,15 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     const u32 *perm = nullptr;
     if (args.perm_on != nullptr && *args.perm_on)
         recs = args.grouped, perm = args.perm;
+    if (args.one_inline) {
+        // a lone record's descriptor from the kernel arguments into LDS: the per-record path stages its inputs in
+        // mapped host memory, where reading the descriptor would put a PCIe round trip ahead of everything else
+        recs = (const ptls_mi355x_record_t *)(smem + CLDS_ONE);
+        if (threadIdx.x < sizeof(ptls_mi355x_record_t) / 4)
+            ((lds_u32 *)(lds + CLDS_ONE))[threadIdx.x] = ((const u32 *)&args.one)[threadIdx.x];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // wave 0 writes it and scans it; the other waves read it
+        __builtin_amdgcn_wave_barrier();                          // after the prologue barrier
+    }
     auto ok_at = [&](u64 i) -> u64 { return perm != nullptr ? (u64)perm[i] : i; };
 
     // the first run's state on wave 0 (later runs are scanned during the previous run's tail) while waves 1.. copy

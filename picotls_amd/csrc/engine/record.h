@@ -58,6 +58,10 @@ struct BatchArgs {
     const ptls_mi355x_record_t *grouped;
     const u32 *perm;
     const u32 *perm_on;
+    // chunked kernel, a batch of one (the per-record path): when one_inline != 0 the descriptor is `one` (it travels in
+    // the kernel arguments; `recs` is not read)
+    u32 one_inline;
+    ptls_mi355x_record_t one;
 };
 
 #define RUN_SCAN_CAP 256  // records examined per key-run scan (multi-key batches)

@@ -430,6 +430,7 @@ int main(int argc, char **argv)
     tls12_test(&ptls_mi355x_non_temporal_aes256gcm, &ptls_non_temporal_aes256gcm, &ptls_openssl_sha384, "tls12 aes256gcm wire == fusion");
     threads_test(&ptls_mi355x_aes128gcm, &ptls_fusion_aes128gcm, 8, 60, "aes128gcm threads");
     threads_test(&ptls_mi355x_aes256gcm, &ptls_fusion_aes256gcm, 8, 30, "aes256gcm threads");
+    threads_test(&ptls_mi355x_aes128gcm, &ptls_fusion_aes128gcm, 16, 40, "aes128gcm 16 threads");
     large_test(&ptls_mi355x_aes128gcm, &ptls_fusion_aes128gcm, 17u << 20, 13, "17 MiB record");
     large_test(&ptls_mi355x_aes256gcm, &ptls_fusion_aes256gcm, 3000, 70 << 10, "70 KiB AAD");
     large_test(&ptls_mi355x_aes128gcm, &ptls_fusion_aes128gcm, 1 << 20, (1 << 17) + 3, "1 MiB record, 128 KiB AAD");

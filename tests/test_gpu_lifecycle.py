@@ -80,6 +80,73 @@ def test_threads_with_own_contexts_and_churn(ref):
     assert errors == []
 
 
+def test_combined_per_record_calls_across_threads(ref):
+    # per-record calls of many threads arriving together are combined into shared launches (submit() in
+    # aesgcm_engine.hip): 16 threads, AES-128 and AES-256 contexts, seal, open (a quarter tampered), seal with the
+    # header-protection mask (encrypt_s) and records above the combining cap (64 KiB, run on their own), released in
+    # bursts by a barrier; every output, ok result and mask equals fusion's
+    nthreads, nops = 16, 48
+    barrier = threading.Barrier(nthreads)
+    errors = []
+    plans = []
+    for t in range(nthreads):
+        rng = np.random.default_rng(5000 + t)
+        ks_size = 16 if t % 2 == 0 else 32
+        key, iv, hpkey = rng.bytes(ks_size), rng.bytes(12), rng.bytes(ks_size)
+        ops = []
+        for i in range(nops):
+            ln = int(rng.choice([0, 1, 15, 16, 17, 100, 1200, 1500, 4096, 16384])) if i != 7 else 70000
+            aad, seq, pt = rng.bytes(int(rng.integers(0, 40))), int(rng.integers(0, 2**62)), None
+            pt = rng.bytes(ln)
+            kind = ["enc", "dec", "dec_bad", "enc_s"][i % 4]
+            if kind == "enc_s":
+                so = int(rng.integers(0, ln + 1))
+                want, mask = ref.seal_with_hp(key, iv, seq, aad, pt, hpkey, so)
+                ops.append((kind, pt, seq, aad, (want, mask, so)))
+            else:
+                want = ref.seal(key, iv, seq, aad, pt)
+                if kind == "dec_bad":
+                    want = bytearray(want)
+                    want[int(rng.integers(0, len(want)))] ^= 0x40
+                    want = bytes(want)
+                ops.append((kind, pt, seq, aad, want))
+        plans.append((ks_size, key, iv, hpkey, ops))
+
+    def worker(t):
+        ks_size, key, iv, hpkey, ops = plans[t]
+        alg = pa.aes128gcm if ks_size == 16 else pa.aes256gcm
+        enc, dec, hp = pa.aead_new_direct(alg, True, key, iv), pa.aead_new_direct(alg, False, key, iv), pa.CtrCipher(hpkey)
+        try:
+            for i, (kind, pt, seq, aad, want) in enumerate(ops):
+                if i % 8 == 0:
+                    barrier.wait()
+                if kind == "enc":
+                    ok = enc.encrypt(pt, seq, aad) == want
+                elif kind == "dec":
+                    ok = dec.decrypt(want, seq, aad) == pt
+                elif kind == "dec_bad":
+                    ok = dec.decrypt(want, seq, aad) is None
+                else:
+                    sealed, mask = enc.encrypt_s(pt, seq, aad, hp, want[2])
+                    ok = sealed == want[0] and mask == want[1]
+                if not ok:
+                    errors.append((t, i, kind, len(pt)))
+        except Exception as e:  # noqa: BLE001 -- reported by the assertion below
+            errors.append((t, repr(e)))
+            barrier.abort()
+        finally:
+            enc.free()
+            dec.free()
+            hp.ks.free()
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(nthreads)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert errors == []
+
+
 def test_free_right_after_launch_is_ordered(ref):
     # keyset_free does not wait on the host: it orders the clearing of the key material after the keyset's launches on
     # every stream. A batch launched on a side stream and freed at once still seals correctly, and keysets made right

@@ -608,15 +608,21 @@ def test_schedule_argument_checked():
     assert pa.load_library().ptls_mi355x_keyset_set_schedule(ks.handle, 7) == -1
 
 
-def test_picotls_vtable_pairs():
+@pytest.mark.parametrize("combine", [None, "0", "1"])
+def test_picotls_vtable_pairs(combine):
     # cross-backend pairs in the reference's style (t/picotls.c:224-370): seal with fusion / open with MI355X and back,
-    # through ptls_aead_new_direct + the ptls_aead_algorithm_t objects (tests/c/test_vtable.c)
+    # through ptls_aead_new_direct + the ptls_aead_algorithm_t objects (tests/c/test_vtable.c); its thread tests run the
+    # per-record calls combined across threads (default: 2 launches in flight per kind), each call on its own (0) and
+    # with one launch in flight per kind (1: the largest batches)
     import subprocess
 
     exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "_bin", "test_vtable")
     if not os.path.exists(exe):
         pytest.skip("tests/c/_bin/test_vtable not built (needs picotls headers at build time)")
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=600)
+    env = dict(os.environ)
+    if combine is not None:
+        env["PTLS_MI355X_COMBINE"] = combine
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     assert "not ok" not in r.stdout
 
