@@ -131,7 +131,7 @@ struct DeviceState {
     std::vector<KeyEntry *> slots;
     std::vector<PendingSlot> pending;
     std::vector<hipEvent_t> events;
-    int combine = 2;              // PTLS_MI355X_COMBINE: combined per-record launches in flight per kind (0: none)
+    int combine = 4;              // PTLS_MI355X_COMBINE: combined per-record launches in flight per kind (0: none)
     Combiner comb[32];
 };
 
@@ -966,6 +966,19 @@ int ptls_mi355x_quiclb_batch(ptls_mi355x_keyset_t *ks, const ptls_mi355x_cid_t *
 
 }  // extern "C"
 
+// PTLS_MI355X_COMBINE_STATS=1: per-record launches, calls and the host time of run_calls, printed at exit (tools/gpu_mt.sh)
+static struct CombineStats {
+    std::atomic<uint64_t> launches{0}, calls{0}, ns{0}, wait_ns{0};
+    bool on = getenv("PTLS_MI355X_COMBINE_STATS") != nullptr;
+    ~CombineStats()
+    {
+        if (on && launches.load() != 0)
+            fprintf(stderr, "combine stats: %llu launches, %llu calls (%.2f per launch), %.1f us per launch in run_calls, %.1f us of it waiting\n",
+                    (unsigned long long)launches.load(), (unsigned long long)calls.load(), (double)calls.load() / (double)launches.load(),
+                    (double)ns.load() / 1e3 / (double)launches.load(), (double)wait_ns.load() / 1e3 / (double)launches.load());
+    }
+} g_cstats;
+
 // ---- the synchronous host-buffer helpers (the per-record picotls path)
 //
 // One call = a staging buffer and its stream from the device pool, a host copy of the inputs into it, launches whose
@@ -1004,7 +1017,10 @@ struct StageCall {
             return -1;
         if (copy)
             HIP_TRY(hipMemcpyAsync(st->h + up, st->d + up, total - up, hipMemcpyDeviceToHost, st->stream));
+        const auto t0 = std::chrono::steady_clock::now();
         HIP_TRY(hipStreamSynchronize(st->stream));
+        if (g_cstats.on)
+            g_cstats.wait_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
         return 0;
     }
 };
@@ -1022,7 +1038,10 @@ static void seen_ready(ptls_mi355x_keyset_t *ks) { ks->ready_seen.store(true, st
 // itself. A lone caller thus launches at once, as before, while N threads calling together share launches instead of
 // queueing theirs on the device's few hardware queues (tools/mt_records.py). The entries of one-key keysets live in
 // per-device slabs, so a combined batch addresses them as key indices from the lowest entry of the batch.
-// PTLS_MI355X_COMBINE=k sets the launches in flight per kind (default 2); 0 runs every call on its own.
+// PTLS_MI355X_COMBINE=k sets the launches in flight per kind (default 4); 0 runs every call on its own. Measured
+// (tools/mt_records.c, 1200-byte seals, one box): 16 threads 222K calls/s on their own, 264-269K combined (2.7 calls
+// a launch, p50 57 vs 76 us); 1-8 threads unchanged. A launch costs the host ~34 us (~24 of them waiting for the
+// stream), so calls in flight / 34 us bounds the rate whatever the combining.
 
 struct OneCall {
     ptls_mi355x_keyset_t *ks;
@@ -1051,11 +1070,13 @@ struct OneCall {
 #define COMBINE_WAIT_US 5                   // how long a call that could lead waits for the rest of the last batch's callers
 #endif
 
+
 // Runs the calls `c[0..n)` (all of one kind) as one batch through one staging buffer and sets each call's ret (and
 // err), then its done flag. Staging layout: [descriptors | hp entries | every call's input and AAD] is read by the
 // device, [every call's output | ok bytes | masks] written (the copy path moves the first part up, the second down).
 static void run_calls(DeviceState *ds, OneCall *const *c, size_t n)
 {
+    const auto t_start = std::chrono::steady_clock::now();
     const OneCall &c0 = *c[0];
     const bool open = c0.open, hp = c0.hp_ks != nullptr;
     const int nr = c0.ks->nr, hp_nr = hp ? c0.hp_ks->nr : 0;
@@ -1143,6 +1164,10 @@ static void run_calls(DeviceState *ds, OneCall *const *c, size_t n)
                 }
             }
         }
+    }
+    if (g_cstats.on) {
+        g_cstats.launches += 1, g_cstats.calls += n;
+        g_cstats.ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t_start).count();
     }
     for (size_t i = 0; i < n; ++i) {
         c[i]->ret = ret;

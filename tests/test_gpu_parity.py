@@ -612,7 +612,7 @@ def test_schedule_argument_checked():
 def test_picotls_vtable_pairs(combine):
     # cross-backend pairs in the reference's style (t/picotls.c:224-370): seal with fusion / open with MI355X and back,
     # through ptls_aead_new_direct + the ptls_aead_algorithm_t objects (tests/c/test_vtable.c); its thread tests run the
-    # per-record calls combined across threads (default: 2 launches in flight per kind), each call on its own (0) and
+    # per-record calls combined across threads (default: 4 launches in flight per kind), each call on its own (0) and
     # with one launch in flight per kind (1: the largest batches)
     import subprocess
 

@@ -122,9 +122,11 @@ int main(int argc, char **argv)
             lens[nlens++] = (size_t)atol(argv[i]);
     }
     const int threads[] = {1, 2, 4, 8, 16, 32};
+    const char *only = getenv("MT_THREADS"); /* one thread count instead of the sweep */
     int rc = 0;
     for (int l = 0; l < nlens; ++l)
         for (size_t t = 0; t < sizeof(threads) / sizeof(threads[0]); ++t)
-            rc |= run(threads[t], lens[l], seconds);
+            if (only == NULL || atoi(only) == threads[t])
+                rc |= run(threads[t], lens[l], seconds);
     return rc;
 }
