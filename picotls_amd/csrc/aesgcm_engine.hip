@@ -713,10 +713,11 @@ static void launch_chunked(bool ct, unsigned grid, hipStream_t s, const BatchArg
 static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int schedule, bool ct, bool open,
                       const ptls_mi355x_record_t *recs, size_t nrecs, const void *in, const void *aad, void *out, uint8_t *ok,
                       hipStream_t s, int frame, u32 unit_log2, const ptls_mi355x_record_t *grouped = nullptr,
-                      const u32 *perm = nullptr, const u32 *perm_on = nullptr, const ptls_mi355x_record_t *one = nullptr)
+                      const u32 *perm = nullptr, const u32 *perm_on = nullptr, const ptls_mi355x_record_t *one = nullptr,
+                      u32 *done_flag = nullptr)
 {
     BatchArgs a = {keys, recs, (u64)nrecs, (const uint8_t *)in, (const uint8_t *)aad, (uint8_t *)out, ok,
-                   nkeys > 1 ? 1u : 0u, nkeys, unit_log2, grouped, perm, perm_on, 0u, {}};
+                   nkeys > 1 ? 1u : 0u, nkeys, unit_log2, grouped, perm, perm_on, 0u, {}, done_flag};
     if (one != nullptr && nrecs == 1)  // the chunked kernel takes a lone record's descriptor from its arguments
         a.one_inline = 1, a.one = *one;
     if (a.aad == NULL)
@@ -842,12 +843,12 @@ static int launch_ecb(const KeyEntry *keys, u32 nkeys, int nr, int ncu, const ui
 }
 
 static int launch_hp(const KeyEntry *keys, u32 nkeys, int nr, int ncu, const ptls_mi355x_hp_t *hp, size_t n, const void *base,
-                     void *masks, hipStream_t s)
+                     void *masks, hipStream_t s, u32 *done_flag = nullptr)
 {
     if (nr == 10)
-        hp_kernel<10><<<aux_grid(n, ncu), 256, LDS_AES_BYTES, s>>>(keys, nkeys, hp, (const uint8_t *)base, (uint8_t *)masks, n);
+        hp_kernel<10><<<aux_grid(n, ncu), 256, LDS_AES_BYTES, s>>>(keys, nkeys, hp, (const uint8_t *)base, (uint8_t *)masks, n, done_flag);
     else
-        hp_kernel<14><<<aux_grid(n, ncu), 256, LDS_AES_BYTES, s>>>(keys, nkeys, hp, (const uint8_t *)base, (uint8_t *)masks, n);
+        hp_kernel<14><<<aux_grid(n, ncu), 256, LDS_AES_BYTES, s>>>(keys, nkeys, hp, (const uint8_t *)base, (uint8_t *)masks, n, done_flag);
     HIP_TRY(hipGetLastError());
     return 0;
 }
@@ -966,6 +967,12 @@ int ptls_mi355x_quiclb_batch(ptls_mi355x_keyset_t *ks, const ptls_mi355x_cid_t *
 
 }  // extern "C"
 
+#ifndef PERREC_FLAG
+#define PERREC_FLAG 1                       // a lone record's launch publishes a completion word the host polls (roundtrip)
+#endif
+#define PERREC_FLAG_SPIN_US 2000
+#define PERREC_FLAG_MAX_BYTES ((size_t)1 << 20)  // staged bytes of a call that polls (larger ones wait for the stream)
+
 // PTLS_MI355X_COMBINE_STATS=1: per-record launches, calls and the host time of run_calls, printed at exit (tools/gpu_mt.sh)
 static struct CombineStats {
     std::atomic<uint64_t> launches{0}, calls{0}, ns{0}, wait_ns{0};
@@ -1007,8 +1014,13 @@ struct StageCall {
     uint8_t *dev() const { return st->h_dev != nullptr ? st->h_dev : st->d; }
     hipStream_t stream() const { return st->stream; }
     // runs launch() on the staged buffer: H2D of [0, up) before and D2H of [up, total) after on the copy path; then waits
+    // flag_off (mapped staging only, 0: none): nflags words, one per workgroup of the launch's last kernel, that it sets
+    // once its results are written (BatchArgs::done_flag); the call returns when it sees them all, without the
+    // stream's completion signal (the next user of this stager's stream is ordered after the kernel anyway). After
+    // PERREC_FLAG_SPIN_US without them (a launch queued behind others) the call waits for the stream as usual.
+    bool mapped() const { return st->h_dev != nullptr; }
     template <typename Launch>
-    int roundtrip(size_t up, Launch launch)
+    int roundtrip(size_t up, Launch launch, size_t flag_off = 0, size_t nflags = 0)
     {
         const bool copy = st->h_dev == nullptr;
         if (copy)
@@ -1018,6 +1030,22 @@ struct StageCall {
         if (copy)
             HIP_TRY(hipMemcpyAsync(st->h + up, st->d + up, total - up, hipMemcpyDeviceToHost, st->stream));
         const auto t0 = std::chrono::steady_clock::now();
+        if (flag_off != 0 && !copy) {
+            const u32 *flag = (const u32 *)(st->h + flag_off);
+            size_t seen = 0;  // flags [0, seen) are set
+            for (unsigned k = 0;; ++k) {
+                while (seen < nflags && __atomic_load_n(flag + seen, __ATOMIC_ACQUIRE) != 0)
+                    ++seen;
+                if (seen == nflags) {
+                    if (g_cstats.on)
+                        g_cstats.wait_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+                    return 0;
+                }
+                __builtin_ia32_pause();
+                if ((k & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(PERREC_FLAG_SPIN_US))
+                    break;
+            }
+        }
         HIP_TRY(hipStreamSynchronize(st->stream));
         if (g_cstats.on)
             g_cstats.wait_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
@@ -1096,7 +1124,10 @@ static void run_calls(DeviceState *ds, OneCall *const *c, size_t n)
     size_t off_ok = up;
     for (size_t i = 0; i < n; ++i)
         off_ok += a16(c[i]->len + (open ? 0 : 16));
-    const size_t off_mask = off_ok + a16(n), total = off_mask + 16 * n;
+    // completion words: one per workgroup of the last kernel (the GCM launch: one workgroup per record up to the CU
+    // count; the header-protection launch: aux_grid)
+    const size_t nflags = hp ? (size_t)aux_grid(n, ds->ncu) : (n < (size_t)ds->ncu ? n : (size_t)ds->ncu);
+    const size_t off_mask = off_ok + a16(n), off_flag = off_mask + 16 * n, total = off_flag + a16(4 * nflags);
     int ret = -1;
     {
         StageCall call(ds);
@@ -1139,13 +1170,21 @@ static void run_calls(DeviceState *ds, OneCall *const *c, size_t n)
             // Long records, and batches (one workgroup per record), pass CHUNK_LOG2: the kernel's scan then picks.
             const size_t steps = ((c0.aadlen + 15) / 16 + (c0.len + 15) / 16 + 1 + ENGINE_G - 1) / ENGINE_G;
             const u32 unit_log2 = n > 1 ? CHUNK_LOG2 : steps <= 24 ? 0 : steps <= 96 ? 1 : steps <= 400 ? 2 : steps <= 1600 ? 3 : CHUNK_LOG2;
+            // (launches of small records only: a 4 MiB record's launch, ~2 ms, measured 1.3 ms slower with the host
+            // polling its staging buffer than waiting for the stream)
+            const bool flag = PERREC_FLAG && call.mapped() && c0.ks->schedule != PTLS_MI355X_SCHEDULE_LOCKSTEP && total <= PERREC_FLAG_MAX_BYTES;
+            if (flag)
+                memset(h + off_flag, 0, 4 * nflags);
             if (ret == 0)
                 ret = call.roundtrip(up, [&] {
                     if (launch_gcm(kbase, nkeys, nr, ds->ncu, c0.ks->schedule, c0.ks->ct, open, (const ptls_mi355x_record_t *)(d + off_rec),
-                                   n, d, d, d, d + off_ok, s, 0, unit_log2, nullptr, nullptr, nullptr, n == 1 ? &first : nullptr) != 0)
+                                   n, d, d, d, d + off_ok, s, 0, unit_log2, nullptr, nullptr, nullptr, n == 1 ? &first : nullptr,
+                                   flag && !hp ? (u32 *)(d + off_flag) : nullptr) != 0)
                         return -1;
-                    return !hp ? 0 : launch_hp(hbase, hp_nkeys, hp_nr, ds->ncu, (const ptls_mi355x_hp_t *)(d + off_hp), n, d, d + off_mask, s);
-                });
+                    return !hp ? 0
+                               : launch_hp(hbase, hp_nkeys, hp_nr, ds->ncu, (const ptls_mi355x_hp_t *)(d + off_hp), n, d, d + off_mask, s,
+                                           flag ? (u32 *)(d + off_flag) : nullptr);
+                }, flag ? off_flag : 0, nflags);
             if (ret == 0) {
                 out_at = up;
                 for (size_t i = 0; i < n; ++i) {

@@ -569,6 +569,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         pos = run_end;
         rb ^= 1;
     }
+    publish_done(args.done_flag);  // the per-record path polls these instead of waiting for the stream
 }
 
 #endif  // PTLS_MI355X_ENGINE_GCM_KERNELS_H

@@ -62,6 +62,9 @@ struct BatchArgs {
     // the kernel arguments; `recs` is not read)
     u32 one_inline;
     ptls_mi355x_record_t one;
+    // chunked kernel on the per-record path: workgroup w sets done_flag[w] to 1 (system scope) once every output byte
+    // it writes is written, for the host thread that polls them (null: none)
+    u32 *done_flag;
 };
 
 #define RUN_SCAN_CAP 256  // records examined per key-run scan (multi-key batches)
