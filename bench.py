@@ -50,6 +50,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=3.0, help="wall budget of each cpu_baseline leg")
     p.add_argument("--e2e", action="store_true", help="also time pinned-host -> H2D -> seal -> D2H (DESIGN.md)")
+    p.add_argument("--e2e-chunks", type=int, default=256,
+                   help="--e2e: chunks of the pipelined mode (16 MiB at the default 4 GiB: 34.4 GiB/s vs 31.6-31.8 with 64-16)")
     p.add_argument("--schedule", default="auto", choices=["auto", "lockstep", "chunked"],
                    help="batch schedule (ptls_mi355x_keyset_set_schedule)")
     p.add_argument("--verify", type=int, default=1, help="verify round trip + fusion spot checks after timing")
@@ -464,6 +466,31 @@ def run_e2e(R, wl, nchunks: int = 16, reps: int = 3, schedule: str = "auto"):
         verified = bool(d_ok.min().item() == 1) and bool(np.array_equal(h_back.numpy()[m], h_pt.numpy()[m]))
         out[mode] = {"seal_GiBps": round(gib / ts, 2), "open_GiBps": round(gib / to, 2),
                      "seal_open_GiBps": round(2 * gib / (ts + to), 2), "verified": verified}
+    # the link itself: the same arenas copied H2D and D2H at once on two streams, no kernel (the ceiling of every mode
+    # above, where a payload byte crosses once in each direction per seal and once per open)
+    s_up, s_down = streams[0], streams[1]
+    tl = 0.0
+    for _ in range(reps + 1):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        with torch.cuda.stream(s_up):
+            d_pt.copy_(h_pt, non_blocking=True)
+        with torch.cuda.stream(s_down):
+            h_back.copy_(d_back, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        if _ > 0:
+            tl += time.perf_counter() - t0
+    link = b.pt_bytes * reps / 2**30 / tl
+    up_only = []
+    for src, dst in ((h_pt, d_pt), (d_back, h_back)):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        up_only.append(b.pt_bytes * reps / 2**30 / (time.perf_counter() - t0))
+    out["link"] = {"both_directions_GiBps_each": round(link, 2), "h2d_alone_GiBps": round(up_only[0], 2),
+                   "d2h_alone_GiBps": round(up_only[1], 2)}
     out.update({"records": b.n, "payload_bytes": b.payload_bytes, "chunks": len(chunks),
                 "verified": all(out[k]["verified"] for k in ("serial", "pipelined", "in_place")),
                 "note": "pinned host buffers; PCIe Gen5 x16 ~63 GB/s/direction bounds this path; in_place: the kernels "
@@ -583,7 +610,7 @@ def main():
     if extra:
         out["extra"] = extra
     if args.e2e:
-        out["e2e_host_buffers"] = run_e2e(R, WORKLOADS[args.workload].scaled(min(wl.nrecs, max(1, (4 << 30) // (wl.rec_len or 8192)))),
+        out["e2e_host_buffers"] = run_e2e(R, WORKLOADS[args.workload].scaled(min(wl.nrecs, max(1, (4 << 30) // (wl.rec_len or 8192)))), args.e2e_chunks,
                                           schedule=args.schedule)
     if R.rank == 0 and R.world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], checks = cpu_baseline(wl, args.cpu_seconds, samples if args.verify else {}, ptlsbench_gpu)
