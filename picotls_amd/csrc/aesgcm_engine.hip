@@ -1170,8 +1170,8 @@ static void run_calls(DeviceState *ds, OneCall *const *c, size_t n)
             // Long records, and batches (one workgroup per record), pass CHUNK_LOG2: the kernel's scan then picks.
             const size_t steps = ((c0.aadlen + 15) / 16 + (c0.len + 15) / 16 + 1 + ENGINE_G - 1) / ENGINE_G;
             const u32 unit_log2 = n > 1 ? CHUNK_LOG2 : steps <= 24 ? 0 : steps <= 96 ? 1 : steps <= 400 ? 2 : steps <= 1600 ? 3 : CHUNK_LOG2;
-            // (launches of small records only: a 4 MiB record's launch, ~2 ms, measured 1.3 ms slower with the host
-            // polling its staging buffer than waiting for the stream)
+            // (calls staging at most 1 MiB: a larger record's launch runs for hundreds of microseconds or more, which
+            // the caller need not spend spinning on a core)
             const bool flag = PERREC_FLAG && call.mapped() && c0.ks->schedule != PTLS_MI355X_SCHEDULE_LOCKSTEP && total <= PERREC_FLAG_MAX_BYTES;
             if (flag)
                 memset(h + off_flag, 0, 4 * nflags);

@@ -145,6 +145,11 @@ __device__ __forceinline__ unsigned long long stamp()
 #define PROF_ADD(i, x)
 #endif
 
+#ifndef EARLY_GHASH
+#define EARLY_GHASH 1
+#endif
+#define EARLY_GHASH_WAVE 11  // waves 11..15 (320 threads: one per table window of 9 tables) build a one-key launch's tables
+
 // Run-state control words (RUN_CTL_WORDS per buffer)
 #define RC_KEY 0     // key index of the run
 #define RC_NEXT 1    // next unit to hand out
@@ -379,8 +384,16 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     auto ok_at = [&](u64 i) -> u64 { return perm != nullptr ? (u64)perm[i] : i; };
 
     // the first run's state on wave 0 (later runs are scanned during the previous run's tail) while waves 1.. copy
-    // the AES tables
-    if (wave == 0) {
+    // the AES tables. A one-key launch knows its key before the scan: waves EARLY_GHASH_WAVE.. build its GHASH tables
+    // H^1..H^8 meanwhile (and the unit combine table when the launch fixes the unit length: the per-record path),
+    // instead of after the prologue barrier; the AES copy keeps the waves in between.
+    const bool early = EARLY_GHASH && !args.multi_key;
+    const u32 fixed_usrc = args.unit_log2 == CHUNK_LOG2 ? 8u : args.unit_log2 == 0 ? 7u : 8u + args.unit_log2;
+    const bool early_combine = early && args.unit_log2 < CHUNK_LOG2;
+    if (early && wave >= EARLY_GHASH_WAVE) {
+        build_ghash_tables(lds, args.keys, early_combine ? 9u : 8u, fixed_usrc, 0, EARLY_GHASH_WAVE * 64,
+                           ENGINE_WG - EARLY_GHASH_WAVE * 64);
+    } else if (wave == 0) {
         if (beg < end)
             scan_run<OPEN, FRAME, true>(args, recs, beg, end, (lds_u32 *)(lds + CLDS_RUN0));
 #if ENGINE_PROFILE
@@ -388,13 +401,16 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             PROF_ADD(9, stamp() - tk), PROF_ADD(10, 1);
 #endif
     } else {
-        build_aes_tables(lds, 64);
+        build_aes_tables(lds, 64, early ? EARLY_GHASH_WAVE * 64 : 0);
 #if ENGINE_PROFILE
         if (threadIdx.x == 64)
             PROF_ADD(8, stamp() - tk);
 #endif
     }
     __syncthreads();
+
+    if (early)  // key 0's tables are in place (and the combine table of the fixed unit length)
+        loaded_key = 0, loaded_usrc = early_combine ? fixed_usrc : 0xffffffffu;
 
     u32 rb = 0;  // run-state buffer of the current run
     for (u64 pos = beg; pos < end;) {

@@ -33,10 +33,11 @@ constexpr AesTtabImage make_aes_ttab()
 }
 __device__ const AesTtabImage g_aes_ttab = make_aes_ttab();
 
-// Threads [skip, blockDim.x) build it (skip: a multiple of 64; the chunked kernel's wave 0 scans meanwhile)
-__device__ void build_aes_tables(lds_u8 *lds, u32 skip = 0)
+// Threads [skip, end) build it (end 0: blockDim.x; both multiples of 64; the chunked kernel's other waves scan the first
+// run and build the GHASH tables meanwhile)
+__device__ void build_aes_tables(lds_u8 *lds, u32 skip = 0, u32 end = 0)
 {
-    const u32 tid = threadIdx.x - skip, nthr = blockDim.x - skip;
+    const u32 tid = threadIdx.x - skip, nthr = (end != 0 ? end : blockDim.x) - skip;
 #if AES_TTAB_COPY
     const u32x4 *src = (const u32x4 *)g_aes_ttab.v;
     lds_u32x4 *dst = (lds_u32x4 *)lds;
@@ -83,10 +84,13 @@ __device__ void build_aes_tables(lds_u8 *lds, u32 skip = 0)
 // 16 entries. Entries are GF(2)-linear in n, so the XOR combinations are formed after the byte swap back to memory
 // order, and entry n ^ c = e(n) ^ e(c): at store n a lane writes slot n ^ (p mod 16), spreading a wave's 16-byte stores
 // over the bank groups. A few hundred VALU operations per thread: the build is a small part of a launch of one record.
+// Threads [tid0, tid0 + nthr) take part (nthr 0: the whole workgroup).
 template <typename KeyPtr>  // a KeyEntry in global memory, or its copy staged in LDS (the chunked kernel)
-__device__ void build_ghash_tables(lds_u8 *lds, KeyPtr key, u32 ntables = ENGINE_G, u32 src8 = 8, u32 first = 0)
+__device__ void build_ghash_tables(lds_u8 *lds, KeyPtr key, u32 ntables = ENGINE_G, u32 src8 = 8, u32 first = 0, u32 tid0 = 0,
+                                   u32 nthr = 0)
 {
-    for (u32 idx = first * 32 + threadIdx.x; idx < ntables * 32; idx += blockDim.x) {
+    const u32 stride = nthr != 0 ? nthr : blockDim.x;
+    for (u32 idx = first * 32 + threadIdx.x - tid0; idx < ntables * 32; idx += stride) {
         const u32 t = idx >> 5, p = idx & 31;
         const auto *h = key->h[t == 8 ? src8 : t];  // table 8: the unit combine power (chunked kernel)
         u32 b0 = bswap32(h[0]), b1 = bswap32(h[1]), b2 = bswap32(h[2]), b3 = bswap32(h[3]);
