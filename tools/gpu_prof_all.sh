@@ -2,6 +2,6 @@
 set +e
 cd $GRAFT_REPO_ROOT
 for w in "tls16k 1048576" "quic1200 4194304" "mixed 4194304"; do set -- $w
-  bash tools/gpu_prof.sh $1 $2 r1 || exit 1
+  bash tools/gpu_prof.sh $1 $2 ${PROF_TAG:-r2f} || exit 1
 done
 exit 0
