@@ -145,6 +145,9 @@ __device__ __forceinline__ unsigned long long stamp()
 #define PROF_ADD(i, x)
 #endif
 
+#ifndef RUN_FILL_UNITS
+#define RUN_FILL_UNITS (ENGINE_WG / ENGINE_G / 2)  // a cut run takes the longest units that still give this many
+#endif
 #ifndef EARLY_GHASH
 #define EARLY_GHASH 1
 #endif
@@ -179,7 +182,7 @@ __device__ __forceinline__ unsigned long long stamp()
 __device__ __forceinline__ u32 run_unit_log2(u32 total_steps, u32 smax, u32 cap)
 {
     u32 fill = 0, chain = 0;
-    while (fill < cap && (total_steps >> (fill + 1)) >= (u32)(ENGINE_WG / ENGINE_G / 2))
+    while (fill < cap && (total_steps >> (fill + 1)) >= (u32)RUN_FILL_UNITS)
         ++fill;
     while (chain < cap && ((smax + (1u << chain) - 1) >> chain) > 36u)
         ++chain;
