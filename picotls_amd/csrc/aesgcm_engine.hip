@@ -708,6 +708,26 @@ static void launch_chunked(bool ct, unsigned grid, hipStream_t s, const BatchArg
         gcm_chunked_kernel<NR, OPEN, FRAME, false><<<grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
 }
 
+// Records per chunk of the chunked kernel's dealt-out assignment (BatchArgs::chunk), 0 for contiguous ranges. Each
+// workgroup gets up to CHUNKS_PER_WG chunks spread over the batch, so that a batch ordered by record size (or by
+// connections whose records differ in size) still shares its bytes evenly: 4M records of U[64 B, 16 KiB] sorted by
+// length ran at 467 GiB/s seal+open with contiguous ranges against 802 in random order (bench.py, mixedsorted vs
+// mixed1key). Chunks stay at least CHUNK_MIN_RECS records (whole-record runs need 128 and gain from more), and a
+// batch too small for two such chunks per workgroup keeps contiguous ranges.
+#ifndef CHUNKS_PER_WG
+#define CHUNKS_PER_WG 8
+#endif
+#define CHUNK_MIN_RECS 256
+static u64 deal_chunk(u64 nrecs, u64 grid)
+{
+    for (u64 k = CHUNKS_PER_WG; k >= 2; k /= 2) {
+        const u64 c = (nrecs + grid * k - 1) / (grid * k);
+        if (c >= CHUNK_MIN_RECS)
+            return c;
+    }
+    return 0;
+}
+
 // The GCM kernel launch of a batch over `nkeys` entries at `keys` (no key grouping, no keyset bookkeeping). ct: the
 // constant-time GHASH variant of the chunked kernel (the lockstep schedule is not offered in that mode).
 static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int schedule, bool ct, bool open,
@@ -717,7 +737,7 @@ static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int sche
                       u32 *done_flag = nullptr)
 {
     BatchArgs a = {keys, recs, (u64)nrecs, (const uint8_t *)in, (const uint8_t *)aad, (uint8_t *)out, ok,
-                   nkeys > 1 ? 1u : 0u, nkeys, unit_log2, grouped, perm, perm_on, 0u, {}, done_flag};
+                   nkeys > 1 ? 1u : 0u, nkeys, unit_log2, grouped, perm, perm_on, 0u, {}, done_flag, 0};
     if (one != nullptr && nrecs == 1)  // the chunked kernel takes a lone record's descriptor from its arguments
         a.one_inline = 1, a.one = *one;
     if (a.aad == NULL)
@@ -728,6 +748,7 @@ static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int sche
         grid = nrecs;
     if (grid < 1)
         grid = 1;
+    a.chunk = deal_chunk(nrecs, grid);
 #define CHUNKED_LAUNCH(nr_, op, frame_) launch_chunked<nr_, op, frame_>(ct, (unsigned)grid, s, a)
 #define CHUNKED_BY_KEY(frame_)                                                                                          \
     do {                                                                                                                \

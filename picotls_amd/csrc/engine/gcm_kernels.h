@@ -341,7 +341,8 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
     }
 }
 
-// Chunked schedule for many-key / mixed-length batches. The lockstep kernel above gives each G-lane group a whole
+// Chunked schedule for many-key / mixed-length batches (and the default for every batch). Workgroup w walks the chunks
+// w, w + grid, ... of BatchArgs::chunk records (or one contiguous range), run by run. The lockstep kernel above gives each G-lane group a whole
 // record, so a wave runs as long as its longest record and a key run (~64 records of a connection) as long as its
 // longest record too; with U[64 B, 16 KiB] lengths and a workgroup barrier per key that halves throughput twice.
 // Here a run's records are cut into units of at most CHUNK_BLOCKS GHASH-stream blocks, counted from the END of the
@@ -366,8 +367,11 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     const u32 tsel_horner = 0x10000u + (u32)(G - 1) * GHASH_TABLE_BYTES;
     const u32 tsel_chunk = 0x10000u + 8u * GHASH_TABLE_BYTES;
 
-    const u64 n = args.nrecs;
-    const u64 beg = n * blockIdx.x / gridDim.x, end = n * (blockIdx.x + 1) / gridDim.x;
+    const u64 n = args.nrecs, C = args.chunk;
+    // this workgroup's records: the chunk [beg, end) (cstart: its first record), then the chunk grid * C further on
+    // (C != 0), or one contiguous range (C == 0)
+    const u64 beg = C != 0 ? min(n, (u64)blockIdx.x * C) : n * blockIdx.x / gridDim.x;
+    u64 end = C != 0 ? min(n, beg + C) : n * (blockIdx.x + 1) / gridDim.x, cstart = beg;
     u32 loaded_key = 0xffffffffu, loaded_usrc = 0xffffffffu;
     // the descriptors in batch order, or (an ungrouped many-key batch) the key-grouped copy built on the device; ok
     // bytes go to the record's batch index either way
@@ -434,16 +438,23 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         const u32 usrc = ustep == CHUNK_STEPS ? 8u : ulog2 == 0 ? 7u : 8u + ulog2;
         const u32 nfull = total_units - run_n;
         const u64 run_end = pos + run_n;
+        // the next run: the rest of this chunk, or the workgroup's next chunk
+        u64 nxt = run_end, nxt_end = end, nxt_cstart = cstart;
+        if (C != 0 && run_end >= end) {
+            nxt_cstart = cstart + (u64)gridDim.x * C;
+            nxt = min(n, nxt_cstart);
+            nxt_end = min(n, nxt_cstart + C);
+        }
         PROF_STAMP(t1);
 
         if (key_idx >= args.nkeys) {  // invalid key: nothing is written except a failed ok byte
             if (OPEN)
                 for (u64 t = pos + threadIdx.x; t < run_end; t += blockDim.x)
                     args.ok[ok_at(t)] = 0;
-            if (wave == 0 && run_end < end)
-                scan_run<OPEN, FRAME>(args, recs, run_end, end, rs_next);
+            if (wave == 0 && nxt < nxt_end)
+                scan_run<OPEN, FRAME>(args, recs, nxt, nxt_end, rs_next);
             __syncthreads();
-            pos = run_end;
+            pos = nxt, end = nxt_end, cstart = nxt_cstart;
             rb ^= 1;
             continue;
         }
@@ -567,8 +578,8 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         u32 claim = 0;
         if (lane_here() == 0)
             claim = atomicAdd((u32 *)&rs[RC_CLAIM], 1u) == 0;
-        if (__builtin_amdgcn_readfirstlane(claim) && run_end < end)
-            scan_run<OPEN, FRAME>(args, recs, run_end, end, rs_next);
+        if (__builtin_amdgcn_readfirstlane(claim) && nxt < nxt_end)
+            scan_run<OPEN, FRAME>(args, recs, nxt, nxt_end, rs_next);
         PROF_STAMP(tw);
         __syncthreads();  // the run's tables, partials and counters are free again
         PROF_STAMP(t3);
@@ -585,7 +596,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 PROF_ADD(3, t0 - tk);
         }
 #endif
-        pos = run_end;
+        pos = nxt, end = nxt_end, cstart = nxt_cstart;
         rb ^= 1;
     }
     publish_done(args.done_flag);  // the per-record path polls these instead of waiting for the stream

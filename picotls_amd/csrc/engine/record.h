@@ -65,6 +65,10 @@ struct BatchArgs {
     // chunked kernel on the per-record path: workgroup w sets done_flag[w] to 1 (system scope) once every output byte
     // it writes is written, for the host thread that polls them (null: none)
     u32 *done_flag;
+    // chunked kernel: 0 = workgroup w walks the contiguous records [n*w/grid, n*(w+1)/grid); else it walks the chunks
+    // w, w + grid, w + 2*grid, ... of `chunk` records each (records are dealt out across the batch, so a batch whose
+    // record sizes follow its order still gives every workgroup a similar share of bytes)
+    u64 chunk;
 };
 
 #define RUN_SCAN_CAP 256  // records examined per key-run scan (multi-key batches)

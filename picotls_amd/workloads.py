@@ -90,6 +90,7 @@ class Workload:
     seed: int = 0x5EED
     desc: str = ""
     key_order: str = "grouped"  # many keys: "grouped" by connection, or "random" (key_idx = splitmix(i) mod nkeys)
+    sorted_lens: bool = False  # mixed lengths in ascending order over the batch (a batch built by record size)
 
     def scaled(self, nrecs: int) -> "Workload":
         return replace(self, nrecs=nrecs)
@@ -98,6 +99,9 @@ class Workload:
     def lens(self, begin: int, end: int) -> np.ndarray:
         if self.rec_len is not None:
             return np.full(end - begin, self.rec_len, dtype=np.uint64)
+        if self.sorted_lens:
+            w = np.sort(splitmix_words_np(self.seed ^ 0x4C454E, 0, self.nrecs) % np.uint64(self.max_len - self.min_len + 1))
+            return (np.uint64(self.min_len) + w[begin:end]).astype(np.uint64)
         w = splitmix_words_np(self.seed ^ 0x4C454E, begin, end - begin)
         return (np.uint64(self.min_len) + w % np.uint64(self.max_len - self.min_len + 1)).astype(np.uint64)
 
@@ -180,6 +184,8 @@ WORKLOADS = {
     # analysis variants (not BASELINE configs): isolate key switching and length mix from the AES-256 cost
     "mixed1key": Workload("mixed1key", 4 << 20, None, 13, 32,
                           desc="4M mixed-length records 64 B-16 KiB, AES-256-GCM, one key"),
+    "mixedsorted": Workload("mixedsorted", 4 << 20, None, 13, 32, sorted_lens=True,
+                            desc="4M mixed-length records 64 B-16 KiB sorted by length, AES-256-GCM, one key"),
     "tls16k256": Workload("tls16k256", 1 << 20, 16384, 5, 32, tls_header_aad=True,
                           desc="1M x 16384 B TLS records, AES-256-GCM, one key"),
     "u8k256": Workload("u8k256", 4 << 20, 8192, 13, 32, desc="4M x 8192 B records, AES-256-GCM, one key"),

@@ -112,3 +112,56 @@ def test_config3_mixedrand_64k_keys_vs_fusion():
     assert np.array_equal(ok.astype(bool), ~bad)
     assert np.array_equal(d_back.cpu().numpy(), back_want)  # plaintext written for every record, as fusion does
     ks.free()
+
+
+def test_sorted_lengths_dealt_chunks_vs_fusion():
+    # a batch large enough for the chunked kernel's dealt-out chunks (BatchArgs::chunk: each workgroup walks chunks
+    # spread over the batch instead of one contiguous range): 300,000 records sorted by length (0..2000 B), 300 keys
+    # grouped by connection, so chunk edges cut key runs and whole-record runs; every record equals fusion's, and an
+    # open with 1 % of the records tampered reports exactly those
+    if not os.path.exists(os.path.join(REF_DIR, "libfusion_ref.so")):
+        pytest.skip("oracle/_ref/libfusion_ref.so not shipped")
+    from picotls_amd.records import RecordBatch
+
+    ref = FusionRef()
+    rng = np.random.default_rng(17)
+    n, nkeys = 300000, 300
+    lens = np.sort(rng.integers(0, 2001, n)).astype(np.uint64)
+    key_idx = (np.arange(n) * nkeys // n).astype(np.uint32)
+    b = RecordBatch.build(lens, 13, seqs=np.arange(n, dtype=np.uint64), key_idx=key_idx)
+    keys, ivs = rng.bytes(16 * nkeys), rng.bytes(12 * nkeys)
+    keys_np, ivs_np = np.frombuffer(keys, np.uint8), np.frombuffer(ivs, np.uint8)
+    dev = torch.device("cuda:0")
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(b.aad_bytes), np.uint8)
+    ks = pa.Keyset(keys, ivs, 16)
+    s = torch.cuda.current_stream().cuda_stream
+    d_recs, d_pt, d_aad = (torch.from_numpy(x.view(np.uint8).copy()).to(dev) for x in (b.seal, pt, aad))
+    d_sealed = torch.zeros(b.sealed_bytes, dtype=torch.uint8, device=dev)
+    pa.seal_batch(ks, d_recs.data_ptr(), b.n, d_pt.data_ptr(), d_aad.data_ptr(), d_sealed.data_ptr(), s)
+    torch.cuda.synchronize()
+    want = np.zeros(b.sealed_bytes, np.uint8)
+    ref.run_batch(True, keys_np, ivs_np, 16, b.seal, pt, aad, want, nthreads=_threads())
+    sealed = d_sealed.cpu().numpy()
+    for i in (0, n // 2, n - 1):  # padding between slots is zero in both arenas: compare per record, then whole
+        o, ln = int(b.seal["out_off"][i]), int(b.seal["len"][i]) + 16
+        assert np.array_equal(sealed[o:o + ln], want[o:o + ln]), i
+    assert np.array_equal(sealed, want)
+
+    bad = rng.random(n) < 0.01
+    bad_idx = np.flatnonzero(bad)
+    pos = b.seal["out_off"][bad_idx].astype(np.int64) + rng.integers(0, b.seal["len"][bad_idx].astype(np.int64) + 16)
+    tampered = want.copy()
+    tampered[pos] ^= np.uint8(0x10)
+    d_open = torch.from_numpy(b.open.view(np.uint8).copy()).to(dev)
+    d_in = torch.from_numpy(tampered).to(dev)
+    d_back = torch.zeros(b.pt_bytes, dtype=torch.uint8, device=dev)
+    d_ok = torch.full((n,), 0xAA, dtype=torch.uint8, device=dev)
+    pa.open_batch(ks, d_open.data_ptr(), n, d_in.data_ptr(), d_aad.data_ptr(), d_back.data_ptr(), d_ok.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_ok.cpu().numpy().astype(bool), ~bad)
+    m = np.zeros(b.pt_bytes, bool)
+    for o, ln in zip(b.seal["in_off"][~bad][:2000], b.seal["len"][~bad][:2000]):
+        m[int(o):int(o) + int(ln)] = True
+    assert np.array_equal(d_back.cpu().numpy()[m], pt[m])
+    ks.free()
