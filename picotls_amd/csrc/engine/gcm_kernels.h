@@ -148,6 +148,9 @@ __device__ __forceinline__ unsigned long long stamp()
 #ifndef RUN_FILL_UNITS
 #define RUN_FILL_UNITS (ENGINE_WG / ENGINE_G / 2)  // a cut run takes the longest units that still give this many
 #endif
+#ifndef COMBINE_TAB
+#define COMBINE_TAB 0  // unit combine with gmul_tab (every lane the whole product, same table rows) in the default mode too
+#endif
 #ifndef EARLY_GHASH
 #define EARLY_GHASH 1
 #endif
@@ -555,9 +558,9 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                     // its own window rows)
                     u32x4 g = s_part[first];
                     for (u32 i = 1; i < unc; ++i) {
-                        g = CT ? gmul_tab(lds, g, tsel_chunk) : gmul_group(lds, g, tsel_chunk, j);
+                        g = CT || COMBINE_TAB ? gmul_tab(lds, g, tsel_chunk) : gmul_group(lds, g, tsel_chunk, j);
                         for (u32 t = 1; t < mul; ++t)  // huge records only
-                            g = CT ? gmul_tab(lds, g, tsel_chunk) : gmul_group(lds, g, tsel_chunk, j);
+                            g = CT || COMBINE_TAB ? gmul_tab(lds, g, tsel_chunk) : gmul_group(lds, g, tsel_chunk, j);
                         g ^= s_part[first + i];
                     }
                     const u32x4 tag = g;
