@@ -718,6 +718,10 @@ static void launch_chunked(bool ct, unsigned grid, hipStream_t s, const BatchArg
 #define CHUNKS_PER_WG 8
 #endif
 #define CHUNK_MIN_RECS 256
+#ifndef BALANCE
+#define BALANCE 1  // many-key batches: workgroup ranges balanced by weight (balance_*_kernel)
+#endif
+#define BALANCE_MIN_RECS ((size_t)131072)  // ... from this many records (2 x 256 per workgroup)
 static u64 deal_chunk(u64 nrecs, u64 grid)
 {
     for (u64 k = CHUNKS_PER_WG; k >= 2; k /= 2) {
@@ -734,10 +738,10 @@ static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int sche
                       const ptls_mi355x_record_t *recs, size_t nrecs, const void *in, const void *aad, void *out, uint8_t *ok,
                       hipStream_t s, int frame, u32 unit_log2, const ptls_mi355x_record_t *grouped = nullptr,
                       const u32 *perm = nullptr, const u32 *perm_on = nullptr, const ptls_mi355x_record_t *one = nullptr,
-                      u32 *done_flag = nullptr)
+                      u32 *done_flag = nullptr, const u64 *bounds = nullptr)
 {
     BatchArgs a = {keys, recs, (u64)nrecs, (const uint8_t *)in, (const uint8_t *)aad, (uint8_t *)out, ok,
-                   nkeys > 1 ? 1u : 0u, nkeys, unit_log2, grouped, perm, perm_on, 0u, {}, done_flag, 0};
+                   nkeys > 1 ? 1u : 0u, nkeys, unit_log2, grouped, perm, perm_on, 0u, {}, done_flag, 0, bounds};
     if (one != nullptr && nrecs == 1)  // the chunked kernel takes a lone record's descriptor from its arguments
         a.one_inline = 1, a.one = *one;
     if (a.aad == NULL)
@@ -810,8 +814,12 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
     int ret;
     if (group) {
         std::lock_guard<std::mutex> lk(ks->mu);
-        // scratch: ctl[2] | counts[nkeys + 1] | perm[n] | (8-byte aligned) grouped descriptors[n]
-        const size_t nb = ks->nkeys + 1, words = ((2 + nb + nrecs + 1) & ~(size_t)1) + nrecs * (sizeof(ptls_mi355x_record_t) / 4);
+        // scratch: ctl[2] | counts[nkeys + 1] | perm[n] | (8-byte aligned) grouped descriptors[n] | balance tiles | bounds
+        const bool balance = BALANCE && nrecs >= BALANCE_MIN_RECS;
+        const size_t ntiles = (nrecs + BALANCE_TILE - 1) / BALANCE_TILE, ncu = (size_t)ks->ds->ncu;
+        const size_t gwords = ((2 + ks->nkeys + 1 + nrecs + 1) & ~(size_t)1) + nrecs * (sizeof(ptls_mi355x_record_t) / 4);
+        const size_t twords = balance ? (ntiles + 1) & ~(size_t)1 : 0, bwords = balance ? 2 * (ncu + 1) : 0;
+        const size_t nb = ks->nkeys + 1, words = gwords + twords + bwords;
         if (ks->group_ev == NULL)
             HIP_TRY(hipEventCreateWithFlags(&ks->group_ev, hipEventDisableTiming));
         HIP_TRY(hipStreamWaitEvent(s, ks->group_ev, 0));  // a batch on another stream may still use the scratch
@@ -831,8 +839,16 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
         key_scan_kernel<<<1, 1024, 0, s>>>(cnt, (u32)nb, nrecs, ctl);
         ptls_mi355x_record_t *grouped = (ptls_mi355x_record_t *)(ctl + ((2 + nb + nrecs + 1) & ~(size_t)1));
         key_scatter_kernel<<<gh, 256, 0, s>>>(recs, nrecs, (u32)ks->nkeys, cnt, perm, grouped, ctl);
+        u64 *bounds = nullptr;
+        if (balance && use_chunked(ks->schedule)) {  // workgroup ranges of equal work (balance_bounds_kernel)
+            u32 *tiles = ks->d_group + gwords;
+            bounds = (u64 *)(ks->d_group + gwords + twords);
+            const u32 grid = (u32)(ncu < nrecs ? ncu : nrecs);
+            balance_tiles_kernel<<<(unsigned)min((ntiles + 3) / 4, ncu * 8), 256, 0, s>>>(recs, grouped, ctl + 1, nrecs, tiles);
+            balance_bounds_kernel<<<1, 1024, 0, s>>>(tiles, nrecs, grid, bounds);
+        }
         ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, ks->ct, open, recs, nrecs, in, aad, out, ok, s,
-                         frame, CHUNK_LOG2, grouped, perm, ctl + 1);
+                         frame, CHUNK_LOG2, grouped, perm, ctl + 1, nullptr, nullptr, bounds);
         if (ret == 0)
             HIP_TRY(hipEventRecord(ks->group_ev, s));
     } else {

@@ -98,6 +98,86 @@ __global__ __launch_bounds__(256) void key_scatter_kernel(const ptls_mi355x_reco
     }
 }
 
+// ------------------------------------------------------------------------------------------------ byte balance
+// A many-key batch of 256 or more records per workgroup is split among the chunked kernel's workgroups by work, not by
+// record count: connections differ (a bulk download's 16 KiB records next to a chat's 100-byte ones), and a quarter
+// of 64K connections being bulk left the busiest workgroup 26 % above the mean (max-over-workgroups is the launch
+// time). Weight of a record = its GHASH stream steps (capped) + 1 for the per-record work; the sums of tiles of
+// BALANCE_TILE records, then one workgroup cuts the batch at tile edges into grid ranges of equal weight (a tile is
+// < 2 % of a workgroup's share at the sizes this runs at). Both walk the descriptor order the chunked kernel walks.
+#define BALANCE_TILE 64
+
+__device__ __forceinline__ u32 balance_weight(const ptls_mi355x_record_t &r)
+{
+    const u32 aad = (u32)r.aad_len | (u32)r.flags << 16;
+    const u32 steps = (u32)(((u64)aad + 15) / 16 + ((u64)r.len + 15) / 16 + 1 + 7) / 8;
+    return (steps < 65535u ? steps : 65535u) + 1;
+}
+
+// tiles[t] = weight of records [t * 64, t * 64 + 64): one wave per tile
+__global__ __launch_bounds__(256) void balance_tiles_kernel(const ptls_mi355x_record_t *recs, const ptls_mi355x_record_t *grouped,
+                                                            const u32 *perm_on, u64 n, u32 *tiles)
+{
+    static_assert(BALANCE_TILE == 64, "one lane per record of a tile");
+    const ptls_mi355x_record_t *r = perm_on != nullptr && *perm_on ? grouped : recs;
+    const u64 ntiles = (n + BALANCE_TILE - 1) / BALANCE_TILE, lane = threadIdx.x & 63;
+    for (u64 t = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < ntiles; t += ((u64)gridDim.x * blockDim.x) >> 6) {
+        const u64 i = t * BALANCE_TILE + lane;
+        u32 w = i < n ? balance_weight(r[i]) : 0u;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1)
+            w += (u32)__shfl_xor((int)w, off, 64);
+        if (lane == 0)
+            tiles[t] = w;
+    }
+}
+
+// bounds[0..grid]: the record ranges of the grid workgroups, cut at tile edges so that each holds about total / grid of
+// the weight (one workgroup of 1024 threads: a scan of per-thread tile stretches, then each thread places the cuts that
+// fall into its stretch)
+__global__ __launch_bounds__(1024) void balance_bounds_kernel(const u32 *tiles, u64 n, u32 grid, u64 *bounds)
+{
+    __shared__ u64 s_off[1024];
+    const u64 ntiles = (n + BALANCE_TILE - 1) / BALANCE_TILE;
+    const u32 t = threadIdx.x;
+    const u64 per = (ntiles + blockDim.x - 1) / blockDim.x, t0 = min(ntiles, t * per), t1 = min(ntiles, t0 + per);
+    u64 sum = 0;
+    for (u64 i = t0; i < t1; ++i)
+        sum += tiles[i];
+    s_off[t] = sum;
+    __syncthreads();
+    // inclusive scan of s_off (Hillis-Steele over 1024 entries; the batch's only serial step, a few microseconds)
+    for (u32 off = 1; off < blockDim.x; off <<= 1) {
+        const u64 v = t >= off ? s_off[t - off] : 0;
+        __syncthreads();
+        s_off[t] += v;
+        __syncthreads();
+    }
+    const u64 total = s_off[blockDim.x - 1], lo = s_off[t] - sum, hi = s_off[t];
+    if (t == 0) {
+        bounds[0] = 0;
+        bounds[grid] = n;
+    }
+    if (total == 0) {  // (no weight: an empty batch) contiguous ranges by count
+        for (u32 b = 1 + t; b < grid; b += blockDim.x)
+            bounds[b] = n * b / grid;
+        return;
+    }
+    // cuts b (1 <= b < grid) with target total * b / grid in [lo, hi): walk this stretch's tiles to the first tile edge
+    // at or past the target
+    u64 b = (lo * grid + total - 1) / total;  // least b with total * b / grid >= lo (as exact integers: b * total >= lo * grid)
+    b = b < 1 ? 1 : b;
+    u64 acc = lo, i = t0;
+    for (; b < grid; ++b) {
+        const u64 tb = total * b;  // (weights are capped per record: total * grid stays far below 2^64)
+        if (tb >= hi * grid)
+            break;
+        while (i < t1 && (acc + tiles[i]) * grid <= tb)
+            acc += tiles[i++];
+        bounds[b] = min(n, i * BALANCE_TILE);
+    }
+}
+
 // AES-ECB of independent blocks (one block per thread, keys from the keyset). Blocks whose key index is out of range
 // produce zeros.
 template <int NR>

@@ -370,11 +370,12 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     const u32 tsel_horner = 0x10000u + (u32)(G - 1) * GHASH_TABLE_BYTES;
     const u32 tsel_chunk = 0x10000u + 8u * GHASH_TABLE_BYTES;
 
-    const u64 n = args.nrecs, C = args.chunk;
+    const u64 n = args.nrecs, C = args.bounds != nullptr ? 0 : args.chunk;
     // this workgroup's records: the chunk [beg, end) (cstart: its first record), then the chunk grid * C further on
-    // (C != 0), or one contiguous range (C == 0)
-    const u64 beg = C != 0 ? min(n, (u64)blockIdx.x * C) : n * blockIdx.x / gridDim.x;
-    u64 end = C != 0 ? min(n, beg + C) : n * (blockIdx.x + 1) / gridDim.x, cstart = beg;
+    // (C != 0), or one contiguous range (C == 0): balanced by weight (args.bounds) or by count
+    const u64 beg = args.bounds != nullptr ? args.bounds[blockIdx.x] : C != 0 ? min(n, (u64)blockIdx.x * C) : n * blockIdx.x / gridDim.x;
+    u64 end = args.bounds != nullptr ? args.bounds[blockIdx.x + 1] : C != 0 ? min(n, beg + C) : n * (blockIdx.x + 1) / gridDim.x;
+    u64 cstart = beg;
     u32 loaded_key = 0xffffffffu, loaded_usrc = 0xffffffffu;
     // the descriptors in batch order, or (an ungrouped many-key batch) the key-grouped copy built on the device; ok
     // bytes go to the record's batch index either way

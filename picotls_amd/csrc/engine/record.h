@@ -69,6 +69,8 @@ struct BatchArgs {
     // w, w + grid, w + 2*grid, ... of `chunk` records each (records are dealt out across the batch, so a batch whose
     // record sizes follow its order still gives every workgroup a similar share of bytes)
     u64 chunk;
+    // chunked kernel: workgroup w walks records [bounds[w], bounds[w + 1]) (balance_bounds_kernel; null: chunk rule)
+    const u64 *bounds;
 };
 
 #define RUN_SCAN_CAP 256  // records examined per key-run scan (multi-key batches)

@@ -91,6 +91,7 @@ class Workload:
     desc: str = ""
     key_order: str = "grouped"  # many keys: "grouped" by connection, or "random" (key_idx = splitmix(i) mod nkeys)
     sorted_lens: bool = False  # mixed lengths in ascending order over the batch (a batch built by record size)
+    conn_classes: bool = False  # each connection (key) bulk (U[8 KiB, 16 KiB], one in four) or interactive (U[64, 1500])
 
     def scaled(self, nrecs: int) -> "Workload":
         return replace(self, nrecs=nrecs)
@@ -99,6 +100,13 @@ class Workload:
     def lens(self, begin: int, end: int) -> np.ndarray:
         if self.rec_len is not None:
             return np.full(end - begin, self.rec_len, dtype=np.uint64)
+        if self.conn_classes:
+            w = splitmix_words_np(self.seed ^ 0x4C454E, begin, end - begin)
+            key, _ = self.key_and_seq(begin, end)
+            bulk = (splitmix_words_np(self.seed ^ 0x434C53, 0, self.nkeys)[key] % np.uint64(4)) == 0
+            lo = np.where(bulk, np.uint64(8192), np.uint64(64))
+            span = np.where(bulk, np.uint64(16384 - 8192 + 1), np.uint64(1500 - 64 + 1))
+            return (lo + w % span).astype(np.uint64)
         if self.sorted_lens:
             w = np.sort(splitmix_words_np(self.seed ^ 0x4C454E, 0, self.nrecs) % np.uint64(self.max_len - self.min_len + 1))
             return (np.uint64(self.min_len) + w[begin:end]).astype(np.uint64)
@@ -181,11 +189,15 @@ WORKLOADS = {
                           desc="4M mixed-length records 64 B-16 KiB, AES-256-GCM, 64K traffic keys in random order"),
     "shard1200": Workload("shard1200", 32 << 20, 1200, 13, 16,
                           desc="32M x 1200 B records sharded evenly across GPUs, AES-128-GCM"),
-    # analysis variants (not BASELINE configs): isolate key switching and length mix from the AES-256 cost
+    # analysis variants (not BASELINE configs): isolate key switching and length mix from the AES-256 cost; batches
+    # ordered by record size (mixedsorted) and connections of two size classes (mixedconn) for the workgroup split
     "mixed1key": Workload("mixed1key", 4 << 20, None, 13, 32,
                           desc="4M mixed-length records 64 B-16 KiB, AES-256-GCM, one key"),
     "mixedsorted": Workload("mixedsorted", 4 << 20, None, 13, 32, sorted_lens=True,
                             desc="4M mixed-length records 64 B-16 KiB sorted by length, AES-256-GCM, one key"),
+    "mixedconn": Workload("mixedconn", 4 << 20, None, 13, 32, nkeys=65536, conn_classes=True,
+                          desc="4M records of 64K connections grouped, a quarter bulk (8-16 KiB records), the rest "
+                               "interactive (64-1500 B), AES-256-GCM"),
     "tls16k256": Workload("tls16k256", 1 << 20, 16384, 5, 32, tls_header_aad=True,
                           desc="1M x 16384 B TLS records, AES-256-GCM, one key"),
     "u8k256": Workload("u8k256", 4 << 20, 8192, 13, 32, desc="4M x 8192 B records, AES-256-GCM, one key"),
