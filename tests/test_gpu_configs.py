@@ -165,3 +165,61 @@ def test_sorted_lengths_dealt_chunks_vs_fusion():
         m[int(o):int(o) + int(ln)] = True
     assert np.array_equal(d_back.cpu().numpy()[m], pt[m])
     ks.free()
+
+
+def test_balanced_many_key_batch_with_skew_and_rejects_vs_fusion():
+    # a many-key batch large enough for the work-balanced workgroup ranges (balance_*_kernel): 150,000 records over 97
+    # connections, mostly 0-300 B but eight 256 KiB records at the front (one workgroup's share by count would hold
+    # them all), and rejected descriptors (length above the cap, key outside the keyset) among them: every valid record
+    # equals fusion's, the rejected ones write nothing and open with ok = 0
+    if not os.path.exists(os.path.join(REF_DIR, "libfusion_ref.so")):
+        pytest.skip("oracle/_ref/libfusion_ref.so not shipped")
+    from picotls_amd.records import RecordBatch
+
+    ref = FusionRef()
+    rng = np.random.default_rng(23)
+    n, nkeys = 150000, 97
+    lens = rng.integers(0, 301, n).astype(np.uint64)
+    lens[rng.choice(2000, 8, replace=False)] = 256 * 1024
+    key_idx = (np.arange(n) * nkeys // n).astype(np.uint32)
+    b = RecordBatch.build(lens, rng.integers(0, 40, n), seqs=rng.integers(0, 2**40, n, dtype=np.uint64), key_idx=key_idx)
+    keys, ivs = rng.bytes(32 * nkeys), rng.bytes(12 * nkeys)
+    keys_np, ivs_np = np.frombuffer(keys, np.uint8), np.frombuffer(ivs, np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(b.aad_bytes), np.uint8)
+    want = np.zeros(b.sealed_bytes, np.uint8)
+    ref.run_batch(True, keys_np, ivs_np, 32, b.seal, pt, aad, want, nthreads=_threads())
+    bad = np.sort(rng.choice(n, 40, replace=False))
+    seal, opn = b.seal.copy(), b.open.copy()
+    seal["len"][bad[:20]] = opn["len"][bad[:20]] = (1 << 30) + 7  # above PTLS_MI355X_MAX_RECORD_LEN
+    seal["key_idx"][bad[20:]] = opn["key_idx"][bad[20:]] = nkeys + 3  # not in the keyset
+    dev = torch.device("cuda:0")
+    ks = pa.Keyset(keys, ivs, 32)
+    s = torch.cuda.current_stream().cuda_stream
+    d_recs, d_pt, d_aad = (torch.from_numpy(x.view(np.uint8).copy()).to(dev) for x in (seal, pt, aad))
+    d_sealed = torch.full((b.sealed_bytes,), 0xEE, dtype=torch.uint8, device=dev)
+    pa.seal_batch(ks, d_recs.data_ptr(), n, d_pt.data_ptr(), d_aad.data_ptr(), d_sealed.data_ptr(), s)
+    torch.cuda.synchronize()
+    sealed = d_sealed.cpu().numpy()
+    isbad = np.zeros(n, bool)
+    isbad[bad] = True
+    mask = np.zeros(b.sealed_bytes, bool)  # the bytes of the valid records' outputs
+    for o, ln in zip(b.seal["out_off"][~isbad], b.seal["len"][~isbad]):
+        mask[int(o):int(o) + int(ln) + 16] = True
+    assert np.array_equal(sealed[mask], want[mask])
+    for i in bad:  # nothing written for a rejected record
+        o, ln = int(b.seal["out_off"][i]), int(b.seal["len"][i]) + 16
+        assert (sealed[o:o + ln] == 0xEE).all(), i
+    d_open = torch.from_numpy(opn.view(np.uint8).copy()).to(dev)
+    d_in = torch.from_numpy(want).to(dev)
+    d_back = torch.zeros(b.pt_bytes, dtype=torch.uint8, device=dev)
+    d_ok = torch.full((n,), 0xAA, dtype=torch.uint8, device=dev)
+    pa.open_batch(ks, d_open.data_ptr(), n, d_in.data_ptr(), d_aad.data_ptr(), d_back.data_ptr(), d_ok.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_ok.cpu().numpy().astype(bool), ~isbad)
+    big = np.flatnonzero(lens == 256 * 1024)
+    back = d_back.cpu().numpy()
+    for i in big:
+        o = int(b.seal["in_off"][i])
+        assert np.array_equal(back[o:o + 256 * 1024], pt[o:o + 256 * 1024]), i
+    ks.free()
