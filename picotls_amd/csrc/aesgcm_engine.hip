@@ -844,7 +844,7 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
             u32 *tiles = ks->d_group + gwords;
             bounds = (u64 *)(ks->d_group + gwords + twords);
             const u32 grid = (u32)(ncu < nrecs ? ncu : nrecs);
-            balance_tiles_kernel<<<(unsigned)min((ntiles + 3) / 4, ncu * 8), 256, 0, s>>>(recs, grouped, ctl + 1, nrecs, tiles);
+            balance_tiles_kernel<<<(unsigned)min((ntiles + 3) / 4, ncu * 8), 256, 0, s>>>(recs, grouped, ctl + 1, nrecs, (u32)frame, tiles);
             balance_bounds_kernel<<<1, 1024, 0, s>>>(tiles, nrecs, grid, bounds);
         }
         ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, ks->ct, open, recs, nrecs, in, aad, out, ok, s,

@@ -107,23 +107,24 @@ __global__ __launch_bounds__(256) void key_scatter_kernel(const ptls_mi355x_reco
 // < 2 % of a workgroup's share at the sizes this runs at). Both walk the descriptor order the chunked kernel walks.
 #define BALANCE_TILE 64
 
-__device__ __forceinline__ u32 balance_weight(const ptls_mi355x_record_t &r)
+__device__ __forceinline__ u32 balance_weight(const ptls_mi355x_record_t &r, u32 frame)
 {
-    const u32 aad = (u32)r.aad_len | (u32)r.flags << 16;
+    // (framed batches: flags carries the content type, the AAD is the record header)
+    const u32 aad = frame != 0 ? TLS12_AAD_SIZE : (u32)r.aad_len | (u32)r.flags << 16;
     const u32 steps = (u32)(((u64)aad + 15) / 16 + ((u64)r.len + 15) / 16 + 1 + 7) / 8;
     return (steps < 65535u ? steps : 65535u) + 1;
 }
 
 // tiles[t] = weight of records [t * 64, t * 64 + 64): one wave per tile
 __global__ __launch_bounds__(256) void balance_tiles_kernel(const ptls_mi355x_record_t *recs, const ptls_mi355x_record_t *grouped,
-                                                            const u32 *perm_on, u64 n, u32 *tiles)
+                                                            const u32 *perm_on, u64 n, u32 frame, u32 *tiles)
 {
     static_assert(BALANCE_TILE == 64, "one lane per record of a tile");
     const ptls_mi355x_record_t *r = perm_on != nullptr && *perm_on ? grouped : recs;
     const u64 ntiles = (n + BALANCE_TILE - 1) / BALANCE_TILE, lane = threadIdx.x & 63;
     for (u64 t = ((u64)blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < ntiles; t += ((u64)gridDim.x * blockDim.x) >> 6) {
         const u64 i = t * BALANCE_TILE + lane;
-        u32 w = i < n ? balance_weight(r[i]) : 0u;
+        u32 w = i < n ? balance_weight(r[i], frame) : 0u;
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1)
             w += (u32)__shfl_xor((int)w, off, 64);
