@@ -52,6 +52,7 @@
 #include "engine/segment.h"
 #include "engine/gcm_kernels.h"
 #include "engine/aux_kernels.h"
+#include "engine/span_kernels.h"
 
 // ------------------------------------------------------------------------------------------------ host side
 
@@ -167,6 +168,10 @@ static int set_kernel_attrs(void)
     HIP_TRY(hipFuncSetAttribute((const void *)hp_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
     HIP_TRY(hipFuncSetAttribute((const void *)hp_kernel<14>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
     HIP_TRY(hipFuncSetAttribute((const void *)quiclb_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_span_kernel<10, false>, hipFuncAttributeMaxDynamicSharedMemorySize, SPAN_LDS));
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_span_kernel<10, true>, hipFuncAttributeMaxDynamicSharedMemorySize, SPAN_LDS));
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_span_kernel<14, false>, hipFuncAttributeMaxDynamicSharedMemorySize, SPAN_LDS));
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_span_kernel<14, true>, hipFuncAttributeMaxDynamicSharedMemorySize, SPAN_LDS));
     return 0;
 }
 
@@ -791,6 +796,36 @@ static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int sche
     return 0;
 }
 
+// One long record (descriptor `one`, key entry `key`) over many workgroups (span_kernels.h): `units` 16-step units in
+// spans of 2^e, their partials at `part` (nspans x 16 B, device-addressable), then the combine launch, which writes the
+// tag or ok[0] and sets done_flag[0] when given.
+static int launch_span(const KeyEntry *key, int nr, bool open, const ptls_mi355x_record_t &one, const void *in, const void *aad,
+                       void *out, uint8_t *ok, u32 units, u32 e, u32 nspans, void *part, u32 *done_flag, hipStream_t s)
+{
+    BatchArgs a = {key, nullptr, 1, (const uint8_t *)in, (const uint8_t *)aad, (uint8_t *)out, ok, 0u, 1u, CHUNK_LOG2,
+                   nullptr, nullptr, nullptr, 1u, one, done_flag, 0, nullptr};
+    const u32 span = 1u << e;
+    if (nr == 10) {
+        if (open)
+            gcm_span_kernel<10, true><<<nspans, ENGINE_WG, SPAN_LDS, s>>>(a, span, units, (u32x4 *)part);
+        else
+            gcm_span_kernel<10, false><<<nspans, ENGINE_WG, SPAN_LDS, s>>>(a, span, units, (u32x4 *)part);
+    } else {
+        if (open)
+            gcm_span_kernel<14, true><<<nspans, ENGINE_WG, SPAN_LDS, s>>>(a, span, units, (u32x4 *)part);
+        else
+            gcm_span_kernel<14, false><<<nspans, ENGINE_WG, SPAN_LDS, s>>>(a, span, units, (u32x4 *)part);
+    }
+    HIP_TRY(hipGetLastError());
+    const size_t clds = GHASH_TABLE_BYTES + 16 * 257;
+    if (open)
+        span_combine_kernel<true><<<1, 256, clds, s>>>(a, nspans, e, (const u32x4 *)part);
+    else
+        span_combine_kernel<false><<<1, 256, clds, s>>>(a, nspans, e, (const u32x4 *)part);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
 // A batch call on a keyset: waits for the keyset's setup, groups an ungrouped many-key batch by key on the device, launches,
 // and records the use (teardown and rekey are ordered after it).
 static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
@@ -1008,6 +1043,9 @@ int ptls_mi355x_quiclb_batch(ptls_mi355x_keyset_t *ks, const ptls_mi355x_cid_t *
 #define PERREC_FLAG 1                       // a lone record's launch publishes a completion word the host polls (roundtrip)
 #endif
 #define PERREC_FLAG_SPIN_US 2000
+#ifndef SPAN_MIN_BYTES
+#define SPAN_MIN_BYTES ((size_t)262144)  // a lone record from this length runs over many workgroups (launch_span)
+#endif
 #define PERREC_FLAG_MAX_BYTES ((size_t)1 << 20)  // staged bytes of a call that polls (larger ones wait for the stream)
 
 // PTLS_MI355X_COMBINE_STATS=1: per-record launches, calls and the host time of run_calls, printed at exit (tools/gpu_mt.sh)
@@ -1034,11 +1072,15 @@ struct StageCall {
     DeviceState *ds;
     Stager *st = nullptr;
     size_t total = 0;
+    size_t clear_lo = 0, clear_hi = SIZE_MAX;  // the staged bytes that held plaintext (all unless narrowed)
     StageCall(DeviceState *d) : ds(d) {}
     ~StageCall()
     {
         if (st != nullptr) {
-            memset(st->h, 0, total);  // staged plaintext and keystream-derived bytes do not outlive the call
+            // staged plaintext does not outlive the call (with it gone, the ciphertext beside it reveals nothing)
+            const size_t hi = clear_hi < total ? clear_hi : total;
+            if (hi > clear_lo)
+                memset(st->h + clear_lo, 0, hi - clear_lo);
             stager_put(ds, st);
         }
     }
@@ -1164,10 +1206,28 @@ static void run_calls(DeviceState *ds, OneCall *const *c, size_t n)
     // completion words: one per workgroup of the last kernel (the GCM launch: one workgroup per record up to the CU
     // count; the header-protection launch: aux_grid)
     const size_t nflags = hp ? (size_t)aux_grid(n, ds->ncu) : (n < (size_t)ds->ncu ? n : (size_t)ds->ncu);
-    const size_t off_mask = off_ok + a16(n), off_flag = off_mask + 16 * n, total = off_flag + a16(4 * nflags);
+    // a lone long record runs over many workgroups (launch_span): 16-step units in spans of 2^e, at most one span per CU
+    u32 span_units = 0, span_e = 0, span_n = 0;
+    if (SPAN_MIN_BYTES != 0 && n == 1 && c0.len >= SPAN_MIN_BYTES && !c0.ks->ct && c0.ks->schedule != PTLS_MI355X_SCHEDULE_LOCKSTEP) {
+        const size_t steps = ((c0.aadlen + 15) / 16 + (c0.len + 15) / 16 + 1 + ENGINE_G - 1) / ENGINE_G;
+        span_units = (u32)((steps + CHUNK_STEPS - 1) / CHUNK_STEPS);
+        const u32 cap = ds->ncu < 256 ? (u32)ds->ncu : 256u;
+        while (((span_units + (1u << span_e) - 1) >> span_e) > cap)
+            ++span_e;
+        span_n = (span_units + (1u << span_e) - 1) >> span_e;
+        if ((1u << span_e) > SPAN_MAX_UNITS)
+            span_units = span_e = span_n = 0;
+    }
+    const size_t off_mask = off_ok + a16(n), off_flag = off_mask + 16 * n, off_span = off_flag + a16(4 * nflags),
+                 total = off_span + 16 * (size_t)span_n;
     int ret = -1;
     {
         StageCall call(ds);
+        // the plaintext side: a seal's inputs (up), an open's outputs (down); the copy path's device buffer is not cleared
+        if (open)
+            call.clear_lo = up;
+        else
+            call.clear_hi = up;
         if (call.acquire(total) == 0) {
             uint8_t *h = call.host(), *d = call.dev();
             const hipStream_t s = call.stream();
@@ -1209,12 +1269,17 @@ static void run_calls(DeviceState *ds, OneCall *const *c, size_t n)
             const u32 unit_log2 = n > 1 ? CHUNK_LOG2 : steps <= 24 ? 0 : steps <= 96 ? 1 : steps <= 400 ? 2 : steps <= 1600 ? 3 : CHUNK_LOG2;
             // (calls staging at most 1 MiB: a larger record's launch runs for hundreds of microseconds or more, which
             // the caller need not spend spinning on a core)
-            const bool flag = PERREC_FLAG && call.mapped() && c0.ks->schedule != PTLS_MI355X_SCHEDULE_LOCKSTEP && total <= PERREC_FLAG_MAX_BYTES;
+            const bool flag = PERREC_FLAG && call.mapped() && c0.ks->schedule != PTLS_MI355X_SCHEDULE_LOCKSTEP &&
+                              (total <= PERREC_FLAG_MAX_BYTES || span_n != 0);
             if (flag)
                 memset(h + off_flag, 0, 4 * nflags);
             if (ret == 0)
                 ret = call.roundtrip(up, [&] {
-                    if (launch_gcm(kbase, nkeys, nr, ds->ncu, c0.ks->schedule, c0.ks->ct, open, (const ptls_mi355x_record_t *)(d + off_rec),
+                    if (span_n != 0) {
+                        if (launch_span(kbase, nr, open, first, d, d, d, d + off_ok, span_units, span_e, span_n, d + off_span,
+                                        flag && !hp ? (u32 *)(d + off_flag) : nullptr, s) != 0)
+                            return -1;
+                    } else if (launch_gcm(kbase, nkeys, nr, ds->ncu, c0.ks->schedule, c0.ks->ct, open, (const ptls_mi355x_record_t *)(d + off_rec),
                                    n, d, d, d, d + off_ok, s, 0, unit_log2, nullptr, nullptr, nullptr, n == 1 ? &first : nullptr,
                                    flag && !hp ? (u32 *)(d + off_flag) : nullptr) != 0)
                         return -1;

@@ -374,3 +374,33 @@ def test_tls_records_on_pinned_host_arenas(ref):
         o, p0, ln = int(back_b.seal[i]["in_off"]), int(b.seal[i]["in_off"]), int(lens[i])
         assert np.array_equal(back[o:o + ln], pt[p0:p0 + ln])
     ks.free()
+
+
+@pytest.mark.parametrize("key_size", [16, 32])
+def test_long_records_over_many_workgroups_vs_fusion(ref, key_size):
+    # a lone record from 256 KiB on runs over many workgroups (launch_span: spans of 2^e 16-step units, their partials
+    # combined by a tree with H^(128 * 2^e)); lengths around the threshold and the span sizes, AADs of 0, 13 and 70,000
+    # bytes, through the per-record calls: sealed bytes equal fusion's, open recovers them, a flipped bit anywhere fails
+    rng = np.random.default_rng(4242 + key_size)
+    alg = pa.aes128gcm if key_size == 16 else pa.aes256gcm
+    key, iv = rng.bytes(key_size), rng.bytes(12)
+    enc, dec = pa.aead_new_direct(alg, True, key, iv), pa.aead_new_direct(alg, False, key, iv)
+    cases = [(262143, 13), (262144, 0), (262161, 13), (524288 + 5, 70000), ((1 << 20) + 17, 13), (3 * (1 << 20) + 1, 0),
+             ((1 << 22) + 2047, 13)]
+    for ln, al in cases:
+        pt, aad, seq = rng.bytes(ln), rng.bytes(al), int(rng.integers(0, 2**62))
+        want = ref.seal(key, iv, seq, aad, pt)
+        assert enc.encrypt(pt, seq, aad) == want, (ln, al)
+        assert dec.decrypt(want, seq, aad) == pt, (ln, al)
+        bad = bytearray(want)
+        bad[int(rng.integers(0, len(bad)))] ^= 0x08
+        assert dec.decrypt(bytes(bad), seq, aad) is None, (ln, al)
+    # with the header-protection mask of a sample after the long seal (a launch after the span launches)
+    hpkey = rng.bytes(key_size)
+    hp = pa.CtrCipher(hpkey)
+    pt, aad = rng.bytes(300000), rng.bytes(13)
+    sealed, mask = enc.encrypt_s(pt, 9, aad, hp, 299990)  # the sample reaches into the tag
+    assert (sealed, mask) == ref.seal_with_hp(key, iv, 9, aad, pt, hpkey, 299990)
+    hp.ks.free()
+    enc.free()
+    dec.free()
