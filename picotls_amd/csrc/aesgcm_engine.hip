@@ -1042,7 +1042,7 @@ int ptls_mi355x_quiclb_batch(ptls_mi355x_keyset_t *ks, const ptls_mi355x_cid_t *
 #ifndef PERREC_FLAG
 #define PERREC_FLAG 1                       // a lone record's launch publishes a completion word the host polls (roundtrip)
 #endif
-#define PERREC_FLAG_SPIN_US 2000
+#define PERREC_FLAG_SPIN_US 2000  // + 0.5 us per staged KiB: long records (the span path) poll to their end too
 #ifndef SPAN_MIN_BYTES
 #define SPAN_MIN_BYTES ((size_t)262144)  // a lone record from this length runs over many workgroups (launch_span)
 #endif
@@ -1096,7 +1096,8 @@ struct StageCall {
     // flag_off (mapped staging only, 0: none): nflags words, one per workgroup of the launch's last kernel, that it sets
     // once its results are written (BatchArgs::done_flag); the call returns when it sees them all, without the
     // stream's completion signal (the next user of this stager's stream is ordered after the kernel anyway). After
-    // PERREC_FLAG_SPIN_US without them (a launch queued behind others) the call waits for the stream as usual.
+    // PERREC_FLAG_SPIN_US (+ 0.5 us per staged KiB) without them (a launch queued behind others) the call waits for the
+    // stream as usual.
     bool mapped() const { return st->h_dev != nullptr; }
     template <typename Launch>
     int roundtrip(size_t up, Launch launch, size_t flag_off = 0, size_t nflags = 0)
@@ -1121,7 +1122,8 @@ struct StageCall {
                     return 0;
                 }
                 __builtin_ia32_pause();
-                if ((k & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(PERREC_FLAG_SPIN_US))
+                if ((k & 255) == 255 &&
+                    std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(PERREC_FLAG_SPIN_US + (int64_t)(total >> 11)))
                     break;
             }
         }
