@@ -1361,8 +1361,8 @@ static int submit(DeviceState *ds, OneCall *c)
                 ++cb.inflight;
                 cb.expect = take;
                 lk.unlock();
-                // a batch's calls must address their entries as u32 key indices from its lowest entry; a call of
-                // another slab further away than that runs on its own (never expected: slabs are 512 KiB apart)
+                // a batch's calls address their entries as key indices from its lowest entry; slabs are separate
+                // allocations, so a batch whose entries span more than 2^30 entries (never seen) runs call by call
                 auto near = [&](bool hp_entries) {
                     const KeyEntry *lo = nullptr, *hi = nullptr;
                     for (OneCall *x : batch) {
