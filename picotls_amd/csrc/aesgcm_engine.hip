@@ -132,7 +132,7 @@ struct DeviceState {
     std::vector<KeyEntry *> slots;
     std::vector<PendingSlot> pending;
     std::vector<hipEvent_t> events;
-    int combine = 4;              // PTLS_MI355X_COMBINE: combined per-record launches in flight per kind (0: none)
+    int combine = 0;              // PTLS_MI355X_COMBINE: combined per-record launches in flight per kind (0: none)
     Combiner comb[32];
 };
 
@@ -1147,10 +1147,12 @@ static void seen_ready(ptls_mi355x_keyset_t *ks) { ks->ready_seen.store(true, st
 // itself. A lone caller thus launches at once, as before, while N threads calling together share launches instead of
 // queueing theirs on the device's few hardware queues (tools/mt_records.py). The entries of one-key keysets live in
 // per-device slabs, so a combined batch addresses them as key indices from the lowest entry of the batch.
-// PTLS_MI355X_COMBINE=k sets the launches in flight per kind (default 4); 0 runs every call on its own. Measured
-// (tools/mt_records.c, 1200-byte seals, one box): 16 threads 222K calls/s on their own, 264-269K combined (2.7 calls
-// a launch, p50 57 vs 76 us); 1-8 threads unchanged. A launch costs the host ~34 us (~24 of them waiting for the
-// stream), so calls in flight / 34 us bounds the rate whatever the combining.
+// PTLS_MI355X_COMBINE=k turns it on with k launches in flight per kind (default 0: every call on its own). Measured
+// (tools/mt_records.c, 1200-byte seals): while a call waited for its stream's completion signal, 16 threads made 222K
+// calls/s on their own and 264-269K combined (2.7 calls a launch). Once calls poll their completion words (roundtrip)
+// a lone call is cheaper than a share of a batch: 16 threads 302K calls/s on their own against 249K combined (16 B:
+// 352K / 270K; 16 KiB: 179K / 189K), so combining is off by default
+// (profiles/r2_per_record/final_mt_and_skew.txt).
 
 struct OneCall {
     ptls_mi355x_keyset_t *ks;

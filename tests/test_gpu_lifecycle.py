@@ -81,10 +81,10 @@ def test_threads_with_own_contexts_and_churn(ref):
 
 
 def test_combined_per_record_calls_across_threads(ref):
-    # per-record calls of many threads arriving together are combined into shared launches (submit() in
-    # aesgcm_engine.hip): 16 threads, AES-128 and AES-256 contexts, seal, open (a quarter tampered), seal with the
-    # header-protection mask (encrypt_s) and records above the combining cap (64 KiB, run on their own), released in
-    # bursts by a barrier; every output, ok result and mask equals fusion's
+    # per-record calls of many threads arriving together (each on its own launch by default; combined into shared
+    # launches under PTLS_MI355X_COMBINE, which the C vtable suite runs): 16 threads, AES-128 and AES-256 contexts,
+    # seal, open (a quarter tampered), seal with the header-protection mask (encrypt_s) and records above the combining
+    # cap (64 KiB), released in bursts by a barrier; every output, ok result and mask equals fusion's
     nthreads, nops = 16, 48
     barrier = threading.Barrier(nthreads)
     errors = []

@@ -608,12 +608,12 @@ def test_schedule_argument_checked():
     assert pa.load_library().ptls_mi355x_keyset_set_schedule(ks.handle, 7) == -1
 
 
-@pytest.mark.parametrize("combine", [None, "0", "1"])
+@pytest.mark.parametrize("combine", [None, "1", "4"])
 def test_picotls_vtable_pairs(combine):
     # cross-backend pairs in the reference's style (t/picotls.c:224-370): seal with fusion / open with MI355X and back,
     # through ptls_aead_new_direct + the ptls_aead_algorithm_t objects (tests/c/test_vtable.c); its thread tests run the
-    # per-record calls combined across threads (default: 4 launches in flight per kind), each call on its own (0) and
-    # with one launch in flight per kind (1: the largest batches)
+    # per-record calls each on its own (the default) and combined across threads with 1 (the largest batches) and 4
+    # launches in flight per kind (PTLS_MI355X_COMBINE)
     import subprocess
 
     exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "_bin", "test_vtable")
