@@ -8,6 +8,9 @@
 #ifndef AES_TTAB_COPY
 #define AES_TTAB_COPY 1
 #endif
+#ifndef AES_TTAB_BATCH
+#define AES_TTAB_BATCH 4
+#endif
 
 // AES T-table: Te0 replicated into banks 0..31 (bytes 0..127 of row n), Te2 = rotl16(Te0) into bytes 128..255
 constexpr u32 aes_ttab_word(const SboxTable &sb, u32 idx)
@@ -41,16 +44,17 @@ __device__ void build_aes_tables(lds_u8 *lds, u32 skip = 0, u32 end = 0)
 #if AES_TTAB_COPY
     const u32x4 *src = (const u32x4 *)g_aes_ttab.v;
     lds_u32x4 *dst = (lds_u32x4 *)lds;
-    // every thread's loads are in flight before its first LDS write
-    for (u32 base = 0; base < 256 * 64 / 4; base += 4 * nthr) {
-        u32x4 v[4];
+    // every thread's loads are in flight before its first LDS write (AES_TTAB_BATCH of them: one round trip for 512
+    // threads or more)
+    for (u32 base = 0; base < 256 * 64 / 4; base += AES_TTAB_BATCH * nthr) {
+        u32x4 v[AES_TTAB_BATCH];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < AES_TTAB_BATCH; ++k) {
             const u32 idx = base + tid + k * nthr;
             v[k] = idx < 256 * 64 / 4 ? src[idx] : u32x4{0, 0, 0, 0};
         }
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < AES_TTAB_BATCH; ++k) {
             const u32 idx = base + tid + k * nthr;
             if (idx < 256 * 64 / 4)
                 dst[idx] = v[k];

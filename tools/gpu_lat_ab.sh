@@ -2,7 +2,7 @@
 # multi-thread rates of both at 1200 B
 set +e
 cd $GRAFT_REPO_ROOT
-NEW=picotls_amd/_lib; BASE=${LAT_BASE:-tools/variants/noflag}
+NEW=${LAT_NEW:-picotls_amd/_lib}; BASE=${LAT_BASE:-tools/variants/noflag}
 for i in 1 2; do
   for L in $BASE $NEW; do
     timeout -k 10 120 python tools/latency.py $L/libptls_mi355x.so > gpurun_out/lat.log 2>&1; rc=$?

@@ -1,16 +1,12 @@
-# AES T-table copied from a compile-time image vs derived per launch: small batches, a lone record, bulk, phases, GPU suite
+# AES table copy with 8 loads in flight per thread (vs 4): GPU suite, small-batch launches and per-record latency A/B,
+# bulk A/B
 set +e
-A=tools/variants/lib_derive.so; B=tools/variants/lib_copy.so
-timeout -k 10 300 python tools/small_batch.py $A $B --rounds 3 > gpurun_out/ttab_small.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/ttab_small.log | cut -c1-130; [ $rc -ne 0 ] && exit $rc
-for w in tls16k_1048576 quic1200_4194304 mixed_4194304; do n=${w##*_}; wl=${w%_*}
-  timeout -k 10 280 python tools/ab.py $A $B --workload $wl --records $n --rounds 3 --reps 2 > gpurun_out/ttab_$wl.log 2>&1
-  rc=$?; echo "== $wl rc=$rc"; grep -v amdgpu.ids gpurun_out/ttab_$wl.log | cut -c1-150; [ $rc -ne 0 ] && exit $rc
+cd $GRAFT_REPO_ROOT
+bash tools/gpu_tests.sh -k "first_run or per_record or fuzz" || exit 1
+timeout -k 10 300 python tools/small_batch.py tools/variants/lib_base.so tools/variants/lib_new.so > gpurun_out/small_batch.log 2>&1; rc=$?
+grep -v amdgpu.ids gpurun_out/small_batch.log; [ $rc -ne 0 ] && exit $rc
+for w in "tls16k 1048576" "quic1200 4194304"; do set -- $w
+  timeout -k 10 300 python tools/ab.py tools/variants/lib_base.so tools/variants/lib_new.so --workload $1 --records $2 --rounds 3 --reps 2 > gpurun_out/ab_$1.log 2>&1; rc=$?
+  echo "== $1 rc=$rc"; grep -v amdgpu.ids gpurun_out/ab_$1.log | tail -2; [ $rc -ne 0 ] && exit $rc
 done
-timeout -k 10 200 python tools/latency.py > gpurun_out/ttab_lat.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/ttab_lat.log; [ $rc -ne 0 ] && exit $rc
-cd tools
-for w in "tls16k 1" "tls16k 1000" "quic1200 1000" "tls16k 262144" "mixed 4194304"; do set -- $w
-  timeout -k 10 200 python prof_phases.py variants/lib_prof.so --workload $1 --records $2 --reps 5 2>&1 | grep -v amdgpu.ids || exit 1
-done
-cd ..
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_gpu.log; exit $rc
+LAT_BASE=tools/variants/b4 LAT_NEW=tools/variants/b8 bash tools/gpu_lat_ab.sh
