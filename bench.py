@@ -1,13 +1,16 @@
 #!/usr/bin/env python3
 """AES-GCM seal+open throughput of the MI355X record engine (BASELINE.json metric), device-resident.
 
-    python bench.py [--gpus N --steps K --warmup W] [--workload tls16k] [--extra quic1200,mixed,mixedrand,ptlsbench]
-                    [--no-cpu-baseline]
+    python bench.py [--gpus N --steps K --warmup W] [--workload tls16k]
+                    [--extra quic1200,mixed,mixedrand,shard1200,ptlsbench] [--no-cpu-baseline]
 
 One step = seal the whole batch, then open the sealed batch again (one launch each), inputs already in HBM.
 value = (sum L sealed + sum L opened) over all ranks / max-over-ranks wall time of the K timed steps, in GiB/s
-(2^30 bytes). Multi-GPU (torchrun, one process per GPU): every rank seals/opens its own full batch (weak scaling,
-independent record shards, no collective on the data path; a barrier + max-reduce of the timings only).
+(2^30 bytes). Multi-GPU: one process per GPU. Under torch.distributed.run (the driver's N > 1 form) every rank is one
+of its processes; `python bench.py --gpus N` on its own starts torch.distributed.run with N ranks as a child process
+and relays rank 0's line. The headline workload is weak scaling (every rank seals/opens its own full batch); the
+shard1200 leg (configs[4]: 32M x 1200 B split across the ranks) is strong scaling. Independent record shards, no
+collective on the data path; a barrier + max/sum reductions of the timings only.
 
 Also reported:
   roofline      dominant kernel (seal), algorithmic bytes per launch / average launch time (HIP events on the
@@ -44,7 +47,7 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="tls16k")
-    p.add_argument("--extra", default="quic1200,mixed,mixedrand,ptlsbench",
+    p.add_argument("--extra", default="quic1200,mixed,mixedrand,shard1200,ptlsbench",
                    help="comma list of extra workloads to report ('' for none)")
     p.add_argument("--records", type=int, default=0, help="override record count (smaller runs)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -58,14 +61,46 @@ def parse():
     return p.parse_args()
 
 
+def self_launch(gpus: int):
+    """`bench.py --gpus N` (N > 1) outside torch.distributed.run: start the N ranks as ONE child process
+    (`python -m torch.distributed.run --nproc-per-node N bench.py <same args>`, rendezvous on 127.0.0.1), relay rank 0's
+    JSON line as this process's last stdout line and return the child's exit code. Called before anything touches the
+    GPU (this process never initialises HIP; the ranks do, in their own processes). None when there is nothing to
+    launch (N = 1, or already a rank)."""
+    if gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    line = None
+    with subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env) as p:
+        for out in p.stdout:  # progress and warnings pass through on stderr; the result line is printed last
+            if out.startswith("{") and '"metric"' in out:
+                line = out
+            else:
+                sys.stderr.write(out)
+        rc = p.wait()
+    if line is not None:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    return rc if line is not None or rc != 0 else 1
+
+
 def make_rank(gpus: int):
     import torch
 
     from picotls_amd.dist import RankContext
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world == 1 and gpus > 1:
-        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
+    if gpus > 1 and world != gpus:
+        raise SystemExit(f"--gpus {gpus} but WORLD_SIZE={world}: one rank per GPU")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal of the multi-rank path on a one-GPU box: every rank on cuda:0, gloo for the barrier/reductions
     one_device = os.environ.get("PTLS_BENCH_ONE_DEVICE") == "1"
@@ -145,7 +180,7 @@ def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool
     if verify:
         ok_all = bool(d_ok.min().item() == 1) if b.n else True
         same = bool(torch.equal(d_back, d_pt))
-        res["verified_roundtrip"] = ok_all and same
+        res["verified_roundtrip"] = R.sum(float(ok_all and same)) == R.world  # every rank's shard round-trips
         # records for the bit-exact fusion check, which runs in the cpu_baseline leg (rank 0)
         res["sample"] = collect_sample(wl, b, keys, ivs, d_pt, d_aad, d_sealed) if R.rank == 0 else None
     del d_pt, d_sealed, d_back, d_ok, d_seal, d_open, d_aad
@@ -532,6 +567,9 @@ def traffic_from_profiles(workload: str, records: int):
 
 def main():
     args = parse()
+    rc = self_launch(args.gpus)
+    if rc is not None:
+        sys.exit(rc)
     from picotls_amd.workloads import WORKLOADS
 
     from picotls_amd.dist import aggregate_throughput
@@ -599,6 +637,8 @@ def main():
         samples[name] = r2.get("sample")
         v2, _ = aggregate_throughput(R, r2["payload_bytes"], r2["wall_s"], args.steps)
         extra[name] = {"value": round(v2, 3), "unit": "GiB/s", "desc": w2.desc,
+                       "scaling": "strong" if name == "shard1200" else "weak", "n_gpus": R.world,
+                       "records_total": int(R.sum(float(r2["records"]))),
                        "records_per_gpu": r2["records"], "record_len": w2.rec_len or "U[64,16384]",
                        "aead": f"AES-{8 * w2.key_size}-GCM", "keys": w2.nkeys, "key_order": w2.key_order,
                        "seal_GiBps": round(r2["payload_bytes"] / (r2["seal_ms"] / 1e3) / 2**30, 3),

@@ -96,6 +96,8 @@ ptls_mi355x_keyset_t *ptls_mi355x_keyset_new(const void *keys, const void *ivs, 
 void ptls_mi355x_keyset_free(ptls_mi355x_keyset_t *ks);
 size_t ptls_mi355x_keyset_size(const ptls_mi355x_keyset_t *ks);
 size_t ptls_mi355x_keyset_key_size(const ptls_mi355x_keyset_t *ks);
+/* the HIP device the keyset's entries live on (the current device when it was created) */
+int ptls_mi355x_keyset_device(const ptls_mi355x_keyset_t *ks);
 /**
  * Replaces the key and static IV of the n entries key_idx[0..n) (host arrays: n * key_size key bytes, n * 12 IV bytes),
  * deriving their schedules and H powers on the device: the rekey of some connections of a many-connection keyset, e.g.
@@ -134,9 +136,13 @@ int ptls_mi355x_keyset_set_schedule(ptls_mi355x_keyset_t *ks, int schedule);
  * combine do, in 0.5 % of the kernel's LDS cycles. With on != 0 the keyset's batches and per-record
  * calls use the variant in which every LDS access has a data-independent pattern (SQ_LDS_BANK_CONFLICT equal for any
  * key and payload), at 2-10 % of throughput. The environment variable PTLS_MI355X_CONSTANT_TIME=1 (read when a device
- * is first used) sets it for every keyset, including those behind the picotls objects. Returns 0, or -1.
+ * is first used) sets it for every keyset created afterwards. The picotls AEAD objects (mi355x_picotls.h) turn it on for
+ * their keysets by default, as they replace a constant-time backend; PTLS_MI355X_CONSTANT_TIME=0 turns that off.
+ * Returns 0, or -1.
  */
 int ptls_mi355x_keyset_set_constant_time(ptls_mi355x_keyset_t *ks, int on);
+/* 1 when the keyset uses the constant-time variant, else 0 */
+int ptls_mi355x_keyset_get_constant_time(const ptls_mi355x_keyset_t *ks);
 
 /**
  * Seals nrecs records in one launch. Asynchronous on `stream`. recs, in, aad, out (and ok, results of the calls below)
@@ -273,7 +279,16 @@ int ptls_mi355x_quiclb_transform(ptls_mi355x_keyset_t *ks, size_t key_idx, void 
  * PTLS_MI355X_MAX_RECORD_LEN / PTLS_MI355X_MAX_AAD_LEN (fusion has no limit; TLS and QUIC records are far below it).
  * Environment, read when a device is first used: PTLS_MI355X_MAX_STAGE_BYTES caps the staging buffer of one call (a
  * larger record fails), PTLS_MI355X_STAGE_COPY=1 copies through device memory instead of mapping the pinned buffer.
+ *
+ * The staging pool is bounded (fusion's context owns one allocation and frees it, lib/fusion.c:1043-1049): per device
+ * at most PTLS_MI355X_STAGE_POOL_BYTES (default 64 MiB) of idle pinned buffers are kept for later calls, a buffer above
+ * 16 MiB (a call on a record above ~8 MiB) is freed when its call returns (hipHostFree, which waits for the device), and
+ * the calls of a device share at most 16 streams.
  */
+/* pinned host bytes the staging pools hold now, idle and in use, over all devices */
+size_t ptls_mi355x_staging_bytes(void);
+/* frees every idle staging buffer (e.g. before process exit); calls in progress keep theirs */
+void ptls_mi355x_release_staging(void);
 int ptls_mi355x_encrypt(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const void *input, size_t inlen, uint64_t seq,
                         const void *aad, size_t aadlen);
 size_t ptls_mi355x_decrypt(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output, const void *input, size_t inlen,

@@ -36,11 +36,13 @@ ABI_FUNCTIONS = (
     "ptls_mi355x_keyset_free",
     "ptls_mi355x_keyset_size",
     "ptls_mi355x_keyset_key_size",
+    "ptls_mi355x_keyset_device",
     "ptls_mi355x_keyset_get_iv",
     "ptls_mi355x_keyset_set_iv",
     "ptls_mi355x_keyset_update",
     "ptls_mi355x_keyset_set_schedule",
     "ptls_mi355x_keyset_set_constant_time",
+    "ptls_mi355x_keyset_get_constant_time",
     "ptls_mi355x_seal_batch",
     "ptls_mi355x_open_batch",
     "ptls_mi355x_seal_tls_records",
@@ -57,6 +59,8 @@ ABI_FUNCTIONS = (
     "ptls_mi355x_encrypt_s",
     "ptls_mi355x_decrypt",
     "ptls_mi355x_encrypt_block",
+    "ptls_mi355x_staging_bytes",
+    "ptls_mi355x_release_staging",
     "ptls_mi355x_last_error",
 )
 
@@ -86,11 +90,17 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.ptls_mi355x_keyset_size.restype = sz
     lib.ptls_mi355x_keyset_key_size.argtypes = [vp]
     lib.ptls_mi355x_keyset_key_size.restype = sz
+    lib.ptls_mi355x_keyset_device.argtypes = [vp]
+    lib.ptls_mi355x_keyset_device.restype = ci
+    lib.ptls_mi355x_staging_bytes.restype = sz
+    lib.ptls_mi355x_release_staging.restype = None
     lib.ptls_mi355x_keyset_get_iv.argtypes = [vp, sz, vp]
     lib.ptls_mi355x_keyset_set_iv.argtypes = [vp, sz, vp]
     lib.ptls_mi355x_keyset_update.argtypes = [vp, vp, vp, vp, sz]
     lib.ptls_mi355x_keyset_set_schedule.argtypes = [vp, ci]
     lib.ptls_mi355x_keyset_set_constant_time.argtypes = [vp, ci]
+    lib.ptls_mi355x_keyset_get_constant_time.argtypes = [vp]
+    lib.ptls_mi355x_keyset_get_constant_time.restype = ci
     lib.ptls_mi355x_seal_batch.argtypes = [vp, vp, sz, vp, vp, vp, vp]
     lib.ptls_mi355x_open_batch.argtypes = [vp, vp, sz, vp, vp, vp, vp, vp]
     lib.ptls_mi355x_ecb_batch.argtypes = [vp, vp, vp, vp, sz, vp]
@@ -188,6 +198,10 @@ class Keyset:
         """Constant-time GHASH variant (ptls_mi355x_keyset_set_constant_time)."""
         if load_library().ptls_mi355x_keyset_set_constant_time(self.handle, 1 if on else 0) != 0:
             raise _err("set_constant_time")
+
+    @property
+    def constant_time(self) -> bool:
+        return bool(load_library().ptls_mi355x_keyset_get_constant_time(self.handle))
 
     SCHEDULES = {"auto": 0, "lockstep": 1, "chunked": 2}
 
@@ -298,6 +312,8 @@ class AeadContext:
         self.is_enc = is_enc
         self._iv = bytes(iv)
         self.ks = Keyset(key, iv, algo.key_size)
+        # as the picotls objects (ptls_mi355x.c aesgcm_setup): constant-time unless PTLS_MI355X_CONSTANT_TIME=0
+        self.ks.set_constant_time(os.environ.get("PTLS_MI355X_CONSTANT_TIME") != "0")
 
     def free(self):
         self.ks.free()
@@ -394,6 +410,16 @@ class QuicLbCipher:
                                                        1 if self.is_enc else 0) != 0:
             raise _err("ptls_mi355x_quiclb_transform")
         return bytes(out)
+
+
+def staging_bytes() -> int:
+    """Pinned host bytes held by the per-record path's staging pools (ptls_mi355x_staging_bytes)."""
+    return int(load_library().ptls_mi355x_staging_bytes())
+
+
+def release_staging() -> None:
+    """Frees the idle staging buffers (ptls_mi355x_release_staging)."""
+    load_library().ptls_mi355x_release_staging()
 
 
 def aead_new_direct(algo: AeadAlgorithm, is_enc: bool, key: bytes, iv: bytes) -> AeadContext:

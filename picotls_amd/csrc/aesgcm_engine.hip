@@ -94,9 +94,14 @@ static void clear_memory(void *p, size_t n)  // ptls_clear_memory: a memset the 
 #define MAX_DEVICES 64
 #define STAGE_CLASSES 26   // pinned staging buffers of 4 KiB << class
 #define SLAB_ENTRIES 1024  // one-key keyset entries per slab (512 KiB)
+// Bounds of the staging pool (fusion's context owns one allocation and frees it, lib/fusion.c:1043-1049; here the pinned
+// buffers outlive calls so that the next call of a thread skips hipHostMalloc, but not without limit):
+#define STAGE_POOL_BYTES ((size_t)64 << 20)  // idle pinned bytes kept per device (PTLS_MI355X_STAGE_POOL_BYTES)
+#define STAGE_KEEP_MAX ((size_t)16 << 20)     // a buffer above this (a call of a record > ~8 MiB) is freed after its call
+#define STAGE_STREAMS 16                      // stager streams per device, shared round-robin beyond that
 
 struct Stager {
-    hipStream_t stream;
+    hipStream_t stream;  // one of the device's stager streams (DeviceState::stage_streams), not owned
     uint8_t *h;      // pinned host buffer
     uint8_t *h_dev;  // its device address (NULL: not mapped, or PTLS_MI355X_STAGE_COPY=1: round trips copy through d)
     uint8_t *d;      // device buffer of the copy path
@@ -107,6 +112,7 @@ struct Stager {
 
 struct PendingSlot {
     KeyEntry *e;
+    KeyEntry *slab;
     hipEvent_t cleared;
 };
 
@@ -127,9 +133,15 @@ struct DeviceState {
     bool force_copy = false;      // PTLS_MI355X_STAGE_COPY=1: the staging round trip copies instead of mapping
     size_t stage_limit = 0;       // PTLS_MI355X_MAX_STAGE_BYTES: the largest staging buffer one call may use
     bool ct_default = false;      // PTLS_MI355X_CONSTANT_TIME=1: new keysets use the constant-time GHASH variant
+    bool fault_order = false;     // PTLS_MI355X_FAULT_ORDER=1 (tests only): keyset teardown cannot order itself on the device
     std::mutex mu;                // the pools below
     Stager *stagers[STAGE_CLASSES] = {};
-    std::vector<KeyEntry *> slots;
+    size_t stage_idle = 0;        // pinned bytes of the idle stagers above
+    size_t stage_busy = 0;        // ... and of the stagers in use by calls
+    size_t stage_pool_cap = STAGE_POOL_BYTES;
+    std::vector<hipStream_t> stage_streams;  // at most STAGE_STREAMS
+    unsigned stage_rr = 0;
+    std::vector<std::pair<KeyEntry *, KeyEntry *>> slots;  // free one-key entries and the slab each lies in
     std::vector<PendingSlot> pending;
     std::vector<hipEvent_t> events;
     int combine = 0;              // PTLS_MI355X_COMBINE: combined per-record launches in flight per kind (0: none)
@@ -168,10 +180,14 @@ static int set_kernel_attrs(void)
     HIP_TRY(hipFuncSetAttribute((const void *)hp_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
     HIP_TRY(hipFuncSetAttribute((const void *)hp_kernel<14>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
     HIP_TRY(hipFuncSetAttribute((const void *)quiclb_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
-    HIP_TRY(hipFuncSetAttribute((const void *)gcm_span_kernel<10, false>, hipFuncAttributeMaxDynamicSharedMemorySize, SPAN_LDS));
-    HIP_TRY(hipFuncSetAttribute((const void *)gcm_span_kernel<10, true>, hipFuncAttributeMaxDynamicSharedMemorySize, SPAN_LDS));
-    HIP_TRY(hipFuncSetAttribute((const void *)gcm_span_kernel<14, false>, hipFuncAttributeMaxDynamicSharedMemorySize, SPAN_LDS));
-    HIP_TRY(hipFuncSetAttribute((const void *)gcm_span_kernel<14, true>, hipFuncAttributeMaxDynamicSharedMemorySize, SPAN_LDS));
+#define SPAN_ATTR(nr, open)                                                                                            \
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_span_kernel<nr, open, false>, hipFuncAttributeMaxDynamicSharedMemorySize, SPAN_LDS)); \
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_span_kernel<nr, open, true>, hipFuncAttributeMaxDynamicSharedMemorySize, SPAN_LDS))
+    SPAN_ATTR(10, false);
+    SPAN_ATTR(10, true);
+    SPAN_ATTR(14, false);
+    SPAN_ATTR(14, true);
+#undef SPAN_ATTR
     return 0;
 }
 
@@ -202,6 +218,10 @@ static DeviceState *device_state(int dev)
     const char *comb = getenv("PTLS_MI355X_COMBINE");
     if (comb != nullptr)
         ds->combine = atoi(comb) < 0 ? 0 : atoi(comb);
+    const char *pool = getenv("PTLS_MI355X_STAGE_POOL_BYTES"), *fo = getenv("PTLS_MI355X_FAULT_ORDER");
+    if (pool != nullptr)
+        ds->stage_pool_cap = (size_t)strtoull(pool, nullptr, 0);
+    ds->fault_order = fo != nullptr && strcmp(fo, "1") == 0;
     ds->stage_limit = limit != nullptr ? (size_t)strtoull(limit, nullptr, 0) : (size_t)4096 << (STAGE_CLASSES - 1);
     int least = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &ds->priority) != hipSuccess)
@@ -270,15 +290,16 @@ static void event_put(DeviceState *ds, hipEvent_t e)
     ds->events.push_back(e);
 }
 
-// one cleared keyset entry from the slab: a free one, else one whose clearing (keyset_free) has completed, else a new slab
-static KeyEntry *slot_get(DeviceState *ds)
+// one cleared keyset entry from the slab: a free one, else one whose clearing (keyset_free) has completed, else a new
+// slab; *slab is the slab the entry lies in (entries of one slab may be addressed relative to each other)
+static KeyEntry *slot_get(DeviceState *ds, KeyEntry **slab_of)
 {
     {
         std::lock_guard<std::mutex> lk(ds->mu);
         if (ds->slots.empty()) {
             for (size_t i = 0; i < ds->pending.size();) {
                 if (hipEventQuery(ds->pending[i].cleared) == hipSuccess) {
-                    ds->slots.push_back(ds->pending[i].e);
+                    ds->slots.emplace_back(ds->pending[i].e, ds->pending[i].slab);
                     ds->events.push_back(ds->pending[i].cleared);
                     ds->pending[i] = ds->pending.back();
                     ds->pending.pop_back();
@@ -288,9 +309,10 @@ static KeyEntry *slot_get(DeviceState *ds)
             }
         }
         if (!ds->slots.empty()) {
-            KeyEntry *e = ds->slots.back();
+            const auto e = ds->slots.back();
             ds->slots.pop_back();
-            return e;
+            *slab_of = e.second;
+            return e.first;
         }
     }
     KeyEntry *slab = nullptr;
@@ -300,8 +322,17 @@ static KeyEntry *slot_get(DeviceState *ds)
     }
     std::lock_guard<std::mutex> lk(ds->mu);
     for (int i = SLAB_ENTRIES - 1; i >= 1; --i)
-        ds->slots.push_back(slab + i);
+        ds->slots.emplace_back(slab + i, slab);
+    *slab_of = slab;
     return slab;
+}
+
+static void stager_destroy(Stager *s)
+{
+    if (s->d != nullptr)
+        (void)hipFree(s->d);
+    (void)hipHostFree(s->h);  // (an implicit device synchronisation: only buffers beyond the pool's bounds get here)
+    delete s;
 }
 
 static Stager *stager_get(DeviceState *ds, size_t bytes)
@@ -317,28 +348,38 @@ static Stager *stager_get(DeviceState *ds, size_t bytes)
         fail("%s", "staging: record too large");
         return nullptr;
     }
+    hipStream_t stream = nullptr;
     {
         std::lock_guard<std::mutex> lk(ds->mu);
         Stager *s = ds->stagers[cls];
         if (s != nullptr) {
             ds->stagers[cls] = s->next;
+            ds->stage_idle -= s->cap;
+            ds->stage_busy += s->cap;
             return s;
         }
+        // the device's stager streams: created up to STAGE_STREAMS, then shared (a call then may wait for another
+        // call's launch on the same stream; calls beyond that many at once would share the few hardware queues anyway)
+        if (ds->stage_streams.size() >= STAGE_STREAMS)
+            stream = ds->stage_streams[ds->stage_rr++ % STAGE_STREAMS];
+    }
+    if (stream == nullptr) {
+        if (hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, ds->priority) != hipSuccess) {
+            fail("%s", "staging: stream creation failed");
+            return nullptr;
+        }
+        std::lock_guard<std::mutex> lk(ds->mu);
+        ds->stage_streams.push_back(stream);
     }
     Stager *s = new (std::nothrow) Stager();
     if (s == nullptr) {
         fail("%s", "out of memory");
         return nullptr;
     }
+    s->stream = stream;
     s->cap = (size_t)4096 << cls;
     s->cls = cls;
-    if (hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, ds->priority) != hipSuccess) {
-        delete s;
-        fail("%s", "staging: stream creation failed");
-        return nullptr;
-    }
     if (hipHostMalloc((void **)&s->h, s->cap, hipHostMallocDefault) != hipSuccess) {
-        (void)hipStreamDestroy(s->stream);
         delete s;
         fail("%s", "staging: pinned host allocation failed");
         return nullptr;
@@ -347,19 +388,30 @@ static Stager *stager_get(DeviceState *ds, size_t bytes)
         s->h_dev = nullptr;
     if (s->h_dev == nullptr && hipMalloc((void **)&s->d, s->cap) != hipSuccess) {
         (void)hipHostFree(s->h);
-        (void)hipStreamDestroy(s->stream);
         delete s;
         fail("%s", "staging: device allocation failed");
         return nullptr;
     }
+    std::lock_guard<std::mutex> lk(ds->mu);
+    ds->stage_busy += s->cap;
     return s;
 }
 
+// back to the pool after its call (nothing of the call is still queued on its stream); a buffer beyond the pool's bounds
+// (above STAGE_KEEP_MAX, or with the idle pool full) is freed instead
 static void stager_put(DeviceState *ds, Stager *s)
 {
-    std::lock_guard<std::mutex> lk(ds->mu);
-    s->next = ds->stagers[s->cls];
-    ds->stagers[s->cls] = s;
+    {
+        std::lock_guard<std::mutex> lk(ds->mu);
+        ds->stage_busy -= s->cap;
+        if (s->cap <= STAGE_KEEP_MAX && ds->stage_idle + s->cap <= ds->stage_pool_cap) {
+            s->next = ds->stagers[s->cls];
+            ds->stagers[s->cls] = s;
+            ds->stage_idle += s->cap;
+            return;
+        }
+    }
+    stager_destroy(s);
 }
 
 struct st_ptls_mi355x_keyset_t {
@@ -369,6 +421,7 @@ struct st_ptls_mi355x_keyset_t {
     int nr;
     KeyEntry *d_keys;
     bool slot;  // d_keys is one entry of the device's slab (one-key keysets)
+    KeyEntry *slab;  // ... that slab
     int schedule;
     bool ct;                           // constant-time GHASH (ptls_mi355x_keyset_set_constant_time)
     hipEvent_t ready;                  // the last setup / update / set_iv of the entries
@@ -520,7 +573,7 @@ ptls_mi355x_keyset_t *ptls_mi355x_keyset_new(const void *keys, const void *ivs, 
     if (nkeys == 1) {
         // a picotls context: a slab entry, and the setup launch (the key in its arguments) deferred to the first use,
         // on that use's stream (setup_now)
-        if ((ks->d_keys = slot_get(ds)) == nullptr) {
+        if ((ks->d_keys = slot_get(ds, &ks->slab)) == nullptr) {
             keyset_destroy(ks);
             return NULL;
         }
@@ -613,11 +666,27 @@ void ptls_mi355x_keyset_free(ptls_mi355x_keyset_t *ks)
     ks->pending.store(false, std::memory_order_release);  // never used: its setup never ran (the raw key is cleared below)
     // key material is cleared (ptls_clear_memory, lib/fusion.c:1045) after the keyset's last launch, on the maintenance
     // stream; nothing here waits on the host
-    bool ordered = maint_after_uses(ks) == 0;
+    bool ordered = !ds->fault_order && maint_after_uses(ks) == 0;
     if (ks->group_ev != nullptr && hipStreamWaitEvent(ds->maint, ks->group_ev, 0) != hipSuccess)
         ordered = false;
-    if (!ordered)  // cannot order the teardown: keep the entries (never reused) rather than clear them under a launch
-        (void)hipStreamSynchronize(ds->maint);
+    if (!ordered) {
+        // the teardown cannot be ordered after the keyset's launches on the device: wait for each of them (the recorded
+        // uses on every stream, the setup, the key grouping) on the host before clearing; if even that fails, keep the
+        // entries as they are and never reuse them, rather than clear them under a launch still reading them
+        bool drained = true;
+        {
+            std::lock_guard<std::mutex> lk(ks->mu);
+            for (auto &u : ks->uses)
+                drained = hipEventSynchronize(u.second) == hipSuccess && drained;
+        }
+        drained = hipEventSynchronize(ks->ready) == hipSuccess && drained;
+        if (ks->group_ev != nullptr)
+            drained = hipEventSynchronize(ks->group_ev) == hipSuccess && drained;
+        if (!drained) {
+            keyset_destroy(ks);
+            return;
+        }
+    }
     (void)hipMemsetAsync(ks->d_keys, 0, ks->nkeys * sizeof(KeyEntry), ds->maint);
     if (ks->d_group != nullptr)
         (void)hipFreeAsync(ks->d_group, ds->maint);
@@ -626,7 +695,7 @@ void ptls_mi355x_keyset_free(ptls_mi355x_keyset_t *ks)
         hipEvent_t cleared = event_get(ds);
         if (cleared != nullptr && hipEventRecord(cleared, ds->maint) == hipSuccess) {
             std::lock_guard<std::mutex> lk(ds->mu);
-            ds->pending.push_back({ks->d_keys, cleared});
+            ds->pending.push_back({ks->d_keys, ks->slab, cleared});
         }
     } else {
         (void)hipFreeAsync(ks->d_keys, ds->maint);
@@ -669,8 +738,46 @@ int ptls_mi355x_keyset_set_constant_time(ptls_mi355x_keyset_t *ks, int on)
     return 0;
 }
 
+int ptls_mi355x_keyset_get_constant_time(const ptls_mi355x_keyset_t *ks) { return ks != NULL && ks->ct ? 1 : 0; }
+
 size_t ptls_mi355x_keyset_size(const ptls_mi355x_keyset_t *ks) { return ks->nkeys; }
 size_t ptls_mi355x_keyset_key_size(const ptls_mi355x_keyset_t *ks) { return ks->key_size; }
+int ptls_mi355x_keyset_device(const ptls_mi355x_keyset_t *ks) { return ks->device; }
+
+size_t ptls_mi355x_staging_bytes(void)
+{
+    size_t n = 0;
+    for (int d = 0; d < MAX_DEVICES; ++d) {
+        DeviceState *ds = g_devs[d].load(std::memory_order_acquire);
+        if (ds == nullptr)
+            continue;
+        std::lock_guard<std::mutex> lk(ds->mu);
+        n += ds->stage_idle + ds->stage_busy;
+    }
+    return n;
+}
+
+void ptls_mi355x_release_staging(void)
+{
+    for (int d = 0; d < MAX_DEVICES; ++d) {
+        DeviceState *ds = g_devs[d].load(std::memory_order_acquire);
+        if (ds == nullptr)
+            continue;
+        std::vector<Stager *> idle;
+        {
+            std::lock_guard<std::mutex> lk(ds->mu);
+            for (int c = 0; c < STAGE_CLASSES; ++c) {
+                for (Stager *s = ds->stagers[c]; s != nullptr; s = s->next)
+                    idle.push_back(s);
+                ds->stagers[c] = nullptr;
+            }
+            ds->stage_idle = 0;
+        }
+        DeviceScope scope(d);
+        for (Stager *s : idle)
+            stager_destroy(s);
+    }
+}
 
 int ptls_mi355x_keyset_get_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, void *iv)
 {
@@ -799,22 +906,32 @@ static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int sche
 // One long record (descriptor `one`, key entry `key`) over many workgroups (span_kernels.h): `units` 16-step units in
 // spans of 2^e, their partials at `part` (nspans x 16 B, device-addressable), then the combine launch, which writes the
 // tag or ok[0] and sets done_flag[0] when given.
-static int launch_span(const KeyEntry *key, int nr, bool open, const ptls_mi355x_record_t &one, const void *in, const void *aad,
-                       void *out, uint8_t *ok, u32 units, u32 e, u32 nspans, void *part, u32 *done_flag, hipStream_t s)
+template <int NR, bool OPEN>
+static void launch_span_kernel(bool ct, u32 nspans, hipStream_t s, const BatchArgs &a, u32 span, u32 units, void *part)
+{
+    if (ct)
+        gcm_span_kernel<NR, OPEN, true><<<nspans, ENGINE_WG, SPAN_LDS, s>>>(a, span, units, (u32x4 *)part);
+    else
+        gcm_span_kernel<NR, OPEN, false><<<nspans, ENGINE_WG, SPAN_LDS, s>>>(a, span, units, (u32x4 *)part);
+}
+
+static int launch_span(const KeyEntry *key, int nr, bool ct, bool open, const ptls_mi355x_record_t &one, const void *in,
+                       const void *aad, void *out, uint8_t *ok, u32 units, u32 e, u32 nspans, void *part, u32 *done_flag,
+                       hipStream_t s)
 {
     BatchArgs a = {key, nullptr, 1, (const uint8_t *)in, (const uint8_t *)aad, (uint8_t *)out, ok, 0u, 1u, CHUNK_LOG2,
                    nullptr, nullptr, nullptr, 1u, one, done_flag, 0, nullptr};
     const u32 span = 1u << e;
     if (nr == 10) {
         if (open)
-            gcm_span_kernel<10, true><<<nspans, ENGINE_WG, SPAN_LDS, s>>>(a, span, units, (u32x4 *)part);
+            launch_span_kernel<10, true>(ct, nspans, s, a, span, units, part);
         else
-            gcm_span_kernel<10, false><<<nspans, ENGINE_WG, SPAN_LDS, s>>>(a, span, units, (u32x4 *)part);
+            launch_span_kernel<10, false>(ct, nspans, s, a, span, units, part);
     } else {
         if (open)
-            gcm_span_kernel<14, true><<<nspans, ENGINE_WG, SPAN_LDS, s>>>(a, span, units, (u32x4 *)part);
+            launch_span_kernel<14, true>(ct, nspans, s, a, span, units, part);
         else
-            gcm_span_kernel<14, false><<<nspans, ENGINE_WG, SPAN_LDS, s>>>(a, span, units, (u32x4 *)part);
+            launch_span_kernel<14, false>(ct, nspans, s, a, span, units, part);
     }
     HIP_TRY(hipGetLastError());
     const size_t clds = GHASH_TABLE_BYTES + 16 * 257;
@@ -1105,8 +1222,12 @@ struct StageCall {
         const bool copy = st->h_dev == nullptr;
         if (copy)
             HIP_TRY(hipMemcpyAsync(st->d, st->h, up, hipMemcpyHostToDevice, st->stream));
-        if (launch() != 0)
+        if (launch() != 0) {
+            // a kernel of this call may already be queued (the span launch before its combine, the GCM launch before
+            // the header-protection one): the buffer is cleared and reused only once nothing of it is in flight
+            (void)hipStreamSynchronize(st->stream);
             return -1;
+        }
         if (copy)
             HIP_TRY(hipMemcpyAsync(st->h + up, st->d + up, total - up, hipMemcpyDeviceToHost, st->stream));
         const auto t0 = std::chrono::steady_clock::now();
@@ -1212,7 +1333,7 @@ static void run_calls(DeviceState *ds, OneCall *const *c, size_t n)
     const size_t nflags = hp ? (size_t)aux_grid(n, ds->ncu) : (n < (size_t)ds->ncu ? n : (size_t)ds->ncu);
     // a lone long record runs over many workgroups (launch_span): 16-step units in spans of 2^e, at most one span per CU
     u32 span_units = 0, span_e = 0, span_n = 0;
-    if (SPAN_MIN_BYTES != 0 && n == 1 && c0.len >= SPAN_MIN_BYTES && !c0.ks->ct && c0.ks->schedule != PTLS_MI355X_SCHEDULE_LOCKSTEP) {
+    if (SPAN_MIN_BYTES != 0 && n == 1 && c0.len >= SPAN_MIN_BYTES && c0.ks->schedule != PTLS_MI355X_SCHEDULE_LOCKSTEP) {
         const size_t steps = ((c0.aadlen + 15) / 16 + (c0.len + 15) / 16 + 1 + ENGINE_G - 1) / ENGINE_G;
         span_units = (u32)((steps + CHUNK_STEPS - 1) / CHUNK_STEPS);
         const u32 cap = ds->ncu < 256 ? (u32)ds->ncu : 256u;
@@ -1280,7 +1401,7 @@ static void run_calls(DeviceState *ds, OneCall *const *c, size_t n)
             if (ret == 0)
                 ret = call.roundtrip(up, [&] {
                     if (span_n != 0) {
-                        if (launch_span(kbase, nr, open, first, d, d, d, d + off_ok, span_units, span_e, span_n, d + off_span,
+                        if (launch_span(kbase, nr, c0.ks->ct, open, first, d, d, d, d + off_ok, span_units, span_e, span_n, d + off_span,
                                         flag && !hp ? (u32 *)(d + off_flag) : nullptr, s) != 0)
                             return -1;
                     } else if (launch_gcm(kbase, nkeys, nr, ds->ncu, c0.ks->schedule, c0.ks->ct, open, (const ptls_mi355x_record_t *)(d + off_rec),
@@ -1363,17 +1484,17 @@ static int submit(DeviceState *ds, OneCall *c)
                 ++cb.inflight;
                 cb.expect = take;
                 lk.unlock();
-                // a batch's calls address their entries as key indices from its lowest entry; slabs are separate
-                // allocations, so a batch whose entries span more than 2^30 entries (never seen) runs call by call
-                auto near = [&](bool hp_entries) {
-                    const KeyEntry *lo = nullptr, *hi = nullptr;
-                    for (OneCall *x : batch) {
-                        const KeyEntry *e = hp_entries ? x->hp_entry() : x->entry();
-                        lo = lo == nullptr || e < lo ? e : lo, hi = hi == nullptr || e > hi ? e : hi;
-                    }
-                    return (size_t)(hi - lo) < ((size_t)1 << 30);
+                // a batch's calls address their entries as key indices from its lowest entry, which is defined only
+                // within one slab (slabs are separate allocations): calls whose entries lie in several slabs run one
+                // by one
+                auto one_slab = [&](bool hp_entries) {
+                    const KeyEntry *slab = hp_entries ? batch[0]->hp_ks->slab : batch[0]->ks->slab;
+                    for (OneCall *x : batch)
+                        if ((hp_entries ? x->hp_ks->slab : x->ks->slab) != slab)
+                            return false;
+                    return true;
                 };
-                if (batch.size() == 1 || (near(false) && (batch[0]->hp_ks == nullptr || near(true)))) {
+                if (batch.size() == 1 || (one_slab(false) && (batch[0]->hp_ks == nullptr || one_slab(true)))) {
                     run_calls(ds, batch.data(), batch.size());
                 } else {
                     for (OneCall *x : batch)
@@ -1407,7 +1528,7 @@ static int single(ptls_mi355x_keyset_t *ks, size_t key_idx, bool open, void *out
         return fail("%s", "single: invalid arguments");
     if (len > PTLS_MI355X_MAX_RECORD_LEN || aadlen > PTLS_MI355X_MAX_AAD_LEN)
         return fail("%s", "single: record or AAD longer than PTLS_MI355X_MAX_RECORD_LEN / PTLS_MI355X_MAX_AAD_LEN");
-    if (hp_ks != NULL && (hp_key_idx >= hp_ks->nkeys || hp_ks->device != ks->device || sample_off + 16 > len + 16))
+    if (hp_ks != NULL && (hp_key_idx >= hp_ks->nkeys || hp_ks->device != ks->device || sample_off > len))
         return fail("%s", "single: invalid header-protection arguments");
     DeviceScope scope(ks->device);
     OneCall c;

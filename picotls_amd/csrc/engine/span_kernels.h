@@ -55,8 +55,10 @@ __device__ __forceinline__ void build_elem_table(lds_u8 *lds, u32 base, u32x4 h)
 }
 
 // Workgroup s: the units [s * span, min(units, (s + 1) * span)) of the record args.one (key 0 of args.keys), Q_s to
-// part[s]. 16-step units; the record's stream is front-padded to whole steps (gcm_segment, not aligned).
-template <int NR, bool OPEN>
+// part[s]. 16-step units; the record's stream is front-padded to whole steps (gcm_segment, not aligned). CT: the
+// constant-time variant (gcm_segment's uniform-table last multiply; the span's Horner with gmul_tab, every lane the same
+// table rows, instead of the group-cooperative gmul_group whose lanes read different window rows).
+template <int NR, bool OPEN, bool CT>
 __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGINE_WAVES_PER_SIMD, ENGINE_WAVES_PER_SIMD))) void gcm_span_kernel(BatchArgs args, u32 span, u32 units, u32x4 *part)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -94,8 +96,8 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             m_lo = k + 1 == units ? 0u : m_hi - CHUNK_STEPS;
         }
         u32x4 acc, ek0;
-        gcm_segment<NR, OPEN, 1>(args, lds, rk, iv0, iv1, iv2, r, valid, m_lo, m_hi, j, laneoff, tsel_horner, acc, ek0, false,
-                                 0, false);
+        gcm_segment<NR, OPEN, 1, 0, CT>(args, lds, rk, iv0, iv1, iv2, r, valid, m_lo, m_hi, j, laneoff, tsel_horner, acc, ek0,
+                                        false, 0, false);
         if (valid && j == G - 1)  // the length lane holds E(K, J0) in the record's last unit
             s_part[uu] = k == 0 ? acc ^ ek0 : acc;
     }
@@ -105,7 +107,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         if (lane < G) {
             u32x4 g = s_part[n - 1];
             for (u32 i = n - 1; i-- > 0;)
-                g = gmul_group(lds, g, tsel_chunk, j) ^ s_part[i];
+                g = (CT ? gmul_tab(lds, g, tsel_chunk) : gmul_group(lds, g, tsel_chunk, j)) ^ s_part[i];
             if (j == 0)
                 part[blockIdx.x] = g;
         }
@@ -113,7 +115,8 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
 }
 
 // One workgroup: GHASH = sum_s part[s] M^s with M = (H^128)^(2^e), the record's tag: written after the ciphertext
-// (seal) or compared with the received one (open, ok[0]).
+// (seal) or compared with the received one (open, ok[0]). Constant-time as it stands: every product is a gmul_tab in
+// which all threads read the same window row of the same table.
 template <bool OPEN>
 __global__ __launch_bounds__(256) void span_combine_kernel(BatchArgs args, u32 nspans, u32 e, const u32x4 *part)
 {

@@ -12,6 +12,12 @@
  * Unlike fusion, do_encrypt_v (TLS over TCP) is implemented: the iovecs are gathered straight into the staging buffer and
  * sealed as one record.
  *
+ * Constant time. fusion's AES and GHASH are AES-NI / PCLMUL (lib/fusion.c:157-186, :323-335): their timing does not depend on
+ * keys or data. The AEAD objects here therefore put their keysets in the engine's constant-time mode (every LDS access
+ * with a data-independent bank pattern, include/picotls/mi355x.h ptls_mi355x_keyset_set_constant_time) unless the
+ * environment sets PTLS_MI355X_CONSTANT_TIME=0. A per-record call is bound by its launch and PCIe round trip, so the
+ * mode costs it little; batch keysets keep the engine's own default.
+ *
  * Failure behaviour. picotls' encrypt callbacks cannot report errors (fusion asserts on OOM, lib/fusion.c:1143), so
  * every engine failure fails closed in every build: a failed seal overwrites the whole output (inlen + 16 bytes) with
  * zeros, which no peer authenticates and which holds no plaintext even when sealing in place; a cipher that cannot
@@ -99,6 +105,12 @@ static int aes256ctr_setup(ptls_cipher_context_t *ctx, int is_enc, const void *k
 
 /* ------------------------------------------------------------------ AES-GCM */
 
+static int aead_constant_time(void)
+{
+    const char *e = getenv("PTLS_MI355X_CONSTANT_TIME");
+    return !(e != NULL && strcmp(e, "0") == 0);
+}
+
 static void aesgcm_dispose_crypto(ptls_aead_context_t *_ctx)
 {
     struct mi355x_aead_context *ctx = (struct mi355x_aead_context *)_ctx;
@@ -139,7 +151,9 @@ static void aead_do_encrypt(ptls_aead_context_t *_ctx, void *output, const void 
                             const void *aad, size_t aadlen, ptls_aead_supplementary_encryption_t *supp)
 {
     struct mi355x_aead_context *ctx = (struct mi355x_aead_context *)_ctx;
-    if (supp != NULL && is_mi355x_ctr(supp->ctx) && (const uint8_t *)supp->input >= (const uint8_t *)output &&
+    if (supp != NULL && is_mi355x_ctr(supp->ctx) &&
+        ptls_mi355x_keyset_device(((struct mi355x_ctr_context *)supp->ctx)->ks) == ptls_mi355x_keyset_device(ctx->ks) &&
+        (const uint8_t *)supp->input >= (const uint8_t *)output &&
         (const uint8_t *)supp->input + 16 <= (const uint8_t *)output + inlen + PTLS_AESGCM_TAG_SIZE) {
         /* the header-protection mask of a sample inside the sealed output, computed in the seal's round trip (fusion
          * computes it inside the seal, lib/fusion.c:425-430,636-651) */
@@ -193,6 +207,11 @@ static int aesgcm_setup(ptls_aead_context_t *_ctx, int is_enc, const void *key, 
 
     if ((ctx->ks = ptls_mi355x_keyset_new(key, iv, 1, key_size)) == NULL)
         return PTLS_ERROR_LIBRARY;
+    if (ptls_mi355x_keyset_set_constant_time(ctx->ks, aead_constant_time()) != 0) {
+        ptls_mi355x_keyset_free(ctx->ks);
+        ctx->ks = NULL;
+        return PTLS_ERROR_LIBRARY;
+    }
     ctx->super.dispose_crypto = aesgcm_dispose_crypto;
     ctx->super.do_get_iv = aesgcm_get_iv;
     ctx->super.do_set_iv = aesgcm_set_iv;

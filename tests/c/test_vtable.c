@@ -417,6 +417,15 @@ int main(int argc, char **argv)
            ptls_mi355x_aes128gcm.integrity_limit == ptls_fusion_aes128gcm.integrity_limit,
        "aes128gcm algorithm fields match fusion");
     OK(strcmp(ptls_mi355x_aes256gcm.name, "AES256-GCM") == 0 && ptls_mi355x_aes256gcm.key_size == 32, "aes256gcm fields");
+    {
+        /* the AEAD objects replace a constant-time backend: constant-time unless PTLS_MI355X_CONSTANT_TIME=0 */
+        static const uint8_t k[16], iv[12];
+        ptls_aead_context_t *c = ptls_aead_new_direct(&ptls_mi355x_aes128gcm, 1, k, iv);
+        const char *e = getenv("PTLS_MI355X_CONSTANT_TIME");
+        OK(c != NULL && ptls_mi355x_keyset_get_constant_time(ptls_mi355x_aead_get_keyset(c)) == !(e != NULL && strcmp(e, "0") == 0),
+           "aead contexts constant-time by default");
+        ptls_aead_free(c);
+    }
     ecb_kat();
     pair_test(&ptls_fusion_aes128gcm, &ptls_mi355x_aes128gcm, "aes128gcm fusion<->mi355x", 60);
     pair_test(&ptls_fusion_aes256gcm, &ptls_mi355x_aes256gcm, "aes256gcm fusion<->mi355x", 60);

@@ -1,0 +1,53 @@
+"""bench.py's multi-GPU entry point as the driver can run it: `python bench.py --gpus 2` with
+no external launcher starts torch.distributed.run itself (a child process, before any GPU call), and its line carries
+the configs[4] strong-scaling leg (shard1200: one global batch split across the ranks) beside the weak-scaling
+headline. Both ranks run on cuda:0 over gloo (PTLS_BENCH_ONE_DEVICE=1), the one-GPU rehearsal of the nccl path.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, extra_env=None, timeout=240):
+    env = dict(os.environ, PTLS_BENCH_ONE_DEVICE="1", MASTER_ADDR="127.0.0.1")
+    env.pop("WORLD_SIZE", None)
+    env.update(extra_env or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.strip()]
+    assert lines, r.stderr[-3000:]
+    return json.loads(lines[-1])  # the result line is the last stdout line
+
+
+def test_bench_self_launches_two_ranks_with_shard1200_leg():
+    records = 2048
+    out = _run(["--gpus", "2", "--steps", "2", "--warmup", "1", "--records", str(records), "--extra", "shard1200",
+                "--no-cpu-baseline"])
+    assert out["n_gpus"] == 2
+    assert out["scaling"] == "weak"
+    assert out["verified"]["roundtrip"] is True
+    assert out["value"] > 0 and out["config"]["records_per_gpu"] == records
+    sh = out["extra"]["shard1200"]
+    assert sh["n_gpus"] == 2 and sh["scaling"] == "strong"
+    assert sh["verified"]["roundtrip"] is True
+    want_total = records * 16384 // 1200  # --records scales the extra legs by bytes (bench.py)
+    assert sh["records_total"] == want_total
+    assert sh["records_per_gpu"] in (want_total // 2, want_total - want_total // 2)
+    assert sh["value"] > 0
+    assert out["cpu_baseline"] is None  # rank 0 at N = 1 only
+
+
+def test_bench_single_gpu_line_has_shard1200_by_default():
+    """The default --extra list includes configs[4] (N = 1 anchor of the scaling curve)."""
+    out = _run(["--steps", "1", "--warmup", "1", "--records", "1024", "--no-cpu-baseline", "--extra", "shard1200"])
+    assert out["n_gpus"] == 1
+    sh = out["extra"]["shard1200"]
+    assert sh["scaling"] == "strong" and sh["n_gpus"] == 1 and sh["verified"]["roundtrip"] is True
