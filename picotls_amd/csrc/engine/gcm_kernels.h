@@ -37,9 +37,12 @@ __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u
         valid = false;
     }
     const u32 K = valid ? gcm_steps<OPEN, 0>(r) : 0;
-    u32x4 acc, ek0;
-    gcm_segment<NR, OPEN, NB>(args, lds, rk, iv0, iv1, iv2, r, valid, 0, K, j, laneoff, tsel_horner, acc, ek0, true, rec,
+    u32x4 acc;
+    u32 okw;
+    gcm_segment<NR, OPEN, NB>(args, lds, rk, iv0, iv1, iv2, r, valid, 0, K, j, laneoff, tsel_horner, acc, true, okw,
                               true);
+    if (OPEN && okw <= 1)
+        args.ok[rec] = (uint8_t)okw;
 }
 
 // Persistent kernel: workgroup w owns the contiguous record range [n*w/grid, n*(w+1)/grid) and walks it in key runs
@@ -484,75 +487,95 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                   iv2 = __builtin_amdgcn_readfirstlane(key->iv[2]);
 
         // ---- units: each wave takes RPW consecutive units (one per group) at a time
+        // unit_of: the group's unit u -> its record (lo, in run order), the record's first unit, its unit count and
+        // how many of its units follow this one (k_back), from the run state in LDS. It runs again after the segment
+        // instead of keeping these values (and the descriptor, the ok index) live across it: kept, they were spilled to
+        // scratch once per unit (the open kernels: 13 spill stores, which reached HBM as extra writes).
+        auto unit_of = [&](u32 u, u32 &lo, u32 &first, u32 &unc, u32 &k_back) {
+            lo = u, first = u, unc = 1, k_back = 0;
+            if (whole)
+                return;
+            if (u < nhuge || u >= nhuge + nfull) {  // a front unit
+                lo = s_front[u < nhuge ? u : u - nfull];
+                first = s_ubase[lo];
+                unc = s_ubase[lo + 1] - first;
+                k_back = unc - 1;
+            } else {  // full unit f: record lo with s_ubase[lo] - lo <= f < s_ubase[lo + 1] - (lo + 1)
+                const u32 f = u - nhuge;
+                u32 hi = run_n;
+                lo = 0;
+                while (hi - lo > 1) {
+                    const u32 mid = (lo + hi) >> 1;
+                    if (s_ubase[mid] - mid <= f)
+                        lo = mid;
+                    else
+                        hi = mid;
+                }
+                first = s_ubase[lo];
+                unc = s_ubase[lo + 1] - first;
+                k_back = f - (first - lo);
+            }
+        };
         for (;;) {
-            const u32 lane = lane_here(), j = lane % G, slot = lane / G, laneoff = (lane & 31) * 4;
             u32 ub = 0;
-            if (lane == 0)
+            if (lane_here() == 0)
                 ub = atomicAdd((u32 *)&rs[RC_NEXT], (u32)RPW);
             ub = __builtin_amdgcn_readfirstlane(ub);
             if (ub >= total_units)
                 break;
-            const u32 u = ub + slot;
-            const bool valid = u < total_units;
-            u32 lo = u, first = u, unc = 1, k_back = 0;
-            if (!whole && valid) {
-                if (u < nhuge || u >= nhuge + nfull) {  // a front unit
-                    lo = s_front[u < nhuge ? u : u - nfull];
-                    first = s_ubase[lo];
-                    unc = s_ubase[lo + 1] - first;
-                    k_back = unc - 1;
-                } else {  // full unit f: record lo with s_ubase[lo] - lo <= f < s_ubase[lo + 1] - (lo + 1)
-                    const u32 f = u - nhuge;
-                    u32 hi = run_n;
-                    lo = 0;
-                    while (hi - lo > 1) {
-                        const u32 mid = (lo + hi) >> 1;
-                        if (s_ubase[mid] - mid <= f)
-                            lo = mid;
-                        else
-                            hi = mid;
-                    }
-                    first = s_ubase[lo];
-                    unc = s_ubase[lo + 1] - first;
-                    k_back = f - (first - lo);
+            u32x4 acc;
+            u32 okw;
+            {
+                const u32 lane = lane_here(), j = lane % G, slot = lane / G, laneoff = (lane & 31) * 4;
+                const u32 u = ub + slot;
+                const bool valid = u < total_units;
+                u32 lo, first, unc, k_back;
+                unit_of(valid ? u : 0u, lo, first, unc, k_back);
+                ptls_mi355x_record_t r = {};
+                if (valid)
+                    r = recs[pos + lo];
+                const bool live = valid && record_ok<FRAME>(args, r);
+                if (valid && !live) {  // rejected descriptor: the scan gave it one unit; nothing is written
+                    r.len = 0, r.aad_len = 0, r.flags = 0;
+                    if (OPEN && j == 0)
+                        args.ok[ok_at(pos + lo)] = 0;
                 }
+                const u32 steps = gcm_steps<OPEN, FRAME>(r);
+                // unit [m_lo, m_hi) of the record's steps (whole mode: the record); huge records take longer units
+                const u32 mul = whole ? 1u : unit_mul(steps, ulog2);
+                u32 m_hi = steps, m_lo = 0;
+                if (!whole) {
+                    const u32 ulen = mul * ustep;
+                    m_hi = steps - k_back * ulen;
+                    m_lo = k_back + 1 == unc ? 0u : m_hi - ulen;
+                }
+                if (!live)
+                    m_lo = m_hi = 0;
+                gcm_segment<NR, OPEN, 1, FRAME, CT>(args, lds, rk, iv0, iv1, iv2, r, live, m_lo, m_hi, j, laneoff, tsel_horner, acc,
+                                                    unc == 1, okw, whole);
             }
-            const u32 ri = lo;
-            ptls_mi355x_record_t r = {};
-            if (valid)
-                r = recs[pos + ri];
-            const u64 rid = OPEN && valid ? ok_at(pos + ri) : pos + ri;  // the record's batch index (ok byte)
-            const bool live = valid && record_ok<FRAME>(args, r);
-            if (valid && !live) {  // rejected descriptor: the scan gave it one unit; nothing is written
-                r.len = 0, r.aad_len = 0, r.flags = 0;
-                if (OPEN && j == 0)
-                    args.ok[rid] = 0;
-            }
-            const u32 steps = gcm_steps<OPEN, FRAME>(r);
-            // unit [m_lo, m_hi) of the record's steps (whole mode: the record); huge records take longer units
-            const u32 mul = whole ? 1u : unit_mul(steps, ulog2);
-            u32 m_hi = steps, m_lo = 0;
-            if (!whole) {
-                const u32 ulen = mul * ustep;
-                m_hi = steps - k_back * ulen;
-                m_lo = k_back + 1 == unc ? 0u : m_hi - ulen;
-            }
-            if (!live)
-                m_lo = m_hi = 0;
-            u32x4 acc, ek0;
-            gcm_segment<NR, OPEN, 1, FRAME, CT>(args, lds, rk, iv0, iv1, iv2, r, live, m_lo, m_hi, j, laneoff, tsel_horner, acc, ek0,
-                                            unc == 1, rid, whole);
-            if (live && unc > 1) {  // uniform over the group
+            // from here on everything is read again (run state, descriptor), not carried across the segment
+            asm volatile("" ::: "memory");
+            const u32 lane = lane_here(), j = lane % G, u = ub + lane / G;
+            if (u >= total_units)
+                continue;  // (uniform over the group)
+            u32 lo, first, unc, k_back;
+            unit_of(u, lo, first, unc, k_back);
+            if (OPEN && okw <= 1)  // a whole record's tag check (its length lane)
+                args.ok[ok_at(pos + lo)] = (uint8_t)okw;
+            if (unc > 1) {  // uniform over the group; a rejected descriptor is always one unit
                 u32 last = 0;
                 if (j == G - 1) {
                     // stream order, the front unit first; the last unit (k_back 0, multiplier H^0 in the combine)
-                    // carries E(K, J0), so the combine ends on the tag
-                    s_part[first + unc - 1 - k_back] = k_back == 0 ? acc ^ ek0 : acc;
+                    // carries E(K, J0) (gcm_segment), so the combine ends on the tag
+                    s_part[first + unc - 1 - k_back] = acc;
                     __threadfence_block();  // the partial lands before the count that publishes it
-                    last = atomicAdd((u32 *)&s_done[ri], 1u) == unc - 1;
+                    last = atomicAdd((u32 *)&s_done[lo], 1u) == unc - 1;
                 }
                 last = dpp_bcast7(last, lane);
                 if (last) {
+                    const ptls_mi355x_record_t r = recs[pos + lo];
+                    const u32 mul = unit_mul(gcm_steps<OPEN, FRAME>(r), ulog2);
                     // last unit of the record: GHASH = Horner over the partials with H^(G * ulen) = (H^(G * ustep))^mul
                     // (whole group)
                     // (CT: each lane forms the whole product from the same table rows, instead of a share of it from
@@ -570,7 +593,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                         const u32x4 rt = *(const u32x4_u *)(args.in + r.in_off + frame_in_skip<OPEN, FRAME>() +
                                                             gcm_text_len<OPEN, FRAME>(r));
                         const u32x4 d = rt ^ tag;
-                        args.ok[rid] = (d[0] | d[1] | d[2] | d[3]) == 0;
+                        args.ok[ok_at(pos + lo)] = (d[0] | d[1] | d[2] | d[3]) == 0;
                     } else {
                         *(u32x4_u *)(args.out + r.out_off + frame_out_skip<OPEN, FRAME>() + gcm_text_len<OPEN, FRAME>(r)) = tag;
                     }

@@ -7,8 +7,12 @@
 // positions j + G*m and runs them NB at a time. The NB AES-CTR blocks of a step are independent (NB x 16 LDS lookups
 // per round in flight); their GHASH folds stay sequential (Horner with H^G; each lane's last position in the segment
 // with H^(end - position), from its own table). On return every lane of the group holds the segment's GHASH partial
-// sum(X_i * H^(end - i)) and the length lane (lane (N - 1) mod G, when the segment holds the length block) holds
-// E(K, J0) in ek0. Invalid groups pass m_lo == m_hi.
+// sum(X_i * H^(end - i)), plus E(K, J0) when the segment holds the record's length block: the length lane (lane
+// (N - 1) mod G) encrypts J0 in that step and XORs it into its accumulator after its last multiply (the length block is
+// the last stream position, H^0 in every later combine), so a finished record's GHASH sum is its tag, and E(K, J0)
+// need not stay live through the loop (it was spilled to scratch once per segment). Invalid groups pass m_lo == m_hi. With finish (a whole record), a seal writes the tag and an open
+// returns the tag check in okw on the length lane (1 = verified, 0 = not; 2 on every other lane and without finish):
+// the caller stores the ok byte, so the record's batch index need not stay live through the segment.
 //
 // Stream layout. Units of the chunked schedule end on step boundaries, so their stream [zero padding | AAD | text |
 // length] is front-padded to a multiple of G positions (N = G * K). A whole record (ALIGNED: the lockstep kernel and the
@@ -25,8 +29,8 @@
 template <int NR, bool OPEN, int NB, int FRAME = 0, bool CT = false>
 __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 *lds, const u32 (&rk)[NR + 1][4], u32 iv0,
                                             u32 iv1, u32 iv2, const ptls_mi355x_record_t &r, bool valid, u32 m_lo,
-                                            u32 m_hi, u32 j, u32 laneoff, u32 tsel_horner, u32x4 &acc, u32x4 &ek0, bool finish,
-                                            u64 rec, bool aligned)
+                                            u32 m_hi, u32 j, u32 laneoff, u32 tsel_horner, u32x4 &acc, bool finish,
+                                            u32 &okw, bool aligned)
 {
     constexpr int G = ENGINE_G;
     constexpr bool SEAL_FRAME = FRAME == 1 && !OPEN, OPEN_FRAME = FRAME == 1 && OPEN, TLS12 = FRAME == 2;
@@ -81,7 +85,6 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     const uint8_t *aadp = OPEN_FRAME ? args.in + r.in_off : args.aad + r.aad_off;
 
     acc = u32x4{0, 0, 0, 0};
-    ek0 = u32x4{0, 0, 0, 0};
 
     static_assert(NB == 1, "the counter cache runs one block per lane and step");
     CtrCache1 cc1 = {};
@@ -124,7 +127,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     };
     // step m, part 2: with the keystream block ks, write the output and return the GHASH input block X of position
     // j + G*m
-    auto finish_step = [&](u32 m, const u32x4 &ks) -> u32x4 {
+    auto finish_step = [&](u32 m, const u32x4 &ks, u32x4 &ek0) -> u32x4 {
         const bool act = m < m_hi;
         const int logical = (int)(j + G * m) - P;
         const int b = logical - (int)na;
@@ -239,7 +242,8 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         setup_step(m0, st);
         aes_ctr_cached1<NR>(lds, laneoff, rk, cc1, st);
         __builtin_amdgcn_sched_barrier(0);
-        const u32x4 X = finish_step(m0, u32x4{st[0][0], st[0][1], st[0][2], st[0][3]});
+        u32x4 ek0 = {0, 0, 0, 0};
+        const u32x4 X = finish_step(m0, u32x4{st[0][0], st[0][1], st[0][2], st[0][3]}, ek0);
         // scheduling fence: keeps the 32 table loads of this fold from being hoisted next to the other work (that
         // hoisting spills them to scratch)
         __builtin_amdgcn_sched_barrier(0);
@@ -265,7 +269,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             prod = gmul_tab(lds, acc ^ X, !CT && last_here ? tsel_last : tsel_horner);
         }
         if ((int)m0 <= m_last)
-            acc = prod;
+            acc = prod ^ ek0;
         __builtin_amdgcn_sched_barrier(0);
     }
 
@@ -276,12 +280,13 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         acc[c] = dpp_xor8(acc[c]);
     // whole record (finish): tag = GHASH ^ E(K, J0), written after the ciphertext (seal) or compared with the
     // received one (open)
+    okw = 2;
     if (finish && valid && j == jl) {
-        const u32x4 tag = acc ^ ek0;
+        const u32x4 tag = acc;
         if (OPEN) {
             const u32x4 rt = *(const u32x4_u *)(src + L);
             const u32x4 d = rt ^ tag;
-            args.ok[rec] = (d[0] | d[1] | d[2] | d[3]) == 0;
+            okw = (d[0] | d[1] | d[2] | d[3]) == 0;
         } else {
             *(u32x4_u *)(dst + L) = tag;
         }

@@ -95,11 +95,12 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             m_hi = steps - k * CHUNK_STEPS;
             m_lo = k + 1 == units ? 0u : m_hi - CHUNK_STEPS;
         }
-        u32x4 acc, ek0;
-        gcm_segment<NR, OPEN, 1, 0, CT>(args, lds, rk, iv0, iv1, iv2, r, valid, m_lo, m_hi, j, laneoff, tsel_horner, acc, ek0,
-                                        false, 0, false);
-        if (valid && j == G - 1)  // the length lane holds E(K, J0) in the record's last unit
-            s_part[uu] = k == 0 ? acc ^ ek0 : acc;
+        u32x4 acc;
+        u32 okw;
+        gcm_segment<NR, OPEN, 1, 0, CT>(args, lds, rk, iv0, iv1, iv2, r, valid, m_lo, m_hi, j, laneoff, tsel_horner, acc,
+                                        false, okw, false);
+        if (valid && j == G - 1)  // (the record's last unit includes E(K, J0), gcm_segment)
+            s_part[uu] = acc;
     }
     __syncthreads();
     if (wave == 0) {  // Q_s by Horner from the span's highest unit down (group 0; every lane of it holds the result)
