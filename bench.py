@@ -548,15 +548,16 @@ def lds_model(res, key_size: int):
             "per_block": f"{lookups} ds_read_b32 (AES) + 32 ds_read_b128 (GHASH)"}
 
 
-def traffic_from_profiles(workload: str, records: int):
-    """Corrected HBM bytes per seal launch from the committed rocprofv3 PMC summary (profiles/pmc_<workload>.json),
-    scaled to this run's record count when the profile was taken on a different one."""
+def traffic_from_profiles(workload: str, records: int, key: str = "seal_hbm_bytes_per_launch"):
+    """Corrected HBM bytes per seal (or open: key "open_hbm_bytes_per_launch") launch from the committed rocprofv3 PMC
+    summary (profiles/pmc_<workload>.json), scaled to this run's record count when the profile was taken on a different
+    one."""
     path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     if not os.path.exists(path):
         return None
     try:
         d = json.load(open(path))
-        v = d.get("seal_hbm_bytes_per_launch")
+        v = d.get(key)
         if v is None:
             return None
         n = d.get("records")
@@ -608,7 +609,9 @@ def main():
                      "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic_from_profiles(wl.name, res["records"]),
                      "alg_bytes_per_launch": res["seal_alg_bytes"], "avg_launch_ms": round(res["seal_ms"], 4),
-                     "open_achieved": round(res["open_alg_bytes"] / open_s / 1e9, 2)},
+                     "open_achieved": round(res["open_alg_bytes"] / open_s / 1e9, 2),
+                     "open_alg_bytes_per_launch": res["open_alg_bytes"],
+                     "open_traffic": traffic_from_profiles(wl.name, res["records"], "open_hbm_bytes_per_launch")},
         "lds_model": lds_model(res, wl.key_size),
         "verified": {"roundtrip": res.get("verified_roundtrip"), "fusion_spot_check": None},
     }

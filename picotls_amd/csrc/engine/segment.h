@@ -187,7 +187,10 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                 X = rem >= 16 ? *(const u32x4_u *)ap : load_partial(ap, rem);
             }
         } else if (is_len) {
-            const u64 abits = (u64)A * 8, cbits = (u64)L * 8;
+            // (formed here, not hoisted: the loop-invariant length block was kept live through the loop and spilled)
+            u32 Ah = A, Lh = L;
+            asm volatile("" : "+v"(Ah), "+v"(Lh));
+            const u64 abits = (u64)Ah * 8, cbits = (u64)Lh * 8;
             X[0] = bswap32((u32)(abits >> 32));
             X[1] = bswap32((u32)abits);
             X[2] = bswap32((u32)(cbits >> 32));

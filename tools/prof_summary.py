@@ -48,6 +48,11 @@ def main(src, dst_prefix, records=None):
     seal = next((v for n, v in out["kernels"].items() if re.search(r"<\d+, false[,>]", n)), None)
     if seal and "hbm_bytes_per_launch" in seal:
         out["seal_hbm_bytes_per_launch"] = seal["hbm_bytes_per_launch"]
+        out["seal_hbm_read_bytes"], out["seal_hbm_write_bytes"] = seal["hbm_read_bytes_corrected"], seal["hbm_write_bytes"]
+    opn = next((v for n, v in out["kernels"].items() if re.search(r"<\d+, true[,>]", n)), None)
+    if opn and "hbm_bytes_per_launch" in opn:
+        out["open_hbm_bytes_per_launch"] = opn["hbm_bytes_per_launch"]
+        out["open_hbm_read_bytes"], out["open_hbm_write_bytes"] = opn["hbm_read_bytes_corrected"], opn["hbm_write_bytes"]
     json.dump(out, open(dst_prefix + ".json", "w"), indent=1)
     with open(dst_prefix + ".md", "w") as f:
         f.write(f"# rocprofv3 summary: {os.path.basename(dst_prefix)}\n\nsource: `{src}`\n\n")
