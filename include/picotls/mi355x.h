@@ -237,8 +237,9 @@ typedef struct st_ptls_mi355x_hp_t {
 int ptls_mi355x_hp_mask_batch(ptls_mi355x_keyset_t *hp_ks, const ptls_mi355x_hp_t *hp, size_t n, const void *base,
                               void *masks, void *stream);
 
-/* seal_batch, then the masks of samples taken from the sealed output (hp[i] for record i; base = out), on one stream:
- * the sample may cover the tag, as in fusion's supp handling */
+/* seal_batch plus the masks of samples taken from the sealed output (hp[i] for record i; base = out): the sample may
+ * cover the tag, as in fusion's supp handling. One launch: the seal kernel computes each run's masks once the run's
+ * records are sealed (with the LOCKSTEP schedule: the seal, then a second launch). hp_ks must be on ks's device. */
 int ptls_mi355x_seal_batch_hp(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
                               const void *aad, void *out, ptls_mi355x_keyset_t *hp_ks, const ptls_mi355x_hp_t *hp,
                               void *masks, void *stream);

@@ -844,16 +844,31 @@ static u64 deal_chunk(u64 nrecs, u64 grid)
     return 0;
 }
 
+// Header-protection masks computed by the chunked seal launch itself (BatchArgs::hp; seal_batch_hp, encrypt_s)
+struct HpLaunch {
+    const ptls_mi355x_hp_t *hp;
+    const KeyEntry *keys;
+    u32 nkeys;
+    int nr;
+    uint8_t *masks;
+};
+
 // The GCM kernel launch of a batch over `nkeys` entries at `keys` (no key grouping, no keyset bookkeeping). ct: the
-// constant-time GHASH variant of the chunked kernel (the lockstep schedule is not offered in that mode).
+// constant-time GHASH variant of the chunked kernel (the lockstep schedule is not offered in that mode). hpl: the
+// header-protection masks of the sealed records in the same launch (chunked seal of unframed records only).
 static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int schedule, bool ct, bool open,
                       const ptls_mi355x_record_t *recs, size_t nrecs, const void *in, const void *aad, void *out, uint8_t *ok,
                       hipStream_t s, int frame, u32 unit_log2, const ptls_mi355x_record_t *grouped = nullptr,
                       const u32 *perm = nullptr, const u32 *perm_on = nullptr, const ptls_mi355x_record_t *one = nullptr,
-                      u32 *done_flag = nullptr, const u64 *bounds = nullptr)
+                      u32 *done_flag = nullptr, const u64 *bounds = nullptr, const HpLaunch *hpl = nullptr)
 {
     BatchArgs a = {keys, recs, (u64)nrecs, (const uint8_t *)in, (const uint8_t *)aad, (uint8_t *)out, ok,
                    nkeys > 1 ? 1u : 0u, nkeys, unit_log2, grouped, perm, perm_on, 0u, {}, done_flag, 0, bounds};
+    if (hpl != nullptr) {
+        if (open || frame != 0 || !(ct || use_chunked(schedule)))
+            return fail("%s", "launch_gcm: header-protection masks need the chunked seal of unframed records");
+        a.hp = hpl->hp, a.hp_keys = hpl->keys, a.hp_nkeys = hpl->nkeys, a.hp_nr = (u32)hpl->nr, a.masks = hpl->masks;
+    }
     if (one != nullptr && nrecs == 1)  // the chunked kernel takes a lone record's descriptor from its arguments
         a.one_inline = 1, a.one = *one;
     if (a.aad == NULL)
@@ -946,7 +961,7 @@ static int launch_span(const KeyEntry *key, int nr, bool ct, bool open, const pt
 // A batch call on a keyset: waits for the keyset's setup, groups an ungrouped many-key batch by key on the device, launches,
 // and records the use (teardown and rekey are ordered after it).
 static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
-                        const void *aad, void *out, uint8_t *ok, void *stream, int frame = 0)
+                        const void *aad, void *out, uint8_t *ok, void *stream, int frame = 0, const HpLaunch *hpl = nullptr)
 {
     if (ks == NULL || (nrecs != 0 && (recs == NULL || in == NULL || out == NULL || (open && ok == NULL))))
         return fail("%s", "batch: invalid arguments");
@@ -1000,12 +1015,12 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
             balance_bounds_kernel<<<1, 1024, 0, s>>>(tiles, nrecs, grid, bounds);
         }
         ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, ks->ct, open, recs, nrecs, in, aad, out, ok, s,
-                         frame, CHUNK_LOG2, grouped, perm, ctl + 1, nullptr, nullptr, bounds);
+                         frame, CHUNK_LOG2, grouped, perm, ctl + 1, nullptr, nullptr, bounds, hpl);
         if (ret == 0)
             HIP_TRY(hipEventRecord(ks->group_ev, s));
     } else {
         ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, ks->ct, open, recs, nrecs, in, aad, out, ok,
-                         s, frame, CHUNK_LOG2);
+                         s, frame, CHUNK_LOG2, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, hpl);
     }
     if (ret != 0)
         return -1;
@@ -1128,11 +1143,25 @@ int ptls_mi355x_seal_batch_hp(ptls_mi355x_keyset_t *ks, const ptls_mi355x_record
                               const void *aad, void *out, ptls_mi355x_keyset_t *hp_ks, const ptls_mi355x_hp_t *hp,
                               void *masks, void *stream)
 {
-    if (hp_ks == NULL || (nrecs != 0 && (hp == NULL || masks == NULL)))
+    if (ks == NULL || hp_ks == NULL || (nrecs != 0 && (hp == NULL || masks == NULL)))
         return fail("%s", "seal_batch_hp: invalid arguments");
-    if (launch_batch(ks, false, recs, nrecs, in, aad, out, NULL, stream) != 0)
+    if (hp_ks->device != ks->device)
+        return fail("%s", "seal_batch_hp: the keysets are on different devices");
+    if (nrecs == 0)
+        return 0;
+    if (!ks->ct && !use_chunked(ks->schedule)) {  // the lockstep schedule: the seal, then the masks (a second launch)
+        if (launch_batch(ks, false, recs, nrecs, in, aad, out, NULL, stream) != 0)
+            return -1;
+        return ptls_mi355x_hp_mask_batch(hp_ks, hp, nrecs, out, masks, stream);
+    }
+    // one launch: the chunked seal computes each run's masks after sealing it (hp_masks_pass)
+    DeviceScope scope(ks->device);
+    if (wait_ready(hp_ks, (hipStream_t)stream) != 0)
         return -1;
-    return ptls_mi355x_hp_mask_batch(hp_ks, hp, nrecs, out, masks, stream);
+    const HpLaunch hpl = {hp, hp_ks->d_keys, (u32)hp_ks->nkeys, hp_ks->nr, (uint8_t *)masks};
+    if (launch_batch(ks, false, recs, nrecs, in, aad, out, NULL, stream, 0, &hpl) != 0)
+        return -1;
+    return note_use(hp_ks, (hipStream_t)stream);
 }
 
 int ptls_mi355x_quiclb_batch(ptls_mi355x_keyset_t *ks, const ptls_mi355x_cid_t *cids, size_t n, const void *in, void *out,
@@ -1164,6 +1193,9 @@ int ptls_mi355x_quiclb_batch(ptls_mi355x_keyset_t *ks, const ptls_mi355x_cid_t *
 #define SPAN_MIN_BYTES ((size_t)262144)  // a lone record from this length runs over many workgroups (launch_span)
 #endif
 #define PERREC_FLAG_MAX_BYTES ((size_t)1 << 20)  // staged bytes of a call that polls (larger ones wait for the stream)
+#ifndef PERREC_HP_FUSED
+#define PERREC_HP_FUSED 1  // encrypt_s: the header-protection mask computed by the seal launch (BatchArgs::hp)
+#endif
 
 // PTLS_MI355X_COMBINE_STATS=1: per-record launches, calls and the host time of run_calls, printed at exit (tools/gpu_mt.sh)
 static struct CombineStats {
@@ -1328,9 +1360,6 @@ static void run_calls(DeviceState *ds, OneCall *const *c, size_t n)
     size_t off_ok = up;
     for (size_t i = 0; i < n; ++i)
         off_ok += a16(c[i]->len + (open ? 0 : 16));
-    // completion words: one per workgroup of the last kernel (the GCM launch: one workgroup per record up to the CU
-    // count; the header-protection launch: aux_grid)
-    const size_t nflags = hp ? (size_t)aux_grid(n, ds->ncu) : (n < (size_t)ds->ncu ? n : (size_t)ds->ncu);
     // a lone long record runs over many workgroups (launch_span): 16-step units in spans of 2^e, at most one span per CU
     u32 span_units = 0, span_e = 0, span_n = 0;
     if (SPAN_MIN_BYTES != 0 && n == 1 && c0.len >= SPAN_MIN_BYTES && c0.ks->schedule != PTLS_MI355X_SCHEDULE_LOCKSTEP) {
@@ -1343,6 +1372,12 @@ static void run_calls(DeviceState *ds, OneCall *const *c, size_t n)
         if ((1u << span_e) > SPAN_MAX_UNITS)
             span_units = span_e = span_n = 0;
     }
+    // header-protection masks: computed by the chunked seal launch itself (PERREC_HP_FUSED), else by a second launch
+    // (hp_kernel) after the seal, or after the span kernels
+    const bool hp_fused = hp && PERREC_HP_FUSED && span_n == 0 && (c0.ks->ct || use_chunked(c0.ks->schedule));
+    // completion words: one per workgroup of the last kernel (the GCM launch: one workgroup per record up to the CU
+    // count; the header-protection launch: aux_grid)
+    const size_t nflags = hp && !hp_fused ? (size_t)aux_grid(n, ds->ncu) : (n < (size_t)ds->ncu ? n : (size_t)ds->ncu);
     const size_t off_mask = off_ok + a16(n), off_flag = off_mask + 16 * n, off_span = off_flag + a16(4 * nflags),
                  total = off_span + 16 * (size_t)span_n;
     int ret = -1;
@@ -1404,11 +1439,14 @@ static void run_calls(DeviceState *ds, OneCall *const *c, size_t n)
                         if (launch_span(kbase, nr, c0.ks->ct, open, first, d, d, d, d + off_ok, span_units, span_e, span_n, d + off_span,
                                         flag && !hp ? (u32 *)(d + off_flag) : nullptr, s) != 0)
                             return -1;
-                    } else if (launch_gcm(kbase, nkeys, nr, ds->ncu, c0.ks->schedule, c0.ks->ct, open, (const ptls_mi355x_record_t *)(d + off_rec),
-                                   n, d, d, d, d + off_ok, s, 0, unit_log2, nullptr, nullptr, nullptr, n == 1 ? &first : nullptr,
-                                   flag && !hp ? (u32 *)(d + off_flag) : nullptr) != 0)
-                        return -1;
-                    return !hp ? 0
+                    } else {
+                        const HpLaunch hpl = {(const ptls_mi355x_hp_t *)(d + off_hp), hbase, hp_nkeys, hp_nr, d + off_mask};
+                        if (launch_gcm(kbase, nkeys, nr, ds->ncu, c0.ks->schedule, c0.ks->ct, open, (const ptls_mi355x_record_t *)(d + off_rec),
+                                       n, d, d, d, d + off_ok, s, 0, unit_log2, nullptr, nullptr, nullptr, n == 1 ? &first : nullptr,
+                                       flag && (!hp || hp_fused) ? (u32 *)(d + off_flag) : nullptr, nullptr, hp_fused ? &hpl : nullptr) != 0)
+                            return -1;
+                    }
+                    return !hp || hp_fused ? 0
                                : launch_hp(hbase, hp_nkeys, hp_nr, ds->ncu, (const ptls_mi355x_hp_t *)(d + off_hp), n, d, d + off_mask, s,
                                            flag ? (u32 *)(d + off_flag) : nullptr);
                 }, flag ? off_flag : 0, nflags);

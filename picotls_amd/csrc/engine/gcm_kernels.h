@@ -168,6 +168,7 @@ __device__ __forceinline__ unsigned long long stamp()
 #define RC_HUGE 5    // records whose front unit goes first (longer than CHUNK_MAX_UNITS units)
 #define RC_CLAIM 6   // the first wave to find this run's queue empty scans the next run
 #define RC_LOG2 7    // the run's unit length: 2^RC_LOG2 steps (run_unit_log2)
+#define RC_HPNEXT 8  // seal_batch_hp: next header-protection mask of the previous run to hand out (hp_masks_pass)
 
 // Scans the run that starts at record p into one run-state buffer, with ONE wave and no workgroup barrier, so that it
 // runs while the other waves are still busy with the previous run (the end-of-run tail where they would otherwise
@@ -344,6 +345,7 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
         rs[RC_HUGE] = nhuge;
         rs[RC_CLAIM] = 0;
         rs[RC_LOG2] = log2;
+        rs[RC_HPNEXT] = 0;
     }
 }
 
@@ -357,6 +359,89 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
 // GHASH = sum_k P_k * H^(k * CHUNK_BLOCKS). The group that completes a record's last outstanding unit (LDS counter per
 // record) evaluates that sum by Horner with the H^CHUNK_BLOCKS table and finishes the tag, inside the unit loop.
 // Single-unit records finish inside their unit as in the lockstep kernel.
+// QUIC header-protection masks (fusion's supp, lib/fusion.c:425-430,636-651) of sealed records [p, e) of a run, the
+// thread tid of nthr taking records p + tid, p + tid + nthr, ...: AES-ECB of the 16-byte sample under the record's
+// header-protection key, from the LDS T-tables. The records are complete (tags included: the sample may cover the tag),
+// so this runs after the run's end-of-run barrier: a run's masks are work items of the NEXT run's unit loop, taken by
+// waves whose units are done (they fill the tail where waves wait for the run's last units), and the workgroup's last
+// run's masks are computed by all its threads after the last run. This replaces a second launch (hp_kernel), which
+// re-read every sample, rebuilt the T-tables and ran after the whole seal. A thread takes up to HP_PASS_W records at
+// once so their loads are in flight together; when the wave's records share one key (a batch grouped by connection, or
+// one key) the round keys go to SGPRs and the HP_PASS_W AES chains interleave, otherwise each chain runs with its lanes'
+// own round keys. Not inlined: inlined, its registers raised the unit loop's pressure (and the register allocator
+// crashed on the constant-time kernel).
+#define HP_PASS_W 4
+#define HP_ITEM (64 * HP_PASS_W)  // records per work item of a wave
+template <int HNR>
+__device__ __attribute__((noinline)) void hp_masks_pass(const ptls_mi355x_hp_t *hp, const KeyEntry *hp_keys, u32 hp_nkeys,
+                                                        const uint8_t *out, uint8_t *masks, u64 p, u64 e, const u32 *perm,
+                                                        u32 tid, u32 nthr)
+{
+    const lds_u8 *lds = nullptr;  // (absolute LDS addressing: the T-tables are at address 0)
+    const u32 laneoff = (lane_here() & 31) * 4;
+    for (u64 t0 = p + tid; t0 < e; t0 += (u64)HP_PASS_W * nthr) {
+        u64 i[HP_PASS_W];
+        ptls_mi355x_hp_t h[HP_PASS_W];
+        u32x4 v[HP_PASS_W];
+#pragma unroll
+        for (int k = 0; k < HP_PASS_W; ++k) {
+            const u64 t = t0 + (u64)k * nthr;
+            i[k] = t < e ? (perm != nullptr ? (u64)perm[t] : t) : ~(u64)0;  // batch index: the hp entry and mask slot
+            h[k] = {0, 0xffffffffu, 0};
+            if (t < e)
+                h[k] = hp[i[k]];
+        }
+#pragma unroll
+        for (int k = 0; k < HP_PASS_W; ++k) {
+            v[k] = u32x4{0, 0, 0, 0};
+            if (h[k].key_idx < hp_nkeys)  // (a gather from HBM: half of the masks' cost)
+                v[k] = *(const u32x4_u *)(out + h[k].sample_off);
+        }
+        const u32 k0 = __builtin_amdgcn_readfirstlane(h[0].key_idx);
+        bool same = true;
+#pragma unroll
+        for (int k = 0; k < HP_PASS_W; ++k)
+            same = same && (i[k] == ~(u64)0 || h[k].key_idx == k0);
+        if (k0 < hp_nkeys && __all(same)) {
+            // (scalar loads through a constant-address-space pointer: readfirstlane of the loaded words crashed the
+            // register allocator)
+            typedef __attribute__((address_space(4))) const u32 const_u32;
+            const_u32 *key = (const_u32 *)(const void *)(hp_keys + k0);
+            u32 rk[HNR + 1][4];
+#pragma unroll
+            for (int r = 0; r <= HNR; ++r)
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    rk[r][c] = key[4 * r + c];
+            u32 st[HP_PASS_W][4];
+#pragma unroll
+            for (int k = 0; k < HP_PASS_W; ++k)
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    st[k][c] = v[k][c] ^ rk[0][c];
+            aes_rounds_n<HNR, 1, HP_PASS_W>(lds, laneoff, rk, st);
+#pragma unroll
+            for (int k = 0; k < HP_PASS_W; ++k)
+                if (i[k] != ~(u64)0)
+                    *(u32x4_u *)(masks + 16 * i[k]) = u32x4{st[k][0], st[k][1], st[k][2], st[k][3]};
+            continue;
+        }
+#pragma unroll
+        for (int k = 0; k < HP_PASS_W; ++k) {
+            if (i[k] == ~(u64)0)
+                continue;
+            u32x4 o = {0, 0, 0, 0};
+            if (h[k].key_idx < hp_nkeys) {  // (an out-of-range key: a zero mask)
+                const u32(*rk)[4] = hp_keys[h[k].key_idx].rk;
+                u32 s0 = v[k][0] ^ rk[0][0], s1 = v[k][1] ^ rk[0][1], s2 = v[k][2] ^ rk[0][2], s3 = v[k][3] ^ rk[0][3];
+                aes_encrypt_tt<HNR>(lds, laneoff, rk, s0, s1, s2, s3);
+                o = u32x4{s0, s1, s2, s3};
+            }
+            *(u32x4_u *)(masks + 16 * i[k]) = o;
+        }
+    }
+}
+
 template <int NR, bool OPEN, int FRAME, bool CT = false>
 __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGINE_WAVES_PER_SIMD, ENGINE_WAVES_PER_SIMD))) void gcm_chunked_kernel(BatchArgs args)
 {
@@ -396,6 +481,24 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         __builtin_amdgcn_wave_barrier();                          // after the prologue barrier
     }
     auto ok_at = [&](u64 i) -> u64 { return perm != nullptr ? (u64)perm[i] : i; };
+    // seal_batch_hp: the header-protection masks of each run's records once the run is sealed (hp_masks_pass; a macro,
+    // as a lambda called twice was outlined into a call, which put the kernel arguments on the stack). hp_pos / hp_n:
+    // the previous run's records, whose masks the current run's waves take as work items (RC_HPNEXT)
+    constexpr bool HPK = !OPEN && FRAME == 0;
+    const bool with_hp = HPK && args.hp != nullptr;
+    u64 hp_pos = 0;
+    u32 hp_n = 0;
+#define HP_PASS(p_, e_, tid_, nthr_)                                                                                    \
+    do {                                                                                                                \
+        if constexpr (HPK) {                                                                                            \
+            if (args.hp_nr == 10)                                                                                       \
+                hp_masks_pass<10>(args.hp, args.hp_keys, args.hp_nkeys, args.out, args.masks, (p_), (e_), perm, (tid_),  \
+                                  (nthr_));                                                                             \
+            else                                                                                                        \
+                hp_masks_pass<14>(args.hp, args.hp_keys, args.hp_nkeys, args.out, args.masks, (p_), (e_), perm, (tid_),  \
+                                  (nthr_));                                                                             \
+        }                                                                                                               \
+    } while (0)
 
     // the first run's state on wave 0 (later runs are scanned during the previous run's tail) while waves 1.. copy
     // the AES tables. A one-key launch knows its key before the scan: waves EARLY_GHASH_WAVE.. build its GHASH tables
@@ -461,6 +564,12 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             if (wave == 0 && nxt < nxt_end)
                 scan_run<OPEN, FRAME>(args, recs, nxt, nxt_end, rs_next);
             __syncthreads();
+            if (with_hp) {  // (no unit loop to take them: the previous run's masks and this run's, by every thread)
+                if (hp_n != 0)
+                    HP_PASS(hp_pos, hp_pos + hp_n, threadIdx.x, blockDim.x);
+                HP_PASS(pos, run_end, threadIdx.x, blockDim.x);
+                hp_n = 0;
+            }
             pos = nxt, end = nxt_end, cstart = nxt_cstart;
             rb ^= 1;
             continue;
@@ -521,8 +630,19 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             if (lane_here() == 0)
                 ub = atomicAdd((u32 *)&rs[RC_NEXT], (u32)RPW);
             ub = __builtin_amdgcn_readfirstlane(ub);
-            if (ub >= total_units)
+            if (ub >= total_units) {
+                if (with_hp && hp_n != 0) {  // the run's units are all handed out: masks of the previous run
+                    u32 m = 0;
+                    if (lane_here() == 0)
+                        m = atomicAdd((u32 *)&rs[RC_HPNEXT], (u32)HP_ITEM);
+                    m = __builtin_amdgcn_readfirstlane(m);
+                    if (m < hp_n) {
+                        HP_PASS(hp_pos + m, hp_pos + min(hp_n, m + (u32)HP_ITEM), lane_here(), 64u);
+                        continue;
+                    }
+                }
                 break;
+            }
             u32x4 acc;
             u32 okw;
             {
@@ -609,6 +729,8 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             scan_run<OPEN, FRAME>(args, recs, nxt, nxt_end, rs_next);
         PROF_STAMP(tw);
         __syncthreads();  // the run's tables, partials and counters are free again
+        if (with_hp)  // this run's records now await their masks (taken in the next run's unit loop)
+            hp_pos = pos, hp_n = run_n;
         PROF_STAMP(t3);
 #if ENGINE_PROFILE
         if (lane_here() == 0)
@@ -626,7 +748,10 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         pos = nxt, end = nxt_end, cstart = nxt_cstart;
         rb ^= 1;
     }
+    if (with_hp && hp_n != 0)  // the last run's masks
+        HP_PASS(hp_pos, hp_pos + hp_n, threadIdx.x, blockDim.x);
     publish_done(args.done_flag);  // the per-record path polls these instead of waiting for the stream
+#undef HP_PASS
 }
 
 #endif  // PTLS_MI355X_ENGINE_GCM_KERNELS_H

@@ -71,6 +71,14 @@ struct BatchArgs {
     u64 chunk;
     // chunked kernel: workgroup w walks records [bounds[w], bounds[w + 1]) (balance_bounds_kernel; null: chunk rule)
     const u64 *bounds;
+    // chunked seal with QUIC header protection (seal_batch_hp; null hp: none): mask[i] (16 bytes at masks + 16 i) =
+    // AES-ECB(hp_keys[hp[i].key_idx], 16 bytes at out + hp[i].sample_off), an hp_nr-round key; zero for a key index
+    // >= hp_nkeys
+    const ptls_mi355x_hp_t *hp;
+    const KeyEntry *hp_keys;
+    u32 hp_nkeys;
+    u32 hp_nr;
+    uint8_t *masks;
 };
 
 #define RUN_SCAN_CAP 256  // records examined per key-run scan (multi-key batches)

@@ -435,15 +435,20 @@ def test_hp_masks_kat_batch(kat):
         assert masks[i].tobytes().hex() == mask, i
 
 
-@pytest.mark.parametrize("key_size", [16, 32])
-def test_hp_masks_vs_fusion_supp(ref, key_size):
+@pytest.mark.parametrize("key_size,n,nkeys,sort_keys,schedule", [(16, 300, 5, True, "auto"), (32, 300, 5, True, "auto"),
+                                                                  (16, 3000, 40, False, "auto"), (32, 700, 3, True, "lockstep"),
+                                                                  (16, 20000, 1, True, "auto")])
+def test_hp_masks_vs_fusion_supp(ref, key_size, n, nkeys, sort_keys, schedule):
     # random QUIC-like packets through seal_batch_hp against fusion's encrypt_s with supp (lib/fusion.c:425-430,
     # 636-651), per-connection HP keys, sample offset 4 - pn_len into the ciphertext; then the receive-side masks of
-    # the same samples with hp_mask_batch
-    rng = np.random.default_rng(23 + key_size)
-    n, nkeys = 300, 5
-    lens = rng.integers(20, 1500, n)
-    key_idx = np.sort(rng.integers(0, nkeys, n))
+    # the same samples with hp_mask_batch. The chunked schedule computes the masks in the seal launch (each run's masks
+    # after its records), also for batches regrouped by key on the device and uniform one-key batches (whole-record
+    # runs); the lockstep schedule runs a second launch.
+    rng = np.random.default_rng(23 + key_size + n)
+    lens = rng.integers(20, 1500, n) if nkeys > 1 else np.full(n, 1200)
+    key_idx = rng.integers(0, nkeys, n)
+    if sort_keys:
+        key_idx = np.sort(key_idx)
     b = RecordBatch.build(lens, rng.integers(8, 30, n), seqs=rng.integers(0, 2**40, n, dtype=np.uint64), key_idx=key_idx)
     keys = np.frombuffer(rng.bytes(nkeys * key_size), np.uint8)
     ivs = np.frombuffer(rng.bytes(nkeys * 12), np.uint8)
@@ -456,6 +461,7 @@ def test_hp_masks_vs_fusion_supp(ref, key_size):
     hp["key_idx"] = key_idx
     hp["key_idx"][7] = nkeys + 3  # out of range: zero mask
     ks, hp_ks = pa.Keyset(keys, ivs, key_size), pa.Keyset(hp_keys, np.zeros(nkeys * 12, np.uint8), key_size)
+    ks.set_schedule(schedule)
     d_recs, d_pt, d_aad, d_hp = dev(b.seal), dev(pt), dev(aad), dev(hp)
     d_out, d_masks, d_masks2 = empty(b.sealed_bytes), empty(16 * n, 0x5A), empty(16 * n, 0x5A)
     pa.seal_batch_hp(ks, d_recs.data_ptr(), n, d_pt.data_ptr(), d_aad.data_ptr(), d_out.data_ptr(), hp_ks,
