@@ -1193,6 +1193,9 @@ int ptls_mi355x_quiclb_batch(ptls_mi355x_keyset_t *ks, const ptls_mi355x_cid_t *
 #define SPAN_MIN_BYTES ((size_t)262144)  // a lone record from this length runs over many workgroups (launch_span)
 #endif
 #define PERREC_FLAG_MAX_BYTES ((size_t)1 << 20)  // staged bytes of a call that polls (larger ones wait for the stream)
+#ifndef CT_UNIT_SHIFT
+#define CT_UNIT_SHIFT 0  // per-record launches of a constant-time keyset: unit length x 2^CT_UNIT_SHIFT
+#endif
 #ifndef PERREC_HP_FUSED
 #define PERREC_HP_FUSED 1  // encrypt_s: the header-protection mask computed by the seal launch (BatchArgs::hp)
 #endif
@@ -1426,7 +1429,12 @@ static void run_calls(DeviceState *ds, OneCall *const *c, size_t n)
             // wave ~2 us of latency, a unit combine ~0.15 us); steps / 2^k units balance the two (tools/latency.py).
             // Long records, and batches (one workgroup per record), pass CHUNK_LOG2: the kernel's scan then picks.
             const size_t steps = ((c0.aadlen + 15) / 16 + (c0.len + 15) / 16 + 1 + ENGINE_G - 1) / ENGINE_G;
-            const u32 unit_log2 = n > 1 ? CHUNK_LOG2 : steps <= 24 ? 0 : steps <= 96 ? 1 : steps <= 400 ? 2 : steps <= 1600 ? 3 : CHUNK_LOG2;
+            // (the constant-time variant: units CT_UNIT_SHIFT times longer, whose ends cost it 4 GHASH multiplies and
+            // whose combine links a whole gmul_tab each)
+            const u32 ushift = c0.ks->ct ? CT_UNIT_SHIFT : 0u;
+            u32 unit_log2 = n > 1 ? CHUNK_LOG2 : steps <= 24 ? 0 : steps <= 96 ? 1 : steps <= 400 ? 2 : steps <= 1600 ? 3 : CHUNK_LOG2;
+            if (n == 1)
+                unit_log2 = unit_log2 + ushift < CHUNK_LOG2 ? unit_log2 + ushift : CHUNK_LOG2;
             // (calls staging at most 1 MiB: a larger record's launch runs for hundreds of microseconds or more, which
             // the caller need not spend spinning on a core)
             const bool flag = PERREC_FLAG && call.mapped() && c0.ks->schedule != PTLS_MI355X_SCHEDULE_LOCKSTEP &&
