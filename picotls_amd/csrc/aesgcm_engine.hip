@@ -157,11 +157,18 @@ static int set_kernel_attrs(void)
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<10, true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<14, false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<14, true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
-#define CHUNKED_ATTR(nr, open, frame)                                                                                  \
-    HIP_TRY(hipFuncSetAttribute((const void *)gcm_chunked_kernel<nr, open, frame, false>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+#define CHUNKED_ATTR_X(nr, open, frame, ext)                                                                           \
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_chunked_kernel<nr, open, frame, false, ext>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                 CLDS_ALLOC));                                                                              \
-    HIP_TRY(hipFuncSetAttribute((const void *)gcm_chunked_kernel<nr, open, frame, true>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_chunked_kernel<nr, open, frame, true, ext>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                 CLDS_ALLOC))
+#define CHUNKED_ATTR(nr, open, frame) CHUNKED_ATTR_X(nr, open, frame, 0)
+    CHUNKED_ATTR_X(10, false, 0, 1);
+    CHUNKED_ATTR_X(10, true, 0, 1);
+    CHUNKED_ATTR_X(14, false, 0, 1);
+    CHUNKED_ATTR_X(14, true, 0, 1);
+    CHUNKED_ATTR_X(10, false, 0, 2);
+    CHUNKED_ATTR_X(14, false, 0, 2);
     CHUNKED_ATTR(10, false, 0);
     CHUNKED_ATTR(10, true, 0);
     CHUNKED_ATTR(14, false, 0);
@@ -175,6 +182,7 @@ static int set_kernel_attrs(void)
     CHUNKED_ATTR(14, false, 2);
     CHUNKED_ATTR(14, true, 2);
 #undef CHUNKED_ATTR
+#undef CHUNKED_ATTR_X
     HIP_TRY(hipFuncSetAttribute((const void *)ecb_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
     HIP_TRY(hipFuncSetAttribute((const void *)ecb_kernel<14>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
     HIP_TRY(hipFuncSetAttribute((const void *)hp_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
@@ -438,6 +446,12 @@ struct st_ptls_mi355x_keyset_t {
     u32 *d_group;
     size_t group_cap;
     hipEvent_t group_ev;
+    // small one-key batches with long records (spread_pieces): the pieces' partials and per-record counters (zero
+    // between launches), allocated on first use; spread_stream: the stream of the last launch that used them (a launch
+    // on another stream waits for that one's use event, note_use)
+    uint8_t *d_spread;
+    hipStream_t spread_stream;
+    bool spread_used;
 };
 
 static int mark_ready(ptls_mi355x_keyset_t *ks, hipStream_t s);
@@ -690,6 +704,8 @@ void ptls_mi355x_keyset_free(ptls_mi355x_keyset_t *ks)
     (void)hipMemsetAsync(ks->d_keys, 0, ks->nkeys * sizeof(KeyEntry), ds->maint);
     if (ks->d_group != nullptr)
         (void)hipFreeAsync(ks->d_group, ds->maint);
+    if (ks->d_spread != nullptr)
+        (void)hipFreeAsync(ks->d_spread, ds->maint);
     if (ks->slot) {
         // back to the pool once the clear has run (slot_get checks the event)
         hipEvent_t cleared = event_get(ds);
@@ -811,13 +827,33 @@ int ptls_mi355x_keyset_set_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, const vo
 // 784 vs 751 on 1200 B), and its chunked runs balance mixed lengths and short key runs.
 static bool use_chunked(int schedule) { return schedule != PTLS_MI355X_SCHEDULE_LOCKSTEP; }
 
+template <int NR, bool OPEN, int FRAME, int EXT = 0>
+static void launch_chunked_x(bool ct, unsigned grid, hipStream_t s, const BatchArgs &a)
+{
+    if (ct)
+        gcm_chunked_kernel<NR, OPEN, FRAME, true, EXT><<<grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
+    else
+        gcm_chunked_kernel<NR, OPEN, FRAME, false, EXT><<<grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
+}
+
+// the instantiation for the launch: unframed batches with a spread plan (EXT 1) or header-protection masks (EXT 2)
+// have their own (gcm_chunked_kernel)
 template <int NR, bool OPEN, int FRAME>
 static void launch_chunked(bool ct, unsigned grid, hipStream_t s, const BatchArgs &a)
 {
-    if (ct)
-        gcm_chunked_kernel<NR, OPEN, FRAME, true><<<grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
-    else
-        gcm_chunked_kernel<NR, OPEN, FRAME, false><<<grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
+    if constexpr (FRAME == 0) {
+        if (a.spread) {
+            launch_chunked_x<NR, OPEN, 0, 1>(ct, grid, s, a);
+            return;
+        }
+        if constexpr (!OPEN) {
+            if (a.hp != nullptr) {
+                launch_chunked_x<NR, false, 0, 2>(ct, grid, s, a);
+                return;
+            }
+        }
+    }
+    launch_chunked_x<NR, OPEN, FRAME>(ct, grid, s, a);
 }
 
 // Records per chunk of the chunked kernel's dealt-out assignment (BatchArgs::chunk), 0 for contiguous ranges. Each
@@ -844,6 +880,12 @@ static u64 deal_chunk(u64 nrecs, u64 grid)
     return 0;
 }
 
+// scratch of spread launches: per-record piece counters (SPREAD_MAX_RECS, zero between launches), then the pieces'
+// partials: at most one piece per spare workgroup, or (records longer than 2^10 units x their share) 2^19 / 2^10 = 512
+// per record (PTLS_MI355X_MAX_RECORD_LEN)
+#define SPREAD_MAX_RECS 255
+#define SPREAD_CNT_BYTES ((size_t)256 * 4)
+
 // Header-protection masks computed by the chunked seal launch itself (BatchArgs::hp; seal_batch_hp, encrypt_s)
 struct HpLaunch {
     const ptls_mi355x_hp_t *hp;
@@ -860,7 +902,8 @@ static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int sche
                       const ptls_mi355x_record_t *recs, size_t nrecs, const void *in, const void *aad, void *out, uint8_t *ok,
                       hipStream_t s, int frame, u32 unit_log2, const ptls_mi355x_record_t *grouped = nullptr,
                       const u32 *perm = nullptr, const u32 *perm_on = nullptr, const ptls_mi355x_record_t *one = nullptr,
-                      u32 *done_flag = nullptr, const u64 *bounds = nullptr, const HpLaunch *hpl = nullptr)
+                      u32 *done_flag = nullptr, const u64 *bounds = nullptr, const HpLaunch *hpl = nullptr,
+                      uint8_t *spread = nullptr)
 {
     BatchArgs a = {keys, recs, (u64)nrecs, (const uint8_t *)in, (const uint8_t *)aad, (uint8_t *)out, ok,
                    nkeys > 1 ? 1u : 0u, nkeys, unit_log2, grouped, perm, perm_on, 0u, {}, done_flag, 0, bounds};
@@ -873,9 +916,16 @@ static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int sche
         a.one_inline = 1, a.one = *one;
     if (a.aad == NULL)
         a.aad = a.in;
-    // one persistent workgroup per CU. A batch with fewer records than CUs takes one workgroup per record.
+    // one persistent workgroup per CU. A batch with fewer records than CUs takes one workgroup per record, or (spread,
+    // a one-key batch: spread_pieces) one per CU, the workgroups beyond the records sharing its long records
     u64 grid = (u64)ncu;
-    if (grid > nrecs)
+    if (spread != nullptr && nkeys == 1 && frame == 0 && nrecs >= 2 && nrecs < (u64)ncu && nrecs <= SPREAD_MAX_RECS &&
+        hpl == nullptr && one == nullptr && (ct || use_chunked(schedule))) {
+        a.spread = 1;
+        a.spread_cnt = (u32 *)spread;
+        a.spread_part = (u32x4 *)(spread + SPREAD_CNT_BYTES);
+    }
+    if (grid > nrecs && !a.spread)
         grid = nrecs;
     if (grid < 1)
         grid = 1;
@@ -958,6 +1008,39 @@ static int launch_span(const KeyEntry *key, int nr, bool ct, bool open, const pt
     return 0;
 }
 
+static size_t spread_bytes(int ncu) { return SPREAD_CNT_BYTES + 16 * ((size_t)ncu + (size_t)SPREAD_MAX_RECS * 513); }
+
+// the keyset's spread scratch for a launch on `s` (allocated and zeroed in stream order on first use); nullptr when the
+// batch cannot take the spread launch (spread_done records the use afterwards)
+static uint8_t *spread_scratch(ptls_mi355x_keyset_t *ks, hipStream_t s, size_t nrecs, int frame)
+{
+    if (ks->nkeys != 1 || frame != 0 || nrecs < 2 || nrecs >= (size_t)ks->ds->ncu || nrecs > SPREAD_MAX_RECS ||
+        !(ks->ct || use_chunked(ks->schedule)))
+        return nullptr;
+    std::lock_guard<std::mutex> lk(ks->mu);
+    // a launch on another stream than the last user waits for that launch (its use event, recorded after it by
+    // note_use); back-to-back launches on one stream add no event packets (a wait and a record per launch cost a
+    // 23 us small-batch launch 7 us)
+    if (ks->spread_used && ks->spread_stream != s) {
+        for (auto &u : ks->uses)
+            if (u.first == ks->spread_stream && hipStreamWaitEvent(s, u.second, 0) != hipSuccess)
+                return nullptr;
+    }
+    ks->spread_stream = s;
+    ks->spread_used = true;
+    if (ks->d_spread == nullptr) {
+        const size_t bytes = spread_bytes(ks->ds->ncu);
+        if (hipMallocAsync((void **)&ks->d_spread, bytes, s) != hipSuccess)
+            return nullptr;
+        if (hipMemsetAsync(ks->d_spread, 0, SPREAD_CNT_BYTES, s) != hipSuccess) {
+            (void)hipFreeAsync(ks->d_spread, s);
+            ks->d_spread = nullptr;
+            return nullptr;
+        }
+    }
+    return ks->d_spread;
+}
+
 // A batch call on a keyset: waits for the keyset's setup, groups an ungrouped many-key batch by key on the device, launches,
 // and records the use (teardown and rekey are ordered after it).
 static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_record_t *recs, size_t nrecs, const void *in,
@@ -1019,8 +1102,10 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
         if (ret == 0)
             HIP_TRY(hipEventRecord(ks->group_ev, s));
     } else {
+        uint8_t *spread = hpl == nullptr ? spread_scratch(ks, s, nrecs, frame) : nullptr;
         ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, ks->ct, open, recs, nrecs, in, aad, out, ok,
-                         s, frame, CHUNK_LOG2, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, hpl);
+                         s, frame, CHUNK_LOG2, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, hpl, spread);
+        (void)spread;
     }
     if (ret != 0)
         return -1;

@@ -53,7 +53,7 @@ struct KeyEntry {
     u32 rk[15][4];  // round keys, LE column words; rounds 1..NR-1 stored rotated right by 8 bits (see aes_rounds_n)
     u32 iv[4];      // static IV as LE words (word 3 = 0)
     u32 h[16][4];   // GHASH elements (LE words): [0..7] = H^1..H^8, [8] = H^CHUNK_BLOCKS, [9..12] = H^16, H^32, H^64, H^128
-                    // (the combine powers of smaller units), [12..15] = 0
+                    // (the combine powers of smaller units), [13..15] = H^256, H^512, H^1024 (spread_pieces)
 };
 static_assert(sizeof(KeyEntry) == 512, "KeyEntry layout");
 
@@ -124,6 +124,7 @@ __device__ __forceinline__ u32 lane_here()
 #define CLDS_PART (CLDS_RUN1 + 4 * RUN_WORDS)                    // 16 B per unit: GHASH partial
 #define CLDS_ONE (CLDS_PART + 16 * CRUN_UNITS)                   // a lone record's descriptor (BatchArgs::one)
 #define CLDS_ALLOC (CLDS_ONE + 48)
+#define SPAN_MAX_UNITS CRUN_UNITS  // units per span of a long record (span_kernels.h, spread_pieces): the LDS partials
 static_assert(CLDS_ALLOC <= 160 * 1024, "chunked schedule LDS budget");
 static_assert(CHUNK_BLOCKS % ENGINE_G == 0, "units are whole steps");
 static_assert((CHUNK_STEPS & (CHUNK_STEPS - 1)) == 0 && CHUNK_STEPS <= 32, "unit lengths are powers of two up to 32 steps");

@@ -23,6 +23,16 @@ __device__ __forceinline__ bool record_ok(const BatchArgs &args, const ptls_mi35
            r.key_idx < args.nkeys;
 }
 
+// A small one-key batch's long records go to the spare workgroups (spread_pieces): from 512 KiB (a 256 KiB record cut
+// into pieces paid more in the pieces' combine than it gained: 40 x 256 KiB 89 -> 124 us)
+#ifndef SPREAD_MIN_BYTES
+#define SPREAD_MIN_BYTES (512u << 10)
+#endif
+__device__ __forceinline__ bool spread_long(const BatchArgs &a, const ptls_mi355x_record_t &r)
+{
+    return r.len >= SPREAD_MIN_BYTES && record_ok<0>(a, r);
+}
+
 // Seals / opens one whole record per G-lane group.
 template <int NR, bool OPEN, int NB>
 __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u8 *lds, const u32 (&rk)[NR + 1][4], u32 iv0,
@@ -196,7 +206,7 @@ __device__ __forceinline__ u32 run_unit_log2(u32 total_steps, u32 smax, u32 cap)
     return fill > chain ? fill : chain;
 }
 
-template <bool OPEN, int FRAME, bool FIRST = false>
+template <bool OPEN, int FRAME, bool FIRST = false, int EXT = 0>
 __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355x_record_t *__restrict__ recs, u64 p, u64 end,
                                       lds_u32 *rs)
 {
@@ -218,7 +228,7 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
         if (t < lim) {
             ptls_mi355x_record_t r = recs[p + t];
             other = args.multi_key && r.key_idx != key;
-            if (!record_ok<FRAME>(args, r))  // rejected: one empty unit (see the unit loop)
+            if (!record_ok<FRAME>(args, r) || (EXT == 1 && spread_long(args, r)))  // rejected or spread: one empty unit
                 r.len = 0, r.aad_len = 0, r.flags = 0;
             steps[q] = gcm_steps<OPEN, FRAME>(r);
         }
@@ -442,7 +452,175 @@ __device__ __attribute__((noinline)) void hp_masks_pass(const ptls_mi355x_hp_t *
     }
 }
 
-template <int NR, bool OPEN, int FRAME, bool CT = false>
+
+// ---- small one-key batches with long records (fusion takes records of any length at full
+// speed, lib/fusion.c:1018-1041,1141-1145). The chunked kernel gives a record to one workgroup; in a batch of a few
+// records a long one then runs on one CU (10 x 1 MiB: 10 CUs, 0.3 ms). For a one-key batch of fewer records than CUs
+// the launch takes one workgroup per CU: workgroup w < nrecs seals or opens record w unless it is long (spread_long),
+// and the other workgroups share the long records, each record cut into pieces of 2^e 16-step units counted from the
+// stream's end (as the per-record path's span kernels cut a lone record, span_kernels.h). A workgroup seals its piece's
+// units, one per 8-lane group, folds their partials into Q_s = sum_u P_(s 2^e + u) H^(128 u), stores it, and the piece
+// that completes a record evaluates GHASH = sum_s Q_s M^s, M = H^(128 2^e) (e squarings of H^128 from a window table it
+// builds), by Horner, and writes the tag or the ok byte.
+#define SPREAD_PLAN_CTL 512  // plan words: [0, 256) first piece of record t, [256, 512) its e, [512] pieces in total
+
+template <int NR, bool OPEN, bool CT>
+__device__ __attribute__((noinline)) void spread_pieces(BatchArgs args, u32 w, u32 nspare)
+{
+    lds_u8 *lds = (lds_u8 *)nullptr;  // absolute LDS addressing (the kernel checked its base)
+    lds_u32 *plan = (lds_u32 *)(lds + CLDS_RUN0);
+    lds_u32x4 *s_part = (lds_u32x4 *)(lds + CLDS_PART);
+    lds_u32 *s_flag = (lds_u32 *)(lds + CLDS_ONE);
+    constexpr int G = ENGINE_G;
+    const u32 wave = threadIdx.x >> 6;
+    const u32 n = (u32)args.nrecs;  // < 256 (the host's condition)
+    if (wave == 0) {
+        // the plan, the same in every workgroup: the spare workgroups shared among the long records by their units
+        const u32 lane = lane_here();
+        u32 units[4], tot = 0;
+#pragma unroll
+        for (u32 q = 0; q < 4; ++q) {
+            const u32 t = q * 64 + lane;
+            units[q] = 0;
+            if (t < n) {
+                const ptls_mi355x_record_t r = args.recs[t];
+                if (spread_long(args, r))
+                    units[q] = (gcm_steps<OPEN, 0>(r) + CHUNK_STEPS - 1) / CHUNK_STEPS;
+            }
+            tot += units[q];
+        }
+        tot = (u32)__builtin_amdgcn_readlane((int)wave_incl_sum(tot), 63);
+        u32 carry = 0;
+#pragma unroll
+        for (u32 q = 0; q < 4; ++q) {
+            const u32 t = q * 64 + lane;
+            u32 np = 0, e = 0;
+            if (units[q] != 0) {
+                const u64 share = (u64)nspare * units[q] / (tot != 0 ? tot : 1u);
+                const u32 wr = share > 1 ? (u32)share : 1u;
+                const u32 us = (units[q] + wr - 1) / wr;
+                while ((1u << e) < us && (1u << e) < SPAN_MAX_UNITS)
+                    ++e;
+                np = (units[q] + (1u << e) - 1) >> e;
+            }
+            const u32 incl = carry + wave_incl_sum(np);
+            if (t < 256) {
+                plan[t] = incl - np;
+                plan[256 + t] = e;
+            }
+            carry = (u32)__builtin_amdgcn_readlane((int)incl, 63);
+        }
+        if (lane == 0)
+            plan[SPREAD_PLAN_CTL] = carry;
+    }
+    __syncthreads();
+    const u32 P = __builtin_amdgcn_readfirstlane(plan[SPREAD_PLAN_CTL]);
+    if (w >= P)
+        return;  // nothing for this workgroup (a batch without long records: every spare one)
+    if (wave >= EARLY_GHASH_WAVE)  // H^1..H^8 and H^128 of key 0; the AES tables on the other waves
+        build_ghash_tables(lds, args.keys, 9, 8, 0, EARLY_GHASH_WAVE * 64, ENGINE_WG - EARLY_GHASH_WAVE * 64);
+    else
+        build_aes_tables(lds, 0, EARLY_GHASH_WAVE * 64);
+    __syncthreads();
+    const KeyEntry *key = args.keys;
+    u32 rk[NR + 1][4];
+#pragma unroll
+    for (int r = 0; r <= NR; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            rk[r][c] = __builtin_amdgcn_readfirstlane(key->rk[r][c]);
+    const u32 iv0 = __builtin_amdgcn_readfirstlane(key->iv[0]), iv1 = __builtin_amdgcn_readfirstlane(key->iv[1]),
+              iv2 = __builtin_amdgcn_readfirstlane(key->iv[2]);
+    const u32 tsel_horner = 0x10000u + (u32)(G - 1) * GHASH_TABLE_BYTES, tsel_chunk = 0x10000u + 8u * GHASH_TABLE_BYTES;
+    for (u32 p = w; p < P; p += nspare) {
+        // the piece's record: the last t with plan[t] <= p (records without pieces share the next one's start)
+        u32 lo = 0, hi = n;
+        while (hi - lo > 1) {
+            const u32 mid = (lo + hi) >> 1;
+            if (plan[mid] <= p)
+                lo = mid;
+            else
+                hi = mid;
+        }
+        const u32 t = __builtin_amdgcn_readfirstlane(lo), s = p - plan[t], e = plan[256 + t], pbase = plan[t];
+        const u32 np_t = (t + 1 < n ? plan[t + 1] : P) - pbase;
+        const ptls_mi355x_record_t r = args.recs[t];
+        const u32 steps = gcm_steps<OPEN, 0>(r), U = (steps + CHUNK_STEPS - 1) / CHUNK_STEPS;
+        const u32 k0 = s << e, nu = min(U - k0, 1u << e);
+        for (u32 uu0 = wave * 8; uu0 < nu; uu0 += ENGINE_WG / G) {
+            const u32 lane = lane_here(), j = lane % G, uu = uu0 + lane / G, laneoff = (lane & 31) * 4;
+            const bool valid = uu < nu;
+            const u32 k = k0 + uu;
+            u32 m_hi = 0, m_lo = 0;
+            if (valid) {
+                m_hi = steps - k * CHUNK_STEPS;
+                m_lo = k + 1 == U ? 0u : m_hi - CHUNK_STEPS;
+            }
+            u32x4 acc;
+            u32 okw;
+            gcm_segment<NR, OPEN, 1, 0, CT>(args, lds, rk, iv0, iv1, iv2, r, valid, m_lo, m_hi, j, laneoff, tsel_horner, acc,
+                                            false, okw, false);
+            if (valid && j == G - 1)  // (the record's last unit includes E(K, J0), gcm_segment)
+                s_part[uu] = acc;
+        }
+        __syncthreads();
+        if (wave == 0) {  // Q_s by Horner from the piece's highest unit down (every lane of wave 0 holds it)
+            const u32 lane = lane_here();
+            u32x4 g = s_part[nu - 1];
+            for (u32 i = nu - 1; i-- > 0;)
+                g = (CT ? gmul_tab(lds, g, tsel_chunk) : gmul_group(lds, g, tsel_chunk, lane % G)) ^ s_part[i];
+            if (lane == 0) {
+                args.spread_part[pbase + s] = g;
+                __threadfence();  // the partial is visible device-wide before the count that publishes it
+                *s_flag = atomicAdd(args.spread_cnt + t, 1u) == np_t - 1;
+            }
+        }
+        __syncthreads();
+        if (*s_flag) {  // this piece completed the record: GHASH = sum_s Q_s M^s, M = (H^128)^(2^e)
+            __threadfence();
+            lds_u32x4 *s_m = (lds_u32x4 *)(lds + CLDS_PART + GHASH_TABLE_BYTES);  // M (after the element table)
+            // H^(128 * 2^e) from the keyset for e <= 3 (h[12 + e]), else by squaring H^1024
+            const u32 hi = e <= 3 ? 12 + e : 15;
+            if (threadIdx.x == 0)
+                *s_m = u32x4{key->h[hi][0], key->h[hi][1], key->h[hi][2], key->h[hi][3]};
+            __syncthreads();
+            for (u32 i = 3; i < e; ++i) {
+                build_elem_table(lds, CLDS_PART, *s_m);
+                __syncthreads();
+                const u32x4 sq = gmul_tab(lds, *s_m, CLDS_PART);
+                __syncthreads();
+                if (threadIdx.x == 0)
+                    *s_m = sq;
+                __syncthreads();
+            }
+            build_elem_table(lds, CLDS_PART, *s_m);
+            __syncthreads();
+            if (wave == 0) {
+                const u32 lane = lane_here();
+                const volatile u32x4 *vp = args.spread_part + pbase;  // (written by other workgroups: not cached reads)
+                u32x4 g = vp[np_t - 1];
+                for (u32 i = np_t - 1; i-- > 0;)
+                    g = gmul_tab(lds, g, CLDS_PART) ^ u32x4(vp[i]);
+                if (lane == 0) {
+                    if (OPEN) {
+                        const u32x4 rt = *(const u32x4_u *)(args.in + r.in_off + r.len);
+                        const u32x4 d = rt ^ g;
+                        args.ok[t] = (d[0] | d[1] | d[2] | d[3]) == 0;
+                    } else {
+                        *(u32x4_u *)(args.out + r.out_off + r.len) = g;
+                    }
+                    args.spread_cnt[t] = 0;  // zero for the next launch
+                }
+            }
+        }
+        __syncthreads();  // s_part, s_flag and the element table are free again
+    }
+}
+
+// EXT (FRAME 0 only): 0 = plain; 1 = a spread launch (a small one-key batch, spread_pieces); 2 = seal with
+// header-protection masks (seal_batch_hp). Separate instantiations: the calls these add (spread_pieces, hp_masks_pass)
+// cost the plain kernels' loops registers (16 KiB seal -1.2 % with both compiled into one kernel).
+template <int NR, bool OPEN, int FRAME, bool CT = false, int EXT = 0>
 __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGINE_WAVES_PER_SIMD, ENGINE_WAVES_PER_SIMD))) void gcm_chunked_kernel(BatchArgs args)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -459,10 +637,17 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     const u32 tsel_chunk = 0x10000u + 8u * GHASH_TABLE_BYTES;
 
     const u64 n = args.nrecs, C = args.bounds != nullptr ? 0 : args.chunk;
+    constexpr bool SPREAD = FRAME == 0 && EXT == 1;
+    if constexpr (SPREAD) {  // a small one-key batch (spread_pieces): workgroup w < n takes record w unless it is long
+        if (blockIdx.x >= n) {
+            spread_pieces<NR, OPEN, CT>(args, blockIdx.x - (u32)n, gridDim.x - (u32)n);
+            return;
+        }
+    }
     // this workgroup's records: the chunk [beg, end) (cstart: its first record), then the chunk grid * C further on
-    // (C != 0), or one contiguous range (C == 0): balanced by weight (args.bounds) or by count
-    const u64 beg = args.bounds != nullptr ? args.bounds[blockIdx.x] : C != 0 ? min(n, (u64)blockIdx.x * C) : n * blockIdx.x / gridDim.x;
-    u64 end = args.bounds != nullptr ? args.bounds[blockIdx.x + 1] : C != 0 ? min(n, beg + C) : n * (blockIdx.x + 1) / gridDim.x;
+    // (C != 0), or one contiguous range (C == 0): balanced by weight (args.bounds) or by count (spread: record w)
+    const u64 beg = SPREAD ? (u64)blockIdx.x : args.bounds != nullptr ? args.bounds[blockIdx.x] : C != 0 ? min(n, (u64)blockIdx.x * C) : n * blockIdx.x / gridDim.x;
+    u64 end = SPREAD ? (u64)blockIdx.x + 1 : args.bounds != nullptr ? args.bounds[blockIdx.x + 1] : C != 0 ? min(n, beg + C) : n * (blockIdx.x + 1) / gridDim.x;
     u64 cstart = beg;
     u32 loaded_key = 0xffffffffu, loaded_usrc = 0xffffffffu;
     // the descriptors in batch order, or (an ungrouped many-key batch) the key-grouped copy built on the device; ok
@@ -484,7 +669,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     // seal_batch_hp: the header-protection masks of each run's records once the run is sealed (hp_masks_pass; a macro,
     // as a lambda called twice was outlined into a call, which put the kernel arguments on the stack). hp_pos / hp_n:
     // the previous run's records, whose masks the current run's waves take as work items (RC_HPNEXT)
-    constexpr bool HPK = !OPEN && FRAME == 0;
+    constexpr bool HPK = !OPEN && FRAME == 0 && EXT == 2;
     const bool with_hp = HPK && args.hp != nullptr;
     u64 hp_pos = 0;
     u32 hp_n = 0;
@@ -512,7 +697,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                            ENGINE_WG - EARLY_GHASH_WAVE * 64);
     } else if (wave == 0) {
         if (beg < end)
-            scan_run<OPEN, FRAME, true>(args, recs, beg, end, (lds_u32 *)(lds + CLDS_RUN0));
+            scan_run<OPEN, FRAME, true, EXT>(args, recs, beg, end, (lds_u32 *)(lds + CLDS_RUN0));
 #if ENGINE_PROFILE
         if (threadIdx.x == 0)
             PROF_ADD(9, stamp() - tk), PROF_ADD(10, 1);
@@ -562,7 +747,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 for (u64 t = pos + threadIdx.x; t < run_end; t += blockDim.x)
                     args.ok[ok_at(t)] = 0;
             if (wave == 0 && nxt < nxt_end)
-                scan_run<OPEN, FRAME>(args, recs, nxt, nxt_end, rs_next);
+                scan_run<OPEN, FRAME, false, EXT>(args, recs, nxt, nxt_end, rs_next);
             __syncthreads();
             if (with_hp) {  // (no unit loop to take them: the previous run's masks and this run's, by every thread)
                 if (hp_n != 0)
@@ -654,10 +839,12 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 ptls_mi355x_record_t r = {};
                 if (valid)
                     r = recs[pos + lo];
-                const bool live = valid && record_ok<FRAME>(args, r);
+                // a long record of a spread launch is another workgroup's (spread_pieces): nothing here, not even ok
+                const bool spread = SPREAD && valid && spread_long(args, r);
+                const bool live = valid && !spread && record_ok<FRAME>(args, r);
                 if (valid && !live) {  // rejected descriptor: the scan gave it one unit; nothing is written
                     r.len = 0, r.aad_len = 0, r.flags = 0;
-                    if (OPEN && j == 0)
+                    if (OPEN && j == 0 && !spread)
                         args.ok[ok_at(pos + lo)] = 0;
                 }
                 const u32 steps = gcm_steps<OPEN, FRAME>(r);
@@ -726,7 +913,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         if (lane_here() == 0)
             claim = atomicAdd((u32 *)&rs[RC_CLAIM], 1u) == 0;
         if (__builtin_amdgcn_readfirstlane(claim) && nxt < nxt_end)
-            scan_run<OPEN, FRAME>(args, recs, nxt, nxt_end, rs_next);
+            scan_run<OPEN, FRAME, false, EXT>(args, recs, nxt, nxt_end, rs_next);
         PROF_STAMP(tw);
         __syncthreads();  // the run's tables, partials and counters are free again
         if (with_hp)  // this run's records now await their masks (taken in the next run's unit loop)

@@ -132,10 +132,11 @@ __device__ void setup_entry(const S &sb, const uint8_t *k, const uint8_t *v, Key
     u32 s[4] = {0, 0, 0, 0};
     aes_plain<nr>(sb, rk, s);
     // H as big-endian words for the bitwise multiply (SP 800-38D Algorithm 1): H^1..H^8 by multiplication, then
-    // H^16, H^32, H^64, H^CHUNK_BLOCKS by squaring (11 products instead of a walk over every power)
+    // H^16 .. H^1024 by squaring (14 products instead of a walk over every power); H^256..H^1024 are the piece
+    // multipliers of long records over many workgroups (spread_pieces)
     const u32 hb[4] = {bswap32(s[0]), bswap32(s[1]), bswap32(s[2]), bswap32(s[3])};
     u32 p[4] = {hb[0], hb[1], hb[2], hb[3]};  // current power, big-endian words
-    u32 out[13][4];
+    u32 out[16][4];
 #pragma unroll
     for (int n = 1; n <= 8; ++n) {
         for (int c = 0; c < 4; ++c)
@@ -151,7 +152,7 @@ __device__ void setup_entry(const S &sb, const uint8_t *k, const uint8_t *v, Key
     for (int c = 0; c < 4; ++c)
         out[8][c] = out[7][c], out[12][c] = 0;  // CHUNK_BLOCKS == 8
 #pragma unroll
-    for (int n = 16; n <= (CHUNK_BLOCKS > 128 ? CHUNK_BLOCKS : 128); n *= 2) {
+    for (int n = 16; n <= 1024; n *= 2) {
         const u32 q[4] = {p[0], p[1], p[2], p[3]};
         if (WAVE)
             gf_mul_be_wave(p, q);  // p = H^n
@@ -160,19 +161,16 @@ __device__ void setup_entry(const S &sb, const uint8_t *k, const uint8_t *v, Key
         if (n == CHUNK_BLOCKS)
             for (int c = 0; c < 4; ++c)
                 out[8][c] = bswap32(p[c]);
-        if (n <= 128)
-            for (int c = 0; c < 4; ++c)
-                out[n == 16 ? 9 : n == 32 ? 10 : n == 64 ? 11 : 12][c] = bswap32(p[c]);
+        const int slot = n == 16 ? 9 : n == 32 ? 10 : n == 64 ? 11 : n == 128 ? 12 : n == 256 ? 13 : n == 512 ? 14 : 15;
+        for (int c = 0; c < 4; ++c)
+            out[slot][c] = bswap32(p[c]);
     }
     if (writer) {
 #pragma unroll
-        for (int n = 0; n < 13; ++n)
+        for (int n = 0; n < 16; ++n)
 #pragma unroll
             for (int c = 0; c < 4; ++c)
                 e->h[n][c] = out[n][c];
-        for (int n = 13; n < 16; ++n)
-            for (int c = 0; c < 4; ++c)
-                e->h[n][c] = 0;
     }
 }
 

@@ -128,4 +128,41 @@ __device__ void build_ghash_tables(lds_u8 *lds, KeyPtr key, u32 ntables = ENGINE
     }
 }
 
+// The 4-bit window table of one GHASH element at LDS offset `base` (a multiple of 256), by threads [0, 32): the same
+// construction as build_ghash_tables for an element given by value.
+__device__ __forceinline__ void build_elem_table(lds_u8 *lds, u32 base, u32x4 h)
+{
+    const u32 p = threadIdx.x;
+    if (p >= 32)
+        return;
+    u32 b0 = bswap32(h[0]), b1 = bswap32(h[1]), b2 = bswap32(h[2]), b3 = bswap32(h[3]);
+    for (u32 k = 0; k < (p >> 3); ++k)
+        gf_mulxs_be(b0, b1, b2, b3, 32);
+    if (p & 7)
+        gf_mulxs_be(b0, b1, b2, b3, 4 * (p & 7));
+    u32x4 v[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        v[m] = u32x4{bswap32(b0), bswap32(b1), bswap32(b2), bswap32(b3)};
+        if (m < 3)
+            gf_mulxs_be(b0, b1, b2, b3, 1);
+    }
+    const u32 c = p & 15;
+    u32x4 ec = {0, 0, 0, 0};
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+        if ((c >> (3 - m)) & 1u)
+            ec ^= v[m];
+    lds_u32x4 *row = (lds_u32x4 *)(lds + base + p * 256);
+#pragma unroll
+    for (u32 n = 0; n < 16; ++n) {
+        u32x4 e = ec;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            if ((n >> (3 - m)) & 1u)
+                e ^= v[m];
+        row[n ^ c] = e;
+    }
+}
+
 #endif  // PTLS_MI355X_ENGINE_LDS_TABLES_H

@@ -79,6 +79,12 @@ struct BatchArgs {
     u32 hp_nkeys;
     u32 hp_nr;
     uint8_t *masks;
+    // chunked kernel, a small one-key batch (nrecs < grid; spread_pieces): workgroups [0, nrecs) take record w each,
+    // except long ones (spread_long), which the workgroups [nrecs, grid) share; spread_part (grid x 16 B) holds their
+    // pieces' GHASH partials, spread_cnt (nrecs counters, zero between launches) counts finished pieces per record
+    u32 spread;
+    u32x4 *spread_part;
+    u32 *spread_cnt;
 };
 
 #define RUN_SCAN_CAP 256  // records examined per key-run scan (multi-key batches)

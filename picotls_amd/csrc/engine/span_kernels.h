@@ -14,45 +14,8 @@
 #ifndef PTLS_MI355X_ENGINE_SPAN_KERNELS_H
 #define PTLS_MI355X_ENGINE_SPAN_KERNELS_H
 
-#define SPAN_MAX_UNITS 1024                                             // units per span (the LDS partials)
+// SPAN_MAX_UNITS (units per span, the LDS partials): common.h
 #define SPAN_LDS (LDS_BYTES + GHASH_TABLE_BYTES + 16 * SPAN_MAX_UNITS)  // AES + H^1..H^8 + H^128 tables + partials
-
-// The 4-bit window table of one GHASH element at LDS offset `base` (a multiple of 256), by threads [0, 32): the same
-// construction as build_ghash_tables for an element given by value.
-__device__ __forceinline__ void build_elem_table(lds_u8 *lds, u32 base, u32x4 h)
-{
-    const u32 p = threadIdx.x;
-    if (p >= 32)
-        return;
-    u32 b0 = bswap32(h[0]), b1 = bswap32(h[1]), b2 = bswap32(h[2]), b3 = bswap32(h[3]);
-    for (u32 k = 0; k < (p >> 3); ++k)
-        gf_mulxs_be(b0, b1, b2, b3, 32);
-    if (p & 7)
-        gf_mulxs_be(b0, b1, b2, b3, 4 * (p & 7));
-    u32x4 v[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        v[m] = u32x4{bswap32(b0), bswap32(b1), bswap32(b2), bswap32(b3)};
-        if (m < 3)
-            gf_mulxs_be(b0, b1, b2, b3, 1);
-    }
-    const u32 c = p & 15;
-    u32x4 ec = {0, 0, 0, 0};
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-        if ((c >> (3 - m)) & 1u)
-            ec ^= v[m];
-    lds_u32x4 *row = (lds_u32x4 *)(lds + base + p * 256);
-#pragma unroll
-    for (u32 n = 0; n < 16; ++n) {
-        u32x4 e = ec;
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-            if ((n >> (3 - m)) & 1u)
-                e ^= v[m];
-        row[n ^ c] = e;
-    }
-}
 
 // Workgroup s: the units [s * span, min(units, (s + 1) * span)) of the record args.one (key 0 of args.keys), Q_s to
 // part[s]. 16-step units; the record's stream is front-padded to whole steps (gcm_segment, not aligned). CT: the
@@ -129,11 +92,11 @@ __global__ __launch_bounds__(256) void span_combine_kernel(BatchArgs args, u32 n
     const u32 t = threadIdx.x;
     s_val[t] = t < nspans ? part[t] : u32x4{0, 0, 0, 0};
     if (t == 0) {
-        const u32 *h = args.keys->h[8];  // H^128
+        const u32 *h = args.keys->h[e <= 3 ? 12 + e : 15];  // H^(128 * 2^min(e, 3)): H^128 .. H^1024 (keyset)
         *s_pow = u32x4{h[0], h[1], h[2], h[3]};
     }
     __syncthreads();
-    for (u32 i = 0; i < e; ++i) {  // M = (H^128)^(2^e): square e times (a table of the element, then one product)
+    for (u32 i = 3; i < e; ++i) {  // M = (H^128)^(2^e): the squarings left (a table of the element, then one product)
         build_elem_table(lds, 0, *s_pow);
         __syncthreads();
         const u32x4 sq = gmul_tab(lds, *s_pow, 0);

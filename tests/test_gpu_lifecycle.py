@@ -404,3 +404,58 @@ def test_long_records_over_many_workgroups_vs_fusion(ref, key_size):
     hp.ks.free()
     enc.free()
     dec.free()
+
+
+@pytest.mark.parametrize("key_size,ct,case", [(16, False, "10x1MiB"), (32, False, "mixed"), (16, True, "mixed"),
+                                              (16, False, "threshold"), (32, True, "two_huge")])
+def test_small_batch_long_records_spread_vs_fusion(ref, key_size, ct, case):
+    # a one-key batch of fewer records than CUs whose long records (>= 512 KiB) are shared by the spare workgroups
+    # (spread_pieces): every sealed record equals fusion's, opens verify, and a tampered long record is rejected while
+    # its neighbours still open
+    rng = np.random.default_rng({"10x1MiB": 1, "mixed": 2, "threshold": 3, "two_huge": 4}[case] + key_size)
+    if case == "10x1MiB":
+        lens = np.full(10, 1 << 20)
+    elif case == "mixed":
+        lens = np.concatenate([rng.integers(0, 3000, 40), rng.integers(256 << 10, 3 << 20, 6)])
+        rng.shuffle(lens)
+    elif case == "threshold":
+        lens = np.array([(512 << 10) - 1, 512 << 10, (512 << 10) + 1, 16, 0, (512 << 10) + 15, 100000, 300000])
+    else:
+        lens = np.array([5 << 20, 77, (9 << 20) + 3])
+    n = len(lens)
+    b = RecordBatch.build(lens, rng.integers(0, 40, n), seqs=rng.integers(0, 2**62, n, dtype=np.uint64))
+    key, iv = rng.bytes(key_size), rng.bytes(12)
+    ks = pa.Keyset(key, iv, key_size)
+    ks.set_constant_time(ct)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(max(b.aad_bytes, 1)), np.uint8)
+    dev = torch.device("cuda:0")
+    d_seal, d_open = (torch.from_numpy(x.view(np.uint8).copy()).to(dev) for x in (b.seal, b.open))
+    d_pt, d_aad = torch.from_numpy(pt.copy()).to(dev), torch.from_numpy(aad.copy()).to(dev)
+    d_out = torch.zeros(b.sealed_bytes, dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(2):  # the second launch reuses the scratch (its counters back at zero)
+        pa.seal_batch(ks, d_seal.data_ptr(), n, d_pt.data_ptr(), d_aad.data_ptr(), d_out.data_ptr(), s)
+    torch.cuda.synchronize()
+    want = np.zeros(b.sealed_bytes, np.uint8)
+    ref.run_batch(True, np.frombuffer(key, np.uint8), np.frombuffer(iv, np.uint8), key_size, b.seal, pt, aad, want, nthreads=8)
+    got = d_out.cpu().numpy()
+    for i in range(n):  # per record, so that a failure names it
+        o, ln = int(b.seal["out_off"][i]), int(lens[i])
+        assert np.array_equal(got[o:o + ln + 16], want[o:o + ln + 16]), (i, ln)
+    long_idx = int(np.argmax(lens))
+    bad = d_out.clone()
+    o = int(b.seal["out_off"][long_idx]) + int(lens[long_idx]) // 2
+    bad[o] ^= 1
+    d_back = torch.zeros(b.pt_bytes, dtype=torch.uint8, device=dev)
+    d_ok = torch.full((n,), 7, dtype=torch.uint8, device=dev)
+    pa.open_batch(ks, d_open.data_ptr(), n, bad.data_ptr(), d_aad.data_ptr(), d_back.data_ptr(), d_ok.data_ptr(), s)
+    torch.cuda.synchronize()
+    ok = d_ok.cpu().numpy()
+    assert ok[long_idx] == 0 and all(ok[i] == 1 for i in range(n) if i != long_idx), ok
+    back = d_back.cpu().numpy()
+    for i in range(n):
+        if i != long_idx:
+            io, ln = int(b.seal["in_off"][i]), int(lens[i])
+            assert np.array_equal(back[io:io + ln], pt[io:io + ln]), i
+    ks.free()

@@ -14,7 +14,7 @@ import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-CASES = [(10, 1 << 20), (64, 65536), (100, 16384), (256, 16384), (1000, 16384), (2000, 16384), (4096, 16384), (8192, 16384), (1000, 1200),
+CASES = [(10, 1 << 20), (2, 8 << 20), (40, 256 << 10), (64, 65536), (100, 16384), (256, 16384), (1000, 16384), (2000, 16384), (4096, 16384), (8192, 16384), (1000, 1200),
          (4096, 1200), (1000, 64)]
 
 
