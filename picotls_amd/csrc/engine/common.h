@@ -70,6 +70,13 @@ __device__ __forceinline__ u32 lane_here()
 #define ENGINE_FAST_STEP 1         // wave-uniform fast path for steps where every lane holds a full text block
 #endif
 
+#ifndef CT_TREE
+#define CT_TREE 1                  // constant-time mode: the lanes' last powers by a uniform-table tree after the loop
+#endif
+#ifndef CT_COMBINE_TREE
+#define CT_COMBINE_TREE 1          // constant-time mode: a record's unit partials combined by a uniform-table tree
+#endif
+
 #ifndef ALIGN_MIN_STEPS
 #define ALIGN_MIN_STEPS 64         // whole records of this many steps may take one more step to align their stores
 #endif

@@ -559,7 +559,7 @@ __device__ __attribute__((noinline)) void spread_pieces(BatchArgs args, u32 w, u
             u32x4 acc;
             u32 okw;
             gcm_segment<NR, OPEN, 1, 0, CT>(args, lds, rk, iv0, iv1, iv2, r, valid, m_lo, m_hi, j, laneoff, tsel_horner, acc,
-                                            false, okw, false);
+                                            false, okw, false, CLDS_PART + 16u * uu);
             if (valid && j == G - 1)  // (the record's last unit includes E(K, J0), gcm_segment)
                 s_part[uu] = acc;
         }
@@ -620,6 +620,39 @@ __device__ __attribute__((noinline)) void spread_pieces(BatchArgs args, u32 w, u
 // EXT (FRAME 0 only): 0 = plain; 1 = a spread launch (a small one-key batch, spread_pieces); 2 = seal with
 // header-protection masks (seal_batch_hp). Separate instantiations: the calls these add (spread_pieces, hp_masks_pass)
 // cost the plain kernels' loops registers (16 KiB seal -1.2 % with both compiled into one kernel).
+// Constant-time combine of a record's unc unit partials p[0..unc) (GHASH = sum_i p_i M^(unc-1-i), M the unit power in
+// table 8) by the G lanes of one group: blocks of 8 partials from the front (the first one short, right-aligned on the
+// lanes), each summed by a butterfly in which level k pairs lane l (bit k clear) with lane l + k as v_l M^k + v_(l+k)
+// (tables 8, 4, 5: M, M^2, M^4; every lane the same table), the blocks joined by Horner with M^8 (table 6). ceil(log2
+// unc) products instead of unc - 1 chained ones for unc <= 8. Lane G - 1 holds the result.
+__device__ __noinline__ u32x4 ct_combine_tree(const lds_u8 *lds, const lds_u32x4 *p, u32 unc, u32 j)
+{
+    const u32 nblk = (unc + 7) >> 3, c0 = unc - 8 * (nblk - 1);
+    u32x4 g = {0, 0, 0, 0};
+    for (u32 b = 0; b < nblk; ++b) {
+        const int i = (int)j - 8 + (int)c0 + 8 * (int)b;
+        u32x4 v = i >= 0 ? u32x4(p[i]) : u32x4{0, 0, 0, 0};
+        const u32 lv = b != 0 || c0 > 4 ? 3u : c0 > 2 ? 2u : c0 > 1 ? 1u : 0u;
+        for (u32 l = 0; l < lv; ++l) {
+            const u32 k = 1u << l;
+            const u32x4 y = gmul_tab(lds, v, 0x10000u + (l == 0 ? 8u : 3u + l) * GHASH_TABLE_BYTES);
+            const bool hi = (j & k) != 0;
+            const u32x4 send = hi ? v : y;
+            u32x4 recv;
+            // partner lane l ^ k: quad_perm [1,0,3,2], [2,3,0,1]; for k = 4 row_half_mirror (lane 7 - l), which holds
+            // the same value as lane l ^ 4 once levels 1 and 2 made each quad uniform
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                recv[c] = k == 1   ? (u32)__builtin_amdgcn_update_dpp(0, (int)send[c], 0xB1, 0xF, 0xF, false)
+                          : k == 2 ? (u32)__builtin_amdgcn_update_dpp(0, (int)send[c], 0x4E, 0xF, 0xF, false)
+                                   : (u32)__builtin_amdgcn_update_dpp(0, (int)send[c], 0x141, 0xF, 0xF, false);
+            v = hi ? (recv ^ v) : (y ^ recv);
+        }
+        g = b == 0 ? v : (gmul_tab(lds, g, 0x10000u + 6u * GHASH_TABLE_BYTES) ^ v);
+    }
+    return g;
+}
+
 template <int NR, bool OPEN, int FRAME, bool CT = false, int EXT = 0>
 __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGINE_WAVES_PER_SIMD, ENGINE_WAVES_PER_SIMD))) void gcm_chunked_kernel(BatchArgs args)
 {
@@ -694,7 +727,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     const bool early_combine = early && args.unit_log2 < CHUNK_LOG2;
     if (early && wave >= EARLY_GHASH_WAVE) {
         build_ghash_tables(lds, args.keys, early_combine ? 9u : 8u, fixed_usrc, 0, EARLY_GHASH_WAVE * 64,
-                           ENGINE_WG - EARLY_GHASH_WAVE * 64);
+                           ENGINE_WG - EARLY_GHASH_WAVE * 64, CT && CT_COMBINE_TREE);
     } else if (wave == 0) {
         if (beg < end)
             scan_run<OPEN, FRAME, true, EXT>(args, recs, beg, end, (lds_u32 *)(lds + CLDS_RUN0));
@@ -762,8 +795,10 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         typedef __attribute__((address_space(3))) const KeyEntry lds_key_t;
         lds_key_t *key = (lds_key_t *)(rs + RUN_KEY_OFF);  // staged by the scanner
         if (key_idx != loaded_key || (!whole && usrc != loaded_usrc)) {
-            // H^1..H^8 and the unit combine power (only the latter when just the unit length changed)
-            build_ghash_tables(lds, key, 9, usrc, key_idx != loaded_key ? 0u : 8u);
+            // H^1..H^8 and the unit combine power (only the latter when just the unit length changed; constant-time
+            // mode: its powers in tables 4..6 too)
+            constexpr bool CTT = CT && CT_COMBINE_TREE;
+            build_ghash_tables(lds, key, 9, usrc, key_idx != loaded_key ? 0u : CTT ? 4u : 8u, 0, 0, CTT);
             __syncthreads();
             loaded_key = key_idx;
             loaded_usrc = usrc;
@@ -858,8 +893,11 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 }
                 if (!live)
                     m_lo = m_hi = 0;
+                // (constant-time mode: E(K, J0) waits in the slot of the record's last unit partial, or of the group
+                // in a whole-record run, which has no partials)
+                const u32 ekslot = CLDS_PART + 16u * (whole ? threadIdx.x / G : first + unc - 1);
                 gcm_segment<NR, OPEN, 1, FRAME, CT>(args, lds, rk, iv0, iv1, iv2, r, live, m_lo, m_hi, j, laneoff, tsel_horner, acc,
-                                                    unc == 1, okw, whole);
+                                                    unc == 1, okw, whole, ekslot);
             }
             // from here on everything is read again (run state, descriptor), not carried across the segment
             asm volatile("" ::: "memory");
@@ -887,12 +925,17 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                     // (whole group)
                     // (CT: each lane forms the whole product from the same table rows, instead of a share of it from
                     // its own window rows)
-                    u32x4 g = s_part[first];
-                    for (u32 i = 1; i < unc; ++i) {
-                        g = CT || COMBINE_TAB ? gmul_tab(lds, g, tsel_chunk) : gmul_group(lds, g, tsel_chunk, j);
-                        for (u32 t = 1; t < mul; ++t)  // huge records only
+                    u32x4 g;
+                    if (CT && CT_COMBINE_TREE && mul == 1) {
+                        g = ct_combine_tree(lds, s_part + first, unc, j);
+                    } else {
+                        g = s_part[first];
+                        for (u32 i = 1; i < unc; ++i) {
                             g = CT || COMBINE_TAB ? gmul_tab(lds, g, tsel_chunk) : gmul_group(lds, g, tsel_chunk, j);
-                        g ^= s_part[first + i];
+                            for (u32 t = 1; t < mul; ++t)  // huge records only
+                                g = CT || COMBINE_TAB ? gmul_tab(lds, g, tsel_chunk) : gmul_group(lds, g, tsel_chunk, j);
+                            g ^= s_part[first + i];
+                        }
                     }
                     const u32x4 tag = g;
                     if (j != G - 1) {

@@ -89,14 +89,24 @@ __device__ void build_aes_tables(lds_u8 *lds, u32 skip = 0, u32 end = 0)
 // order, and entry n ^ c = e(n) ^ e(c): at store n a lane writes slot n ^ (p mod 16), spreading a wave's 16-byte stores
 // over the bank groups. A few hundred VALU operations per thread: the build is a small part of a launch of one record.
 // Threads [tid0, tid0 + nthr) take part (nthr 0: the whole workgroup).
+// ct (the chunked kernel's constant-time mode, CT_COMBINE_TREE): tables 4, 5, 6 hold M^2, M^4, M^8 for the combine
+// power M = key->h[src8] (the elements after it in the chain H^8, H^16, ..., H^1024: [7], [9..15]; src8 8 is H^128 = [12])
+__device__ __forceinline__ u32 ct_chain_elem(u32 src8, u32 k)
+{
+    const u32 pos = src8 == 7 ? 0u : src8 == 8 ? 4u : src8 - 8u;
+    return 8u + pos + k;
+}
+
 template <typename KeyPtr>  // a KeyEntry in global memory, or its copy staged in LDS (the chunked kernel)
 __device__ void build_ghash_tables(lds_u8 *lds, KeyPtr key, u32 ntables = ENGINE_G, u32 src8 = 8, u32 first = 0, u32 tid0 = 0,
-                                   u32 nthr = 0)
+                                   u32 nthr = 0, bool ct = false)
 {
     const u32 stride = nthr != 0 ? nthr : blockDim.x;
     for (u32 idx = first * 32 + threadIdx.x - tid0; idx < ntables * 32; idx += stride) {
         const u32 t = idx >> 5, p = idx & 31;
-        const auto *h = key->h[t == 8 ? src8 : t];  // table 8: the unit combine power (chunked kernel)
+        // table 8: the unit combine power (chunked kernel)
+        const u32 el = t == 8 ? src8 : ct && t >= 4 && t <= 6 ? ct_chain_elem(src8, t - 3) : t;
+        const auto *h = key->h[el];
         u32 b0 = bswap32(h[0]), b1 = bswap32(h[1]), b2 = bswap32(h[2]), b3 = bswap32(h[3]);
         for (u32 k = 0; k < (p >> 3); ++k)
             gf_mulxs_be(b0, b1, b2, b3, 32);

@@ -10,7 +10,8 @@
 // sum(X_i * H^(end - i)), plus E(K, J0) when the segment holds the record's length block: the length lane (lane
 // (N - 1) mod G) encrypts J0 in that step and XORs it into its accumulator after its last multiply (the length block is
 // the last stream position, H^0 in every later combine), so a finished record's GHASH sum is its tag, and E(K, J0)
-// need not stay live through the loop (it was spilled to scratch once per segment). Invalid groups pass m_lo == m_hi. With finish (a whole record), a seal writes the tag and an open
+// need not stay live through the loop (it was spilled to scratch once per segment); with CT only the length lane's
+// partial includes it. Invalid groups pass m_lo == m_hi. With finish (a whole record), a seal writes the tag and an open
 // returns the tag check in okw on the length lane (1 = verified, 0 = not; 2 on every other lane and without finish):
 // the caller stores the ok byte, so the record's batch index need not stay live through the segment.
 //
@@ -22,15 +23,18 @@
 // lanes past the length block in the last step are idle, and each lane's last position p multiplies by H^(N - p), 1..G.
 //
 // CT (constant-time LDS access): a lane's last multiply by its own power H^e, from its own table, reads another table
-// row than the lanes beside it, so its bank conflicts depend on the data (profiles/r2_ct_counters.txt). With CT, a step
-// in which any lane of the wave takes its last multiply runs four multiplies that every lane takes from the same table
-// (H^8, then H^4, H^2, H^1 on the bits of e, each kept or not per lane): every LDS access of the kernel then has a
-// conflict pattern that depends on the record layout only.
+// row than the lanes beside it, so its bank conflicts depend on the data (profiles/r2_ct_counters.txt). With CT
+// (CT_TREE, round 3), every step multiplies by the uniform Horner table, a lane's last position stays unmultiplied, and
+// after the loop a butterfly over the group's lanes applies the powers H^e (three levels with the tables H, H^2, H^4,
+// then H once more: four uniform-table multiplies per segment). E(K, J0) then waits in an LDS slot of the caller's
+// (ekslot) until the tree is done, and is added on the length lane only (lane jl: the lane the tag or the unit partial
+// is taken from). The round-2 form (CT_TREE 0) ran four multiplies, H^8, H^4, H^2, H^1 kept on the bits of e, in every
+// step in which some lane of the wave was at its last position (two or more steps per segment).
 template <int NR, bool OPEN, int NB, int FRAME = 0, bool CT = false>
 __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 *lds, const u32 (&rk)[NR + 1][4], u32 iv0,
                                             u32 iv1, u32 iv2, const ptls_mi355x_record_t &r, bool valid, u32 m_lo,
                                             u32 m_hi, u32 j, u32 laneoff, u32 tsel_horner, u32x4 &acc, bool finish,
-                                            u32 &okw, bool aligned)
+                                            u32 &okw, bool aligned, u32 ekslot = 0)
 {
     constexpr int G = ENGINE_G;
     constexpr bool SEAL_FRAME = FRAME == 1 && !OPEN, OPEN_FRAME = FRAME == 1 && OPEN, TLS12 = FRAME == 2;
@@ -195,7 +199,10 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             X[1] = bswap32((u32)abits);
             X[2] = bswap32((u32)(cbits >> 32));
             X[3] = bswap32((u32)cbits);
-            ek0 = ks;
+            if (CT && CT_TREE)  // (kept in LDS until the tree: live through the loop, it was spilled to scratch)
+                *(lds_u32x4 *)(const_cast<lds_u8 *>(lds) + ekslot) = ks;
+            else
+                ek0 = ks;
         }
         return X;
     };
@@ -252,7 +259,14 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         __builtin_amdgcn_sched_barrier(0);
         const bool last_here = (int)m0 == m_last;
         u32x4 prod;
-        if (CT && __any(last_here)) {
+        if (CT && CT_TREE) {
+            // every lane multiplies by H^8, the uniform Horner table; a lane's last position stays unmultiplied and
+            // takes its power H^e_last in the tree after the loop
+            const u32x4 t = acc ^ X;
+            prod = gmul_tab(lds, t, tsel_horner);
+            if (last_here)
+                prod = t;
+        } else if (CT && __any(last_here)) {
             // H^8 (the Horner step, and a last power of 8), then H^4, H^2, H^1 kept on the bits of e_last; one
             // multiply site in a loop, so the branch costs no more registers than a plain step
             u32x4 t = acc ^ X;
@@ -276,11 +290,38 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         __builtin_amdgcn_sched_barrier(0);
     }
 
-    // XOR over the G lanes of the group
     static_assert(G == 8, "dpp_xor8 reduces groups of 8 lanes");
+    if constexpr (CT && CT_TREE) {
+        // sum over the group of a_l H^(e_l) (a_l: lane l's partial with its last position unmultiplied, e_l in 1..8 a
+        // permutation over the lanes), as a butterfly over the ranks t = 8 - e: level k pairs rank t (bit k clear) with
+        // rank t + k as v_t H^k + v_(t+k); every lane multiplies by the same table (H, H^2, H^4, then H once more) and
+        // takes its partner's product or value through the crossbar. Lane l holds rank (l - rot) mod 8.
+        const u32 lane = lane_here();
+        const u32 rank = valid ? (u32)G - e_last : j;
+        const u32 rot = (j - rank) & (G - 1);
+        u32x4 v = acc;
+#pragma unroll 1
+        for (u32 lv = 0; lv < 3; ++lv) {
+            const u32 k = 1u << lv;
+            const u32x4 y = gmul_tab(lds, v, 0x10000u + (k - 1u) * GHASH_TABLE_BYTES);  // H^k
+            const bool hi = (rank & k) != 0;
+            const u32x4 send = hi ? v : y;
+            const int src = (int)(((lane & ~(u32)(G - 1)) | (((rank ^ k) + rot) & (G - 1))) * 4);
+            u32x4 recv;
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
-        acc[c] = dpp_xor8(acc[c]);
+            for (int c = 0; c < 4; ++c)
+                recv[c] = (u32)__builtin_amdgcn_ds_bpermute(src, (int)send[c]);
+            v = hi ? (recv ^ v) : (y ^ recv);
+        }
+        acc = gmul_tab(lds, v, 0x10000u);  // * H
+        if (valid && m_hi * G >= N && j == jl)  // the segment holds the length block: E(K, J0), on its lane
+            acc ^= u32x4(*(const lds_u32x4 *)(lds + ekslot));
+    } else {
+        // XOR over the G lanes of the group
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            acc[c] = dpp_xor8(acc[c]);
+    }
     // whole record (finish): tag = GHASH ^ E(K, J0), written after the ciphertext (seal) or compared with the
     // received one (open)
     okw = 2;

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         u32x4 acc;
         u32 okw;
         gcm_segment<NR, OPEN, 1, 0, CT>(args, lds, rk, iv0, iv1, iv2, r, valid, m_lo, m_hi, j, laneoff, tsel_horner, acc,
-                                        false, okw, false);
+                                        false, okw, false, LDS_BYTES + GHASH_TABLE_BYTES + 16u * uu);
         if (valid && j == G - 1)  // (the record's last unit includes E(K, J0), gcm_segment)
             s_part[uu] = acc;
     }
