@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-record seals of 16 B and 1200 B (300 each) for a kernel trace of the per-record path (tools/gpu_latprof.sh)."""
+"""Per-record seals of 16 B and 1200 B (300 each) for a kernel trace of the per-record path (tools/gpu_recipes.sh latprof)."""
 import os
 import sys
 
