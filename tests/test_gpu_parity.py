@@ -482,6 +482,67 @@ def test_hp_masks_vs_fusion_supp(ref, key_size, n, nkeys, sort_keys, schedule):
         assert masks[i].tobytes() == (bytes(16) if i == 7 else mask), i
 
 
+@pytest.mark.parametrize("in_place,nkeys", [(False, 1), (True, 1), (False, 30), (True, 30)])
+def test_hp_masks_edges_vs_fusion(ref, in_place, nkeys):
+    # seal_batch_hp with samples anywhere in the sealed record (its first byte, the middle, the last 16 bytes = the tag
+    # itself), records of one unit and of several (mixed lengths to 16 KiB: cut runs, the tag written by the unit
+    # combine), sealed in place (the masks' pass reads samples where the kernel read plaintext) and not, one key and
+    # per-connection keys, beside rejected descriptors (nothing written) and an out-of-range header-protection key (a
+    # zero mask)
+    rng = np.random.default_rng(77 + 2 * nkeys + in_place)
+    n = 700
+    lens = rng.integers(17, 16385, n)
+    lens[:100] = 1200
+    key_idx = np.sort(rng.integers(0, nkeys, n))
+    b = RecordBatch.build(lens, rng.integers(0, 30, n), seqs=rng.integers(0, 2**40, n, dtype=np.uint64), key_idx=key_idx)
+    key_size = 16
+    keys = np.frombuffer(rng.bytes(nkeys * key_size), np.uint8)
+    ivs = np.frombuffer(rng.bytes(nkeys * 12), np.uint8)
+    hp_keys = np.frombuffer(rng.bytes(nkeys * key_size), np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(max(b.aad_bytes, 1)), np.uint8)
+    recs = b.seal.copy()
+    if in_place:  # the plaintext sits where its ciphertext goes
+        arena = np.zeros(b.sealed_bytes, np.uint8)
+        for i in range(n):
+            io, oo, ln = int(recs["in_off"][i]), int(recs["out_off"][i]), int(lens[i])
+            arena[oo:oo + ln] = pt[io:io + ln]
+        recs["in_off"] = recs["out_off"]
+    off = rng.integers(0, lens + 1)  # sample start inside the sealed record: [0, len]
+    off[0], off[1], off[101] = 0, lens[1], lens[101]  # the first byte; the tag itself (one-unit and multi-unit records)
+    hp = np.zeros(n, dtype=pa.HP_DTYPE)
+    hp["sample_off"] = recs["out_off"] + off
+    hp["key_idx"] = key_idx
+    hp["key_idx"][7] = nkeys  # out-of-range header-protection key: a zero mask
+    rejected = (8, 300)
+    recs["key_idx"][8] = nkeys + 9  # rejected descriptors: nothing is written for them
+    recs["len"][300] = (1 << 30) + 1  # (over PTLS_MI355X_MAX_RECORD_LEN)
+    ks, hp_ks = pa.Keyset(keys, ivs, key_size), pa.Keyset(hp_keys, np.zeros(nkeys * 12, np.uint8), key_size)
+    d_recs, d_aad, d_hp = dev(recs), dev(aad), dev(hp)
+    d_masks = empty(16 * n, 0x5A)
+    if in_place:
+        d_in = d_out = dev(arena)
+    else:
+        d_in, d_out = dev(pt), empty(b.sealed_bytes, 0x33)
+    pa.seal_batch_hp(ks, d_recs.data_ptr(), n, d_in.data_ptr(), d_aad.data_ptr(), d_out.data_ptr(), hp_ks,
+                     d_hp.data_ptr(), d_masks.data_ptr())
+    torch.cuda.synchronize()
+    out, masks = d_out.cpu().numpy(), d_masks.cpu().numpy().reshape(-1, 16)
+    for i in range(n):
+        io, oo, ln = int(b.seal["in_off"][i]), int(b.seal["out_off"][i]), int(lens[i])
+        if i in rejected:  # untouched output
+            want = arena[oo:oo + ln + 16] if in_place else np.full(ln + 16, 0x33, np.uint8)
+            assert np.array_equal(out[oo:oo + ln + 16], want), i
+            continue
+        k = int(key_idx[i])
+        kb, ivb, hkb = (bytes(a[k * w:(k + 1) * w]) for a, w in ((keys, key_size), (ivs, 12), (hp_keys, key_size)))
+        ao, al = int(b.seal["aad_off"][i]), int(b.seal["aad_len"][i])
+        sealed, mask = ref.seal_with_hp(kb, ivb, int(b.seal["seq"][i]), bytes(aad[ao:ao + al]), bytes(pt[io:io + ln]), hkb,
+                                        int(off[i]))
+        assert out[oo:oo + ln + 16].tobytes() == sealed, i
+        assert masks[i].tobytes() == (bytes(16) if i == 7 else mask), i
+
+
 def _tls_header(n):
     return bytes([23, 3, 3, n >> 8, n & 0xFF])
 
