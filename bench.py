@@ -107,7 +107,9 @@ def make_rank(gpus: int):
     if one_device:
         local = 0
     torch.cuda.set_device(local)
-    return RankContext.from_env("gloo" if one_device else "nccl", device=torch.device("cuda", local))
+    # PTLS_BENCH_PROCESS_GROUP=1: join the process group even as the only rank (exercises the nccl branch on one GPU)
+    return RankContext.from_env("gloo" if one_device else "nccl", device=torch.device("cuda", local),
+                                always=os.environ.get("PTLS_BENCH_PROCESS_GROUP") == "1")
 
 
 def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool, schedule: str = "auto"):
@@ -612,7 +614,8 @@ def main():
         "config": {"workload": wl.name, "desc": wl.desc, "records_per_gpu": res["records"],
                    "record_len": wl.rec_len or "U[64,16384]", "aad_len": wl.aad_len,
                    "aead": f"AES-{8 * wl.key_size}-GCM", "keys": wl.nkeys,
-                   "parallelism": f"{R.world} independent per-GPU record shards, no data-path collective"},
+                   "parallelism": f"{R.world} independent per-GPU record shards, no data-path collective",
+                   "dist_backend": R.backend},
         "seal_GiBps": round(res["payload_bytes"] / seal_s / 2**30, 3),
         "open_GiBps": round(res["payload_bytes"] / open_s / 2**30, 3),
         "roofline": {"bound": "hbm", "kernel": f"{'gcm_batch_kernel' if args.schedule == 'lockstep' else 'gcm_chunked_kernel'}"

@@ -158,16 +158,8 @@ __device__ __forceinline__ unsigned long long stamp()
 #define PROF_ADD(i, x)
 #endif
 
-// A cut run takes the longest units that still give this many: half the workgroup's groups, or in a many-key batch
-// (round 3) one per group. Many-key batches of 16 records per key 583.4 -> 604.3 GiB/s with one per group; configs[3]
-// (64 per key) 772.3 -> 774.2 and random order 753.5 -> 752.7 (its runs keep 2 KiB units either way); 256 and 512 cost
-// 1.2 % / 12 % there (per-unit work); one-key small batches lose with it (1000 x 16 KiB 35.6 -> 41.0 us, 4096 x
-// 1200 B 20.6 -> 23.0 us), profiles/r3_unit_fill_ab.txt
 #ifndef RUN_FILL_UNITS
-#define RUN_FILL_UNITS (ENGINE_WG / ENGINE_G / 2)
-#endif
-#ifndef RUN_FILL_UNITS_MULTI
-#define RUN_FILL_UNITS_MULTI (ENGINE_WG / ENGINE_G)
+#define RUN_FILL_UNITS (ENGINE_WG / ENGINE_G / 2)  // a cut run takes the longest units that still give this many
 #endif
 #ifndef COMBINE_TAB
 #define COMBINE_TAB 0  // unit combine with gmul_tab (every lane the whole product, same table rows) in the default mode too
@@ -199,16 +191,15 @@ __device__ __forceinline__ unsigned long long stamp()
 // skips the sort for a lone record and ranks a run of at most 64 records directly; the scans in the run tails keep the plain loops, whose registers the unit loop
 // shares (the guarded form adds VGPR spills to the open kernel).
 // Unit length of a cut run (2^log2 steps, at most 2^cap) when the launch leaves it to the scan (args.unit_log2 ==
-// CHUNK_LOG2): the longest that still gives at least 64 units (half the workgroup's 128 groups; 128 in a many-key
-// batch, RUN_FILL_UNITS_MULTI; shorter units would not shorten the run, only add per-unit work), but long enough that
-// a record's unit combine chains at most 36 partials (a chain is serial, ~0.15 us a link; 36 admits a 16 KiB TLS
-// record, 129 steps, in 4-step units). Big
+// CHUNK_LOG2): the longest that still gives at least 64 units (half the workgroup's 128 groups; shorter units would
+// not shorten the run, only add per-unit work), but long enough that a record's unit combine chains at most 36
+// partials (a chain is serial, ~0.15 us a link; 36 admits a 16 KiB TLS record, 129 steps, in 4-step units). Big
 // batches keep 2 KiB units; a run of a few records -- a small batch -- is cut finer, so its records spread over the
 // waves. (A launch of one record passes its own length rule, single() in aesgcm_engine.hip.)
-__device__ __forceinline__ u32 run_unit_log2(u32 total_steps, u32 smax, u32 cap, u32 fill_units)
+__device__ __forceinline__ u32 run_unit_log2(u32 total_steps, u32 smax, u32 cap)
 {
     u32 fill = 0, chain = 0;
-    while (fill < cap && (total_steps >> (fill + 1)) >= fill_units)
+    while (fill < cap && (total_steps >> (fill + 1)) >= (u32)RUN_FILL_UNITS)
         ++fill;
     while (chain < cap && ((smax + (1u << chain) - 1) >> chain) > 36u)
         ++chain;
@@ -267,8 +258,7 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
             tot += q * 64 + lane < n ? steps[q] : 0u;
         const u32 tot_incl = wave_incl_sum(tot);
         if (log2 == CHUNK_LOG2)
-            log2 = run_unit_log2((u32)__builtin_amdgcn_readlane((int)tot_incl, 63), smax, CHUNK_LOG2,
-                                 args.multi_key ? (u32)RUN_FILL_UNITS_MULTI : (u32)RUN_FILL_UNITS);
+            log2 = run_unit_log2((u32)__builtin_amdgcn_readlane((int)tot_incl, 63), smax, CHUNK_LOG2);
         const u32 ustep = 1u << log2;
 #pragma unroll
         for (u32 q = 0; q < Q; ++q) {

@@ -35,12 +35,15 @@ class RankContext:
     device: object = None
 
     @classmethod
-    def from_env(cls, backend: str = "nccl", device=None) -> "RankContext":
+    def from_env(cls, backend: str = "nccl", device=None, always: bool = False) -> "RankContext":
+        """The rank of this process (torch.distributed.run's environment). The process group (barrier, timing
+        reductions) is joined when there are several ranks, or with `always` also for one (a one-GPU box can run the
+        nccl branch that way)."""
         world = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
         local = int(os.environ.get("LOCAL_RANK", "0"))
         ctx = cls(rank, world, local, None, device)
-        if world > 1:
+        if world > 1 or always:
             import torch.distributed as dist
 
             if backend == "nccl":
@@ -69,6 +72,10 @@ class RankContext:
 
     def sum(self, x: float) -> float:
         return self._reduce(x, None if self.dist is None else self.dist.ReduceOp.SUM)
+
+    @property
+    def backend(self):
+        return self.dist.get_backend() if self.dist is not None else None
 
     def close(self):
         if self.dist is not None:

@@ -51,3 +51,28 @@ def test_bench_single_gpu_line_has_shard1200_by_default():
     assert out["n_gpus"] == 1
     sh = out["extra"]["shard1200"]
     assert sh["scaling"] == "strong" and sh["n_gpus"] == 1 and sh["verified"]["roundtrip"] is True
+
+
+def test_bench_nccl_process_group_on_one_gpu():
+    """The nccl branch of the rank setup (RankContext.from_env: init_process_group("nccl", device_id), the barriers and
+    the device-side max / sum reductions of the timings), which the 8-GPU driver run takes: one rank under
+    torch.distributed.run, made to join its process group (PTLS_BENCH_PROCESS_GROUP=1; two nccl ranks cannot share
+    one GPU)."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", PTLS_BENCH_PROCESS_GROUP="1")
+    env.pop("PTLS_BENCH_ONE_DEVICE", None)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
+                        "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup",
+                        "1", "--records", "1024", "--extra", "shard1200", "--no-cpu-baseline"], capture_output=True,
+                       text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert out["config"]["dist_backend"] == "nccl"
+    assert out["n_gpus"] == 1 and out["verified"]["roundtrip"] is True
+    sh = out["extra"]["shard1200"]
+    assert sh["verified"]["roundtrip"] is True and sh["records_total"] == 1024 * 16384 // 1200
