@@ -161,6 +161,9 @@ __device__ __forceinline__ unsigned long long stamp()
 #ifndef RUN_FILL_UNITS
 #define RUN_FILL_UNITS (ENGINE_WG / ENGINE_G / 2)  // a cut run takes the longest units that still give this many
 #endif
+#ifndef RUN_MAX_CHAIN
+#define RUN_MAX_CHAIN 36  // longest unit-combine chain a cut run's unit length may give a record (run_unit_log2)
+#endif
 #ifndef COMBINE_TAB
 #define COMBINE_TAB 0  // unit combine with gmul_tab (every lane the whole product, same table rows) in the default mode too
 #endif
@@ -201,7 +204,7 @@ __device__ __forceinline__ u32 run_unit_log2(u32 total_steps, u32 smax, u32 cap)
     u32 fill = 0, chain = 0;
     while (fill < cap && (total_steps >> (fill + 1)) >= (u32)RUN_FILL_UNITS)
         ++fill;
-    while (chain < cap && ((smax + (1u << chain) - 1) >> chain) > 36u)
+    while (chain < cap && ((smax + (1u << chain) - 1) >> chain) > (u32)RUN_MAX_CHAIN)
         ++chain;
     return fill > chain ? fill : chain;
 }
