@@ -2,7 +2,7 @@
 """AES-GCM seal+open throughput of the MI355X record engine (BASELINE.json metric), device-resident.
 
     python bench.py [--gpus N --steps K --warmup W] [--workload tls16k]
-                    [--extra quic1200,mixed,mixedrand,shard1200,ptlsbench] [--no-cpu-baseline]
+                    [--extra quic1200,mixed,mixedrand,shard1200,ptlsbench] [--no-cpu-baseline] [--no-e2e]
 
 One step = seal the whole batch, then open the sealed batch again (one launch each), inputs already in HBM.
 value = (sum L sealed + sum L opened) over all ranks / max-over-ranks wall time of the K timed steps, in GiB/s
@@ -20,6 +20,9 @@ Also reported:
                 path, primary) and ptls_non_temporal_aes128gcm (the TLS path, secondary), median of reps with the
                 spread; t/ptlsbench.c's own loop for configs[0]. The same leg checks records sampled from every GPU leg
                 bit for bit against fusion (verified.fusion_spot_check).
+  e2e_host_buffers  (N = 1) the headline records starting and ending in pinned host memory (north_star): serial,
+                pipelined and in-place (kernels on the device-mapped host arenas) seal+open rates beside the PCIe link's
+                own rate (both directions busy); never `value`
   extra         the other BASELINE configs at full size: quic1200 (configs[2]), mixed / mixedrand (configs[3], keys
                 grouped by connection / in random order as SURVEY §8(d) writes it), ptlsbench (configs[0]: 1000-record
                 batches under t/ptlsbench.c's conventions, on the GPU; fusion beside it in cpu_baseline)
@@ -52,7 +55,9 @@ def parse():
     p.add_argument("--records", type=int, default=0, help="override record count (smaller runs)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=3.0, help="wall budget of each cpu_baseline leg")
-    p.add_argument("--e2e", action="store_true", help="also time pinned-host -> H2D -> seal -> D2H (DESIGN.md)")
+    p.add_argument("--e2e", dest="e2e", action="store_true", default=None,
+                   help="time records that start and end in pinned host memory (DESIGN.md); default: on for N = 1")
+    p.add_argument("--no-e2e", dest="e2e", action="store_false")
     p.add_argument("--e2e-chunks", type=int, default=256,
                    help="--e2e: chunks of the pipelined mode (16 MiB at the default 4 GiB: 34.4 GiB/s vs 31.6-31.8 with 64-16)")
     p.add_argument("--schedule", default="auto", choices=["auto", "lockstep", "chunked"],
@@ -666,7 +671,7 @@ def main():
                        "verified": {"roundtrip": r2.get("verified_roundtrip"), "fusion_spot_check": None}}
     if extra:
         out["extra"] = extra
-    if args.e2e:
+    if args.e2e or (args.e2e is None and R.world == 1 and not args.records):  # (N = 1 at full size: 12 GiB pinned)
         out["e2e_host_buffers"] = run_e2e(R, WORKLOADS[args.workload].scaled(min(wl.nrecs, max(1, (4 << 30) // (wl.rec_len or 8192)))), args.e2e_chunks,
                                           schedule=args.schedule)
     if R.rank == 0 and R.world == 1 and not args.no_cpu_baseline:
