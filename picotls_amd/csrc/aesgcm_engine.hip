@@ -881,8 +881,8 @@ static u64 deal_chunk(u64 nrecs, u64 grid)
 }
 
 // scratch of spread launches: per-record piece counters (SPREAD_MAX_RECS, zero between launches), then the pieces'
-// partials: at most one piece per spare workgroup, or (records longer than 2^10 units x their share) 2^19 / 2^10 = 512
-// per record (PTLS_MI355X_MAX_RECORD_LEN)
+// partials: at most one piece per spare workgroup, or (records longer than 2^10 units x their share) 2^23 steps /
+// SPREAD_UNIT_STEPS / 2^10 per record (PTLS_MI355X_MAX_RECORD_LEN)
 #define SPREAD_MAX_RECS 255
 #define SPREAD_CNT_BYTES ((size_t)256 * 4)
 
@@ -1008,7 +1008,11 @@ static int launch_span(const KeyEntry *key, int nr, bool ct, bool open, const pt
     return 0;
 }
 
-static size_t spread_bytes(int ncu) { return SPREAD_CNT_BYTES + 16 * ((size_t)ncu + (size_t)SPREAD_MAX_RECS * 513); }
+// (pieces of a record: at most its units / 2^10 + 1, 2^23 / SPREAD_UNIT_STEPS / 2^10 + 1 for the longest record)
+static size_t spread_bytes(int ncu)
+{
+    return SPREAD_CNT_BYTES + 16 * ((size_t)ncu + (size_t)SPREAD_MAX_RECS * (8192 / SPREAD_UNIT_STEPS + 1));
+}
 
 // the keyset's spread scratch for a launch on `s` (allocated and zeroed in stream order on first use); nullptr when the
 // batch cannot take the spread launch (spread_done records the use afterwards)

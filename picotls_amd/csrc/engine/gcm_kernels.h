@@ -460,12 +460,25 @@ __device__ __attribute__((noinline)) void hp_masks_pass(const ptls_mi355x_hp_t *
 // speed, lib/fusion.c:1018-1041,1141-1145). The chunked kernel gives a record to one workgroup; in a batch of a few
 // records a long one then runs on one CU (10 x 1 MiB: 10 CUs, 0.3 ms). For a one-key batch of fewer records than CUs
 // the launch takes one workgroup per CU: workgroup w < nrecs seals or opens record w unless it is long (spread_long),
-// and the other workgroups share the long records, each record cut into pieces of 2^e 16-step units counted from the
-// stream's end (as the per-record path's span kernels cut a lone record, span_kernels.h). A workgroup seals its piece's
-// units, one per 8-lane group, folds their partials into Q_s = sum_u P_(s 2^e + u) H^(128 u), stores it, and the piece
-// that completes a record evaluates GHASH = sum_s Q_s M^s, M = H^(128 2^e) (e squarings of H^128 from a window table it
-// builds), by Horner, and writes the tag or the ok byte.
+// and the other workgroups share the long records, each record cut into pieces of 2^e units of SPREAD_UNIT_STEPS steps
+// counted from the stream's end (as the per-record path's span kernels cut a lone record, span_kernels.h). A workgroup
+// seals its piece's units, one per 8-lane group, folds their partials into Q_s = sum_u P_(s 2^e + u) M_u^u (M_u =
+// H^(8 SPREAD_UNIT_STEPS)), stores it, and the piece that completes a record evaluates GHASH = sum_s Q_s M^s, M = M_u^(2^e)
+// (from the keyset's H^(2^m), squared further beyond H^1024, in a window table it builds), by Horner, and writes the tag
+// or the ok byte.
 #define SPREAD_PLAN_CTL 512  // plan words: [0, 256) first piece of record t, [256, 512) its e, [512] pieces in total
+// The pieces' unit length in steps (a power of two from 2 to CHUNK_STEPS): a small batch leaves most of each CU's groups
+// idle, so shorter units put more groups to work on fewer steps each, at more partials per piece (folded by eight
+// groups at once, below). 10 x 1 MiB: 16 steps 102 us, 8 steps 93, 4 steps 92, 2 steps 97; 2 x 8 MiB: 141 / 134 / 136 /
+// 146 us (profiles/r3_spread_unit_ab.txt)
+#ifndef SPREAD_UNIT_STEPS
+#define SPREAD_UNIT_STEPS 8
+#endif
+#define SPREAD_UNIT_LOG2 (__builtin_ctz(SPREAD_UNIT_STEPS))
+static_assert(SPREAD_UNIT_STEPS >= 2 && SPREAD_UNIT_STEPS <= CHUNK_STEPS &&
+              (SPREAD_UNIT_STEPS & (SPREAD_UNIT_STEPS - 1)) == 0, "spread unit length");
+// key element index of H^(2^m), 3 <= m <= 10 (KeyEntry::h: [7] = H^8, [9..15] = H^16 .. H^1024)
+__device__ __forceinline__ u32 key_pow2_idx(u32 m) { return m == 3 ? 7u : 5u + m; }
 
 template <int NR, bool OPEN, bool CT>
 __device__ __attribute__((noinline)) void spread_pieces(BatchArgs args, u32 w, u32 nspare)
@@ -488,7 +501,7 @@ __device__ __attribute__((noinline)) void spread_pieces(BatchArgs args, u32 w, u
             if (t < n) {
                 const ptls_mi355x_record_t r = args.recs[t];
                 if (spread_long(args, r))
-                    units[q] = (gcm_steps<OPEN, 0>(r) + CHUNK_STEPS - 1) / CHUNK_STEPS;
+                    units[q] = (gcm_steps<OPEN, 0>(r) + SPREAD_UNIT_STEPS - 1) / SPREAD_UNIT_STEPS;
             }
             tot += units[q];
         }
@@ -520,8 +533,9 @@ __device__ __attribute__((noinline)) void spread_pieces(BatchArgs args, u32 w, u
     const u32 P = __builtin_amdgcn_readfirstlane(plan[SPREAD_PLAN_CTL]);
     if (w >= P)
         return;  // nothing for this workgroup (a batch without long records: every spare one)
-    if (wave >= EARLY_GHASH_WAVE)  // H^1..H^8 and H^128 of key 0; the AES tables on the other waves
-        build_ghash_tables(lds, args.keys, 9, 8, 0, EARLY_GHASH_WAVE * 64, ENGINE_WG - EARLY_GHASH_WAVE * 64);
+    if (wave >= EARLY_GHASH_WAVE)  // H^1..H^8 and the unit power H^(8 SPREAD_UNIT_STEPS) of key 0; the AES tables on the other waves
+        build_ghash_tables(lds, args.keys, 9, SPREAD_UNIT_STEPS == CHUNK_STEPS ? 8u : key_pow2_idx(3 + SPREAD_UNIT_LOG2), 0,
+                           EARLY_GHASH_WAVE * 64, ENGINE_WG - EARLY_GHASH_WAVE * 64);
     else
         build_aes_tables(lds, 0, EARLY_GHASH_WAVE * 64);
     __syncthreads();
@@ -548,7 +562,7 @@ __device__ __attribute__((noinline)) void spread_pieces(BatchArgs args, u32 w, u
         const u32 t = __builtin_amdgcn_readfirstlane(lo), s = p - plan[t], e = plan[256 + t], pbase = plan[t];
         const u32 np_t = (t + 1 < n ? plan[t + 1] : P) - pbase;
         const ptls_mi355x_record_t r = args.recs[t];
-        const u32 steps = gcm_steps<OPEN, 0>(r), U = (steps + CHUNK_STEPS - 1) / CHUNK_STEPS;
+        const u32 steps = gcm_steps<OPEN, 0>(r), U = (steps + SPREAD_UNIT_STEPS - 1) / SPREAD_UNIT_STEPS;
         const u32 k0 = s << e, nu = min(U - k0, 1u << e);
         for (u32 uu0 = wave * 8; uu0 < nu; uu0 += ENGINE_WG / G) {
             const u32 lane = lane_here(), j = lane % G, uu = uu0 + lane / G, laneoff = (lane & 31) * 4;
@@ -556,8 +570,8 @@ __device__ __attribute__((noinline)) void spread_pieces(BatchArgs args, u32 w, u
             const u32 k = k0 + uu;
             u32 m_hi = 0, m_lo = 0;
             if (valid) {
-                m_hi = steps - k * CHUNK_STEPS;
-                m_lo = k + 1 == U ? 0u : m_hi - CHUNK_STEPS;
+                m_hi = steps - k * SPREAD_UNIT_STEPS;
+                m_lo = k + 1 == U ? 0u : m_hi - SPREAD_UNIT_STEPS;
             }
             u32x4 acc;
             u32 okw;
@@ -567,11 +581,42 @@ __device__ __attribute__((noinline)) void spread_pieces(BatchArgs args, u32 w, u
                 s_part[uu] = acc;
         }
         __syncthreads();
-        if (wave == 0) {  // Q_s by Horner from the piece's highest unit down (every lane of wave 0 holds it)
+        // Q_s = sum_u P_u M_u^u (M_u = H^(8 SPREAD_UNIT_STEPS), the table in slot 8). From 16 units, the eight groups of
+        // wave 0 fold L = 2^(e-3) units each (Horner with M_u) while wave 1 builds the table of M_u^L (from the keyset)
+        // after the partials, and the eight sums are then folded with it: L + 7 links instead of nu - 1.
+        const u32 mL = SPREAD_UNIT_LOG2 + e;  // M_u^L = H^(2^mL)
+        const bool split = e >= 4 && mL <= 10 && (16u << e) <= GHASH_TABLE_BYTES;
+        lds_u32x4 *s_sum = (lds_u32x4 *)(lds + CLDS_RUN1);  // the eight groups' sums
+        const u32 tsel_ml = CLDS_PART + GHASH_TABLE_BYTES;
+        if (split) {
+            if (wave == 1)
+                build_elem_table(lds, tsel_ml, u32x4{key->h[key_pow2_idx(mL)][0], key->h[key_pow2_idx(mL)][1],
+                                                     key->h[key_pow2_idx(mL)][2], key->h[key_pow2_idx(mL)][3]}, 64);
+            if (wave == 0) {
+                const u32 lane = lane_here(), c = lane / G, L = 1u << (e - 3), ulo = c * L, uhi = min(ulo + L, nu);
+                u32x4 g = {0, 0, 0, 0};
+                if (ulo < uhi) {
+                    g = s_part[uhi - 1];
+                    for (u32 i = uhi - 1; i-- > ulo;)
+                        g = (CT ? gmul_tab(lds, g, tsel_chunk) : gmul_group(lds, g, tsel_chunk, lane % G)) ^ s_part[i];
+                }
+                if (lane % G == 0)
+                    s_sum[c] = g;
+            }
+            __syncthreads();
+        }
+        if (wave == 0) {  // Q_s by Horner from the highest unit (or group sum) down (every lane of wave 0 holds it)
             const u32 lane = lane_here();
-            u32x4 g = s_part[nu - 1];
-            for (u32 i = nu - 1; i-- > 0;)
-                g = (CT ? gmul_tab(lds, g, tsel_chunk) : gmul_group(lds, g, tsel_chunk, lane % G)) ^ s_part[i];
+            u32x4 g;
+            if (split) {
+                g = s_sum[7];
+                for (u32 c = 7; c-- > 0;)
+                    g = (CT ? gmul_tab(lds, g, tsel_ml) : gmul_group(lds, g, tsel_ml, lane % G)) ^ s_sum[c];
+            } else {
+                g = s_part[nu - 1];
+                for (u32 i = nu - 1; i-- > 0;)
+                    g = (CT ? gmul_tab(lds, g, tsel_chunk) : gmul_group(lds, g, tsel_chunk, lane % G)) ^ s_part[i];
+            }
             if (lane == 0) {
                 args.spread_part[pbase + s] = g;
                 __threadfence();  // the partial is visible device-wide before the count that publishes it
@@ -579,15 +624,15 @@ __device__ __attribute__((noinline)) void spread_pieces(BatchArgs args, u32 w, u
             }
         }
         __syncthreads();
-        if (*s_flag) {  // this piece completed the record: GHASH = sum_s Q_s M^s, M = (H^128)^(2^e)
+        if (*s_flag) {  // this piece completed the record: GHASH = sum_s Q_s M^s, M = H^(8 SPREAD_UNIT_STEPS 2^e)
             __threadfence();
             lds_u32x4 *s_m = (lds_u32x4 *)(lds + CLDS_PART + GHASH_TABLE_BYTES);  // M (after the element table)
-            // H^(128 * 2^e) from the keyset for e <= 3 (h[12 + e]), else by squaring H^1024
-            const u32 hi = e <= 3 ? 12 + e : 15;
+            // M = H^(8 SPREAD_UNIT_STEPS 2^e) = H^(2^m) from the keyset for m <= 10, else by squaring H^1024
+            const u32 m = 3 + SPREAD_UNIT_LOG2 + e, hi = m <= 10 ? key_pow2_idx(m) : 15u;
             if (threadIdx.x == 0)
                 *s_m = u32x4{key->h[hi][0], key->h[hi][1], key->h[hi][2], key->h[hi][3]};
             __syncthreads();
-            for (u32 i = 3; i < e; ++i) {
+            for (u32 i = 10; i < m; ++i) {
                 build_elem_table(lds, CLDS_PART, *s_m);
                 __syncthreads();
                 const u32x4 sq = gmul_tab(lds, *s_m, CLDS_PART);

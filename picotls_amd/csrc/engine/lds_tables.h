@@ -138,11 +138,11 @@ __device__ void build_ghash_tables(lds_u8 *lds, KeyPtr key, u32 ntables = ENGINE
     }
 }
 
-// The 4-bit window table of one GHASH element at LDS offset `base` (a multiple of 256), by threads [0, 32): the same
-// construction as build_ghash_tables for an element given by value.
-__device__ __forceinline__ void build_elem_table(lds_u8 *lds, u32 base, u32x4 h)
+// The 4-bit window table of one GHASH element at LDS offset `base` (a multiple of 256), by threads [tid0, tid0 + 32):
+// the same construction as build_ghash_tables for an element given by value.
+__device__ __forceinline__ void build_elem_table(lds_u8 *lds, u32 base, u32x4 h, u32 tid0 = 0)
 {
-    const u32 p = threadIdx.x;
+    const u32 p = threadIdx.x - tid0;
     if (p >= 32)
         return;
     u32 b0 = bswap32(h[0]), b1 = bswap32(h[1]), b2 = bswap32(h[2]), b3 = bswap32(h[3]);
