@@ -446,7 +446,7 @@ struct st_ptls_mi355x_keyset_t {
     u32 *d_group;
     size_t group_cap;
     hipEvent_t group_ev;
-    // small one-key batches with long records (spread_pieces): the pieces' partials and per-record counters (zero
+    // small batches with long records (spread_pieces): the pieces' partials and per-record counters (zero
     // between launches), allocated on first use; spread_stream: the stream of the last launch that used them (a launch
     // on another stream waits for that one's use event, note_use)
     uint8_t *d_spread;
@@ -917,9 +917,9 @@ static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int sche
     if (a.aad == NULL)
         a.aad = a.in;
     // one persistent workgroup per CU. A batch with fewer records than CUs takes one workgroup per record, or (spread,
-    // a one-key batch: spread_pieces) one per CU, the workgroups beyond the records sharing its long records
+    // an unframed batch: spread_pieces) one per CU, the workgroups beyond the records sharing its long records
     u64 grid = (u64)ncu;
-    if (spread != nullptr && nkeys == 1 && frame == 0 && nrecs >= 2 && nrecs < (u64)ncu && nrecs <= SPREAD_MAX_RECS &&
+    if (spread != nullptr && frame == 0 && nrecs >= 2 && nrecs < (u64)ncu && nrecs <= SPREAD_MAX_RECS &&
         hpl == nullptr && one == nullptr && (ct || use_chunked(schedule))) {
         a.spread = 1;
         a.spread_cnt = (u32 *)spread;
@@ -1018,7 +1018,7 @@ static size_t spread_bytes(int ncu)
 // batch cannot take the spread launch (spread_done records the use afterwards)
 static uint8_t *spread_scratch(ptls_mi355x_keyset_t *ks, hipStream_t s, size_t nrecs, int frame)
 {
-    if (ks->nkeys != 1 || frame != 0 || nrecs < 2 || nrecs >= (size_t)ks->ds->ncu || nrecs > SPREAD_MAX_RECS ||
+    if (frame != 0 || nrecs < 2 || nrecs >= (size_t)ks->ds->ncu || nrecs > SPREAD_MAX_RECS ||
         !(ks->ct || use_chunked(ks->schedule)))
         return nullptr;
     std::lock_guard<std::mutex> lk(ks->mu);
@@ -1066,6 +1066,8 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
     const bool group = false;
 #endif
     int ret;
+    // small batches with long records: the spread scratch (taken before the group scratch: both lock ks->mu)
+    uint8_t *spread = hpl == nullptr ? spread_scratch(ks, s, nrecs, frame) : nullptr;
     if (group) {
         std::lock_guard<std::mutex> lk(ks->mu);
         // scratch: ctl[2] | counts[nkeys + 1] | perm[n] | (8-byte aligned) grouped descriptors[n] | balance tiles | bounds
@@ -1102,14 +1104,12 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
             balance_bounds_kernel<<<1, 1024, 0, s>>>(tiles, nrecs, grid, bounds);
         }
         ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, ks->ct, open, recs, nrecs, in, aad, out, ok, s,
-                         frame, CHUNK_LOG2, grouped, perm, ctl + 1, nullptr, nullptr, bounds, hpl);
+                         frame, CHUNK_LOG2, grouped, perm, ctl + 1, nullptr, nullptr, bounds, hpl, spread);
         if (ret == 0)
             HIP_TRY(hipEventRecord(ks->group_ev, s));
     } else {
-        uint8_t *spread = hpl == nullptr ? spread_scratch(ks, s, nrecs, frame) : nullptr;
         ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, ks->ct, open, recs, nrecs, in, aad, out, ok,
                          s, frame, CHUNK_LOG2, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, hpl, spread);
-        (void)spread;
     }
     if (ret != 0)
         return -1;

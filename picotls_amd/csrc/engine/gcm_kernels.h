@@ -456,10 +456,10 @@ __device__ __attribute__((noinline)) void hp_masks_pass(const ptls_mi355x_hp_t *
 }
 
 
-// ---- small one-key batches with long records (fusion takes records of any length at full
-// speed, lib/fusion.c:1018-1041,1141-1145). The chunked kernel gives a record to one workgroup; in a batch of a few
-// records a long one then runs on one CU (10 x 1 MiB: 10 CUs, 0.3 ms). For a one-key batch of fewer records than CUs
-// the launch takes one workgroup per CU: workgroup w < nrecs seals or opens record w unless it is long (spread_long),
+// ---- small batches with long records (fusion takes records of any length at full speed,
+// lib/fusion.c:1018-1041,1141-1145). The chunked kernel gives a record to one workgroup; in a batch of a few records a
+// long one then runs on one CU (10 x 1 MiB: 10 CUs, 0.3 ms). For an unframed batch of fewer records than CUs (one key
+// or many) the launch takes one workgroup per CU: workgroup w < nrecs seals or opens record w unless it is long (spread_long),
 // and the other workgroups share the long records, each record cut into pieces of 2^e units of SPREAD_UNIT_STEPS steps
 // counted from the stream's end (as the per-record path's span kernels cut a lone record, span_kernels.h). A workgroup
 // seals its piece's units, one per 8-lane group, folds their partials into Q_s = sum_u P_(s 2^e + u) M_u^u (M_u =
@@ -533,24 +533,8 @@ __device__ __attribute__((noinline)) void spread_pieces(BatchArgs args, u32 w, u
     const u32 P = __builtin_amdgcn_readfirstlane(plan[SPREAD_PLAN_CTL]);
     if (w >= P)
         return;  // nothing for this workgroup (a batch without long records: every spare one)
-    if (wave >= EARLY_GHASH_WAVE)  // H^1..H^8 and the unit power H^(8 SPREAD_UNIT_STEPS) of key 0; the AES tables on the other waves
-        build_ghash_tables(lds, args.keys, 9, SPREAD_UNIT_STEPS == CHUNK_STEPS ? 8u : key_pow2_idx(3 + SPREAD_UNIT_LOG2), 0,
-                           EARLY_GHASH_WAVE * 64, ENGINE_WG - EARLY_GHASH_WAVE * 64);
-    else
-        build_aes_tables(lds, 0, EARLY_GHASH_WAVE * 64);
-    __syncthreads();
-    const KeyEntry *key = args.keys;
-    u32 rk[NR + 1][4];
-#pragma unroll
-    for (int r = 0; r <= NR; ++r)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-            rk[r][c] = __builtin_amdgcn_readfirstlane(key->rk[r][c]);
-    const u32 iv0 = __builtin_amdgcn_readfirstlane(key->iv[0]), iv1 = __builtin_amdgcn_readfirstlane(key->iv[1]),
-              iv2 = __builtin_amdgcn_readfirstlane(key->iv[2]);
-    const u32 tsel_horner = 0x10000u + (u32)(G - 1) * GHASH_TABLE_BYTES, tsel_chunk = 0x10000u + 8u * GHASH_TABLE_BYTES;
-    for (u32 p = w; p < P; p += nspare) {
-        // the piece's record: the last t with plan[t] <= p (records without pieces share the next one's start)
+    // the piece's record: the last t with plan[t] <= p (records without pieces share the next one's start)
+    auto piece_record = [&](u32 p) -> u32 {
         u32 lo = 0, hi = n;
         while (hi - lo > 1) {
             const u32 mid = (lo + hi) >> 1;
@@ -559,9 +543,37 @@ __device__ __attribute__((noinline)) void spread_pieces(BatchArgs args, u32 w, u
             else
                 hi = mid;
         }
-        const u32 t = __builtin_amdgcn_readfirstlane(lo), s = p - plan[t], e = plan[256 + t], pbase = plan[t];
+        return __builtin_amdgcn_readfirstlane(lo);
+    };
+    // H^1..H^8 and the unit power H^(8 SPREAD_UNIT_STEPS) of the first piece's key on waves EARLY_GHASH_WAVE.., the AES
+    // tables on the other waves; a many-key batch rebuilds the GHASH tables when a later piece's key differs
+    const u32 src8 = SPREAD_UNIT_STEPS == CHUNK_STEPS ? 8u : key_pow2_idx(3 + SPREAD_UNIT_LOG2);
+    u32 loaded_key = args.multi_key ? args.recs[piece_record(w)].key_idx : 0u;
+    if (wave >= EARLY_GHASH_WAVE)
+        build_ghash_tables(lds, args.keys + loaded_key, 9, src8, 0, EARLY_GHASH_WAVE * 64, ENGINE_WG - EARLY_GHASH_WAVE * 64);
+    else
+        build_aes_tables(lds, 0, EARLY_GHASH_WAVE * 64);
+    __syncthreads();
+    const u32 tsel_horner = 0x10000u + (u32)(G - 1) * GHASH_TABLE_BYTES, tsel_chunk = 0x10000u + 8u * GHASH_TABLE_BYTES;
+    for (u32 p = w; p < P; p += nspare) {
+        const u32 t = piece_record(p), s = p - plan[t], e = plan[256 + t], pbase = plan[t];
         const u32 np_t = (t + 1 < n ? plan[t + 1] : P) - pbase;
         const ptls_mi355x_record_t r = args.recs[t];
+        const u32 kidx = args.multi_key ? __builtin_amdgcn_readfirstlane(r.key_idx) : 0u;  // (< nkeys: spread_long)
+        if (kidx != loaded_key) {
+            build_ghash_tables(lds, args.keys + kidx, 9, src8);  // (the previous piece's barrier freed the tables)
+            __syncthreads();
+            loaded_key = kidx;
+        }
+        const KeyEntry *key = args.keys + kidx;
+        u32 rk[NR + 1][4];
+#pragma unroll
+        for (int rr = 0; rr <= NR; ++rr)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                rk[rr][c] = __builtin_amdgcn_readfirstlane(key->rk[rr][c]);
+        const u32 iv0 = __builtin_amdgcn_readfirstlane(key->iv[0]), iv1 = __builtin_amdgcn_readfirstlane(key->iv[1]),
+                  iv2 = __builtin_amdgcn_readfirstlane(key->iv[2]);
         const u32 steps = gcm_steps<OPEN, 0>(r), U = (steps + SPREAD_UNIT_STEPS - 1) / SPREAD_UNIT_STEPS;
         const u32 k0 = s << e, nu = min(U - k0, 1u << e);
         for (u32 uu0 = wave * 8; uu0 < nu; uu0 += ENGINE_WG / G) {

@@ -407,12 +407,14 @@ def test_long_records_over_many_workgroups_vs_fusion(ref, key_size):
 
 
 @pytest.mark.parametrize("key_size,ct,case", [(16, False, "10x1MiB"), (32, False, "mixed"), (16, True, "mixed"),
-                                              (16, False, "threshold"), (32, True, "two_huge")])
+                                              (16, False, "threshold"), (32, True, "two_huge"), (16, False, "manykey"),
+                                              (32, True, "manykey")])
 def test_small_batch_long_records_spread_vs_fusion(ref, key_size, ct, case):
-    # a one-key batch of fewer records than CUs whose long records (>= 512 KiB) are shared by the spare workgroups
+    # a batch of fewer records than CUs whose long records (>= 512 KiB) are shared by the spare workgroups
     # (spread_pieces): every sealed record equals fusion's, opens verify, and a tampered long record is rejected while
-    # its neighbours still open
-    rng = np.random.default_rng({"10x1MiB": 1, "mixed": 2, "threshold": 3, "two_huge": 4}[case] + key_size)
+    # its neighbours still open. "manykey": records of 5 connections in random key order (the batch is grouped by key
+    # on the device, and the pieces of one workgroup may change keys)
+    rng = np.random.default_rng({"10x1MiB": 1, "mixed": 2, "threshold": 3, "two_huge": 4, "manykey": 5}[case] + key_size)
     if case == "10x1MiB":
         lens = np.full(10, 1 << 20)
     elif case == "mixed":
@@ -420,11 +422,16 @@ def test_small_batch_long_records_spread_vs_fusion(ref, key_size, ct, case):
         rng.shuffle(lens)
     elif case == "threshold":
         lens = np.array([(512 << 10) - 1, 512 << 10, (512 << 10) + 1, 16, 0, (512 << 10) + 15, 100000, 300000])
+    elif case == "manykey":
+        lens = np.concatenate([rng.integers(0, 5000, 16), rng.integers(512 << 10, 2 << 20, 8)])
+        rng.shuffle(lens)
     else:
         lens = np.array([5 << 20, 77, (9 << 20) + 3])
     n = len(lens)
-    b = RecordBatch.build(lens, rng.integers(0, 40, n), seqs=rng.integers(0, 2**62, n, dtype=np.uint64))
-    key, iv = rng.bytes(key_size), rng.bytes(12)
+    nkeys = 5 if case == "manykey" else 1
+    key_idx = rng.integers(0, nkeys, n) if nkeys > 1 else None
+    b = RecordBatch.build(lens, rng.integers(0, 40, n), seqs=rng.integers(0, 2**62, n, dtype=np.uint64), key_idx=key_idx)
+    key, iv = rng.bytes(key_size * nkeys), rng.bytes(12 * nkeys)
     ks = pa.Keyset(key, iv, key_size)
     ks.set_constant_time(ct)
     pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)

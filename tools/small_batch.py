@@ -33,6 +33,8 @@ def main():
     ap.add_argument("libs", nargs="*", default=["picotls_amd/_lib/libptls_mi355x.so"])
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--keys", type=int, default=1, help="connection keys (record i uses key i mod keys)")
+    ap.add_argument("--cases", default="", help="n:len,... instead of the default list")
     a = ap.parse_args()
 
     import torch
@@ -43,11 +45,13 @@ def main():
     dev = torch.device("cuda:0")
     s = torch.cuda.current_stream().cuda_stream
     rng = np.random.default_rng(3)
-    key, iv = np.frombuffer(rng.bytes(16), np.uint8), np.frombuffer(rng.bytes(12), np.uint8)
+    key, iv = np.frombuffer(rng.bytes(16 * a.keys), np.uint8), np.frombuffer(rng.bytes(12 * a.keys), np.uint8)
     libs = [(p, bind(p)) for p in a.libs]
-    kss = {p: ctypes.c_void_p(lib.ptls_mi355x_keyset_new(key.ctypes.data, iv.ctypes.data, 1, 16)) for p, lib in libs}
-    for n, ln in CASES:
-        b = RecordBatch.build(np.full(n, ln, np.uint64), 13, seqs=np.arange(n, dtype=np.uint64))
+    kss = {p: ctypes.c_void_p(lib.ptls_mi355x_keyset_new(key.ctypes.data, iv.ctypes.data, a.keys, 16)) for p, lib in libs}
+    cases = [tuple(int(x) for x in c.split(":")) for c in a.cases.split(",")] if a.cases else CASES
+    for n, ln in cases:
+        b = RecordBatch.build(np.full(n, ln, np.uint64), 13, seqs=np.arange(n, dtype=np.uint64),
+                              key_idx=np.arange(n) % a.keys)
         d_seal = torch.from_numpy(b.seal.view(np.uint8).copy()).to(dev)
         d_open = torch.from_numpy(b.open.view(np.uint8).copy()).to(dev)
         d_aad = torch.from_numpy(np.frombuffer(rng.bytes(b.aad_bytes), np.uint8).copy()).to(dev)
