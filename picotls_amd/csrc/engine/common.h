@@ -76,6 +76,9 @@ __device__ __forceinline__ u32 lane_here()
 #ifndef CT_COMBINE_TREE
 #define CT_COMBINE_TREE 1          // constant-time mode: a record's unit partials combined by a uniform-table tree
 #endif
+#ifndef SEG_COOP
+#define SEG_COOP 1                 // default mode: window-major power tables, the lanes' last powers by coop_last_powers
+#endif
 
 #ifndef ALIGN_MIN_STEPS
 #define ALIGN_MIN_STEPS 64         // whole records of this many steps may take one more step to align their stores
@@ -92,7 +95,8 @@ __device__ __forceinline__ u32 lane_here()
 #define LDS_AES_BYTES 65536        // Te0/Te2, 32-bank replicated
 #define GHASH_TABLE_BYTES 8192     // 32 windows x 16 entries x 16 B
 #define LDS_BYTES (LDS_AES_BYTES + ENGINE_G * GHASH_TABLE_BYTES)
-#define LDS_ALLOC (LDS_BYTES + 16)  // + scratch word for the key-run scan
+#define LDS_EKSLOT (LDS_BYTES + 16)  // lockstep kernel: E(K, J0) slots, one per 8-lane group (gcm_segment's ekslot)
+#define LDS_ALLOC (LDS_EKSLOT + 16 * (ENGINE_WG / ENGINE_G))  // + scratch word for the key-run scan, the E(K, J0) slots
 
 // Chunked schedule (many-key batches): records are cut into units of at most CHUNK_BLOCKS GHASH-stream blocks, and
 // the per-unit GHASH partials are recombined with H^CHUNK_BLOCKS (one more 8 KiB table, LDS table slot 8).

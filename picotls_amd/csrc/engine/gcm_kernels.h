@@ -50,7 +50,7 @@ __device__ __forceinline__ void process_group(const BatchArgs &args, const lds_u
     u32x4 acc;
     u32 okw;
     gcm_segment<NR, OPEN, NB>(args, lds, rk, iv0, iv1, iv2, r, valid, 0, K, j, laneoff, tsel_horner, acc, true, okw,
-                              true);
+                              true, LDS_EKSLOT + 16u * (threadIdx.x / ENGINE_G));
     if (OPEN && okw <= 1)
         args.ok[rec] = (uint8_t)okw;
 }
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         }
         if (key_idx != loaded_key) {
             __syncthreads();  // no wave still reads the previous key's tables
-            build_ghash_tables(lds, args.keys + key_idx);
+            build_ghash_tables(lds, args.keys + key_idx, ENGINE_G, 8, 0, 0, 0, false, SEG_COOP);
             __syncthreads();
             loaded_key = key_idx;
         }
@@ -163,9 +163,6 @@ __device__ __forceinline__ unsigned long long stamp()
 #endif
 #ifndef RUN_MAX_CHAIN
 #define RUN_MAX_CHAIN 36  // longest unit-combine chain a cut run's unit length may give a record (run_unit_log2)
-#endif
-#ifndef COMBINE_TAB
-#define COMBINE_TAB 0  // unit combine with gmul_tab (every lane the whole product, same table rows) in the default mode too
 #endif
 #ifndef EARLY_GHASH
 #define EARLY_GHASH 1
@@ -550,7 +547,8 @@ __device__ __attribute__((noinline)) void spread_pieces(BatchArgs args, u32 w, u
     const u32 src8 = SPREAD_UNIT_STEPS == CHUNK_STEPS ? 8u : key_pow2_idx(3 + SPREAD_UNIT_LOG2);
     u32 loaded_key = args.multi_key ? args.recs[piece_record(w)].key_idx : 0u;
     if (wave >= EARLY_GHASH_WAVE)
-        build_ghash_tables(lds, args.keys + loaded_key, 9, src8, 0, EARLY_GHASH_WAVE * 64, ENGINE_WG - EARLY_GHASH_WAVE * 64);
+        build_ghash_tables(lds, args.keys + loaded_key, 9, src8, 0, EARLY_GHASH_WAVE * 64, ENGINE_WG - EARLY_GHASH_WAVE * 64,
+                           false, !CT && SEG_COOP);
     else
         build_aes_tables(lds, 0, EARLY_GHASH_WAVE * 64);
     __syncthreads();
@@ -561,7 +559,7 @@ __device__ __attribute__((noinline)) void spread_pieces(BatchArgs args, u32 w, u
         const ptls_mi355x_record_t r = args.recs[t];
         const u32 kidx = args.multi_key ? __builtin_amdgcn_readfirstlane(r.key_idx) : 0u;  // (< nkeys: spread_long)
         if (kidx != loaded_key) {
-            build_ghash_tables(lds, args.keys + kidx, 9, src8);  // (the previous piece's barrier freed the tables)
+            build_ghash_tables(lds, args.keys + kidx, 9, src8, 0, 0, 0, false, !CT && SEG_COOP);  // (freed by the last barrier)
             __syncthreads();
             loaded_key = kidx;
         }
@@ -603,14 +601,14 @@ __device__ __attribute__((noinline)) void spread_pieces(BatchArgs args, u32 w, u
         if (split) {
             if (wave == 1)
                 build_elem_table(lds, tsel_ml, u32x4{key->h[key_pow2_idx(mL)][0], key->h[key_pow2_idx(mL)][1],
-                                                     key->h[key_pow2_idx(mL)][2], key->h[key_pow2_idx(mL)][3]}, 64);
+                                                     key->h[key_pow2_idx(mL)][2], key->h[key_pow2_idx(mL)][3]}, 64, !CT && SEG_COOP);
             if (wave == 0) {
                 const u32 lane = lane_here(), c = lane / G, L = 1u << (e - 3), ulo = c * L, uhi = min(ulo + L, nu);
                 u32x4 g = {0, 0, 0, 0};
                 if (ulo < uhi) {
                     g = s_part[uhi - 1];
                     for (u32 i = uhi - 1; i-- > ulo;)
-                        g = (CT ? gmul_tab(lds, g, tsel_chunk) : gmul_group(lds, g, tsel_chunk, lane % G)) ^ s_part[i];
+                        g = gmul_combine<CT>(lds, g, tsel_chunk, lane) ^ s_part[i];
                 }
                 if (lane % G == 0)
                     s_sum[c] = g;
@@ -623,11 +621,11 @@ __device__ __attribute__((noinline)) void spread_pieces(BatchArgs args, u32 w, u
             if (split) {
                 g = s_sum[7];
                 for (u32 c = 7; c-- > 0;)
-                    g = (CT ? gmul_tab(lds, g, tsel_ml) : gmul_group(lds, g, tsel_ml, lane % G)) ^ s_sum[c];
+                    g = gmul_combine<CT>(lds, g, tsel_ml, lane) ^ s_sum[c];
             } else {
                 g = s_part[nu - 1];
                 for (u32 i = nu - 1; i-- > 0;)
-                    g = (CT ? gmul_tab(lds, g, tsel_chunk) : gmul_group(lds, g, tsel_chunk, lane % G)) ^ s_part[i];
+                    g = gmul_combine<CT>(lds, g, tsel_chunk, lane) ^ s_part[i];
             }
             if (lane == 0) {
                 args.spread_part[pbase + s] = g;
@@ -787,7 +785,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     const bool early_combine = early && args.unit_log2 < CHUNK_LOG2;
     if (early && wave >= EARLY_GHASH_WAVE) {
         build_ghash_tables(lds, args.keys, early_combine ? 9u : 8u, fixed_usrc, 0, EARLY_GHASH_WAVE * 64,
-                           ENGINE_WG - EARLY_GHASH_WAVE * 64, CT && CT_COMBINE_TREE);
+                           ENGINE_WG - EARLY_GHASH_WAVE * 64, CT && CT_COMBINE_TREE, !CT && SEG_COOP);
     } else if (wave == 0) {
         if (beg < end)
             scan_run<OPEN, FRAME, true, EXT>(args, recs, beg, end, (lds_u32 *)(lds + CLDS_RUN0));
@@ -858,7 +856,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             // H^1..H^8 and the unit combine power (only the latter when just the unit length changed; constant-time
             // mode: its powers in tables 4..6 too)
             constexpr bool CTT = CT && CT_COMBINE_TREE;
-            build_ghash_tables(lds, key, 9, usrc, key_idx != loaded_key ? 0u : CTT ? 4u : 8u, 0, 0, CTT);
+            build_ghash_tables(lds, key, 9, usrc, key_idx != loaded_key ? 0u : CTT ? 4u : 8u, 0, 0, CTT, !CT && SEG_COOP);
             __syncthreads();
             loaded_key = key_idx;
             loaded_usrc = usrc;
@@ -991,9 +989,9 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                     } else {
                         g = s_part[first];
                         for (u32 i = 1; i < unc; ++i) {
-                            g = CT || COMBINE_TAB ? gmul_tab(lds, g, tsel_chunk) : gmul_group(lds, g, tsel_chunk, j);
+                            g = gmul_combine<CT>(lds, g, tsel_chunk, lane);
                             for (u32 t = 1; t < mul; ++t)  // huge records only
-                                g = CT || COMBINE_TAB ? gmul_tab(lds, g, tsel_chunk) : gmul_group(lds, g, tsel_chunk, j);
+                                g = gmul_combine<CT>(lds, g, tsel_chunk, lane);
                             g ^= s_part[first + i];
                         }
                     }

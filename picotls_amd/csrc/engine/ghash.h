@@ -51,4 +51,136 @@ __device__ __forceinline__ u32x4 gmul_group(const lds_u8 *, u32x4 a, u32 tsel, u
     return r;
 }
 
+// ------------------------------------------------------------------------------------------------ GHASH (window-major)
+//
+// gmul_tab's tables are nibble-major: entry (window w, nibble n) at T + w * 256 + n * 16, so a ds_read_b128's 16-byte
+// bank group is the nibble n. Lanes that read one table row at one window (the Horner step: every lane H^8, window by
+// window) then never conflict: equal nibbles read the same address, different ones different bank groups. Lanes that
+// read different rows in one instruction (each lane its own power, or its own windows of a shared product) conflict
+// whenever two of them meet the same nibble: a count that follows the data (profiles/r2_ct_evidence.txt).
+//
+// Window-major tables (WTAB: H^1..H^7 in slots 0..6 and the unit combine power in slot 8 in the default mode) put entry
+// (w, n) at T + (w >> 4) * 4096 + n * 256 + (w & 15) * 16: the bank group is (w & 15), whatever the data. Lane `lane`
+// of an 8-lane group (index y = lane & 7) handles the four windows 4y..4y+3 of the operand's halfword y, window
+// 4y + (i ^ f) at its i-th lookup, f = (lane >> 2) & 3. At every lookup the 16 lanes of a ds_read_b128 phase (16
+// distinct values of lane & 15) then read the 16 bank groups 4 (lane & 3) + (i ^ f) once each, for any tables and
+// operands: conflict-free by construction, so these multiplies take the same LDS cycles for every key and payload.
+// Within a halfword, window 4y + u sits at bit 4 (u ^ 1) (the high nibble of a byte is the earlier window).
+
+// lane's base for its lookups in a window-major table at T: T + (y >> 2) * 4096 + (y & 3) * 64 + f * 16 (then ^ i * 16)
+__device__ __forceinline__ u32 wtab_lane_base(u32 T, u32 lane)
+{
+    const u32 y = lane & 7, f = (lane >> 2) & 3;
+    return T + (y >> 2) * 4096u + (y & 3) * 64u + f * 16u;
+}
+
+// a * (window-major table at tsel) by the G = 8 lanes of a group together (every lane holds a; every lane gets the
+// product): gmul_group's work split, conflict-free (above). tsel is a multiple of 64.
+__device__ __forceinline__ u32x4 gmul_group_w(const lds_u8 *, u32x4 a, u32 tsel, u32 lane)
+{
+    static_assert(ENGINE_G == 8, "one halfword per lane");
+    const u32 y = lane & 7, f = (lane >> 2) & 3, q = y >> 1;
+    const u32 w = q == 0 ? a[0] : q == 1 ? a[1] : q == 2 ? a[2] : a[3];
+    const u32 W = wtab_lane_base(tsel, lane), sh = 4u * f + 16u * (y & 1);
+    u32x4 e[4];
+#pragma unroll
+    for (u32 i = 0; i < 4; ++i) {
+        const u32 n = (w >> (sh ^ (4u * (i ^ 1u)))) & 15u;
+        e[i] = lds_load128((n << 8) + (W ^ (i << 4)));
+    }
+    u32x4 r;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        r[c] = dpp_xor8(xor3(e[0][c], e[1][c], e[2][c]) ^ e[3][c]);
+    return r;
+}
+
+// A group's product by the unit combine power (table 8) or another combine element: constant-time mode gmul_tab (every
+// lane the whole product from the same rows of a nibble-major table), the default mode gmul_group_w (window-major)
+template <bool CT>
+__device__ __forceinline__ u32x4 gmul_combine(const lds_u8 *lds, u32x4 a, u32 tsel, u32 lane)
+{
+    if constexpr (CT)
+        return gmul_tab(lds, a, tsel);
+    else if constexpr (SEG_COOP)
+        return gmul_group_w(lds, a, tsel, lane);
+    else
+        return gmul_group(lds, a, tsel, lane % ENGINE_G);
+}
+
+// The default mode's segment end (gcm_segment): lane j of a group holds a_j, its partial with its last stream position
+// unmultiplied, and owes it the power H^(e_j), e_j = 8 - rank_j (the ranks are the lanes rotated by rot, uniform over the
+// group). Returns this lane's share of sum_j a_j H^(e_j - 1) (the caller XOR-reduces the group and multiplies the sum by
+// H): the value of rank r moves to lane r (ds_bpermute, only when some group of the wave has rot != 0), an 8 x 8
+// transpose of halfwords over the group (three DPP butterfly stages: lane y then holds halfword y of every rank, rank x
+// in halfword slot x), and lane y looks up its four windows of ranks 0..6 in the window-major tables H^7..H^1 (slots
+// 6..0; rank 7 owes H^0). With the group's product by H (gmul_group_w, 4 lookups) that is 32 conflict-free lookups per
+// lane, what the per-lane last multiply read from each lane's own table with data-dependent conflicts, and no lane
+// needs the Horner multiply in the segment's last step (gcm_segment skips it).
+__device__ __forceinline__ u32 dpp_xor4(u32 v)  // lane ^ 4 within 8 lanes: row_half_mirror (7 - l), then quad_perm [3,2,1,0]
+{
+    return (u32)__builtin_amdgcn_update_dpp(0, __builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false), 0x1B,
+                                            0xF, 0xF, false);
+}
+__device__ __forceinline__ u32x4 coop_last_powers(const lds_u8 *lds, u32x4 v, u32 lane, u32 rot)
+{
+    static_assert(ENGINE_G == 8, "halfword transpose over 8 lanes");
+    const u32 y = lane & 7;
+    if (__any(rot != 0)) {
+        const int src = (int)(((lane & ~7u) | ((y + rot) & 7u)) * 4u);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            v[c] = (u32)__builtin_amdgcn_ds_bpermute(src, (int)v[c]);
+    }
+    u32x4 sum = y == 7 ? v : u32x4{0, 0, 0, 0};  // rank 7: H^0
+    u32 d0 = v[0], d1 = v[1], d2 = v[2], d3 = v[3];
+    {  // slot bit 2 (dword pairs) with lane ^ 4
+        const bool b = (y & 4) != 0;
+        const u32 r0 = dpp_xor4(b ? d0 : d2), r1 = dpp_xor4(b ? d1 : d3);
+        d0 = b ? r0 : d0, d1 = b ? r1 : d1, d2 = b ? d2 : r0, d3 = b ? d3 : r1;
+    }
+    {  // slot bit 1 (dword within a pair) with lane ^ 2
+        const bool b = (y & 2) != 0;
+        const u32 r0 = (u32)__builtin_amdgcn_update_dpp(0, (int)(b ? d0 : d1), 0x4E, 0xF, 0xF, false);
+        const u32 r1 = (u32)__builtin_amdgcn_update_dpp(0, (int)(b ? d2 : d3), 0x4E, 0xF, 0xF, false);
+        d0 = b ? r0 : d0, d1 = b ? d1 : r0, d2 = b ? r1 : d2, d3 = b ? d3 : r1;
+    }
+    {  // slot bit 0 (halfword within a dword) with lane ^ 1: the sent halves packed two per dword
+        const bool b = (y & 1) != 0;
+        const u32 ps = b ? 0x05040100u : 0x07060302u;  // b: send the low halves, else the high ones
+        const u32 q0 = (u32)__builtin_amdgcn_update_dpp(0, (int)__builtin_amdgcn_perm(d1, d0, ps), 0xB1, 0xF, 0xF, false);
+        const u32 q1 = (u32)__builtin_amdgcn_update_dpp(0, (int)__builtin_amdgcn_perm(d3, d2, ps), 0xB1, 0xF, 0xF, false);
+        const u32 ua = b ? 0x03020504u : 0x05040100u, ub = b ? 0x03020706u : 0x07060100u;
+        d0 = __builtin_amdgcn_perm(q0, d0, ua), d1 = __builtin_amdgcn_perm(q0, d1, ub);
+        d2 = __builtin_amdgcn_perm(q1, d2, ua), d3 = __builtin_amdgcn_perm(q1, d3, ub);
+    }
+    // per lookup i: the nibble's shift, less 8 so that the nibble lands at bits 8..11 (even slots from the dword moved up
+    // by 8 bits: their nibbles sit at bits 0..15), and the lane's window base; opaque to the compiler, which otherwise
+    // re-derives them at every lookup (3-4 VALU operations per lookup instead of 2)
+    const u32 W = wtab_lane_base(LDS_AES_BYTES, lane), f4 = 4u * ((lane >> 2) & 3);
+    u32 Wi[4], she[4], sho[4];
+#pragma unroll
+    for (u32 i = 0; i < 4; ++i) {
+        Wi[i] = W ^ (i << 4);
+        she[i] = f4 ^ (4u * (i ^ 1u));  // (even slot, dword << 8): shift - 8 + 8
+        sho[i] = she[i] + 8u;           // (odd slot): 16 + shift - 8
+        asm volatile("" : "+v"(Wi[i]), "+v"(she[i]), "+v"(sho[i]));
+    }
+    const u32 dw[4] = {d0, d1, d2, d3};
+    const u32 dwe[4] = {d0 << 8, d1 << 8, d2 << 8, d3 << 8};
+#pragma unroll
+    for (u32 x = 0; x < 7; ++x) {
+        u32x4 e[4];
+#pragma unroll
+        for (u32 i = 0; i < 4; ++i) {
+            const u32 n8 = ((x & 1) ? dw[x >> 1] >> sho[i] : dwe[x >> 1] >> she[i]) & 0xf00u;
+            e[i] = lds_load128((n8 | Wi[i]) + (6u - x) * GHASH_TABLE_BYTES);  // H^(7 - x)
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            sum[c] = xor3(xor3(sum[c], e[0][c], e[1][c]), e[2][c], e[3][c]);
+    }
+    return sum;
+}
+
 #endif  // PTLS_MI355X_ENGINE_GHASH_H

@@ -82,6 +82,23 @@ __device__ void build_aes_tables(lds_u8 *lds, u32 skip = 0, u32 end = 0)
 #endif
 }
 
+// The 16 entries of one window (v: x^(4p)..x^(4p+3) times the element; ec: entry c), entry n at row + n * stride
+// (nibble-major 16, window-major 256), written in the order n ^ c
+template <bool WL>
+__device__ __forceinline__ void store_window(lds_u8 *row, const u32x4 (&v)[4], u32x4 ec, u32 c)
+{
+    constexpr u32 stride = WL ? 256 : 16;
+#pragma unroll
+    for (u32 n = 0; n < 16; ++n) {
+        u32x4 e = ec;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            if ((n >> (3 - m)) & 1u)
+                e ^= v[m];
+        *(lds_u32x4 *)(row + (n ^ c) * stride) = e;
+    }
+}
+
 // GHASH window tables of one key: table t (element key->h[t]), window p (x^(4p)..x^(4p+3)), entry n (4-bit value,
 // MSB = coefficient of x^(4p)) = sum over set bits of n of x^(4p+q) * h[t]. Thread (t, p) derives V_0 = x^(4p) h[t]
 // with at most three 32-bit steps and one step of 4 (p mod 8) bits, V_1..V_3 by single steps, and writes the window's
@@ -97,9 +114,11 @@ __device__ __forceinline__ u32 ct_chain_elem(u32 src8, u32 k)
     return 8u + pos + k;
 }
 
+// wl (the default mode): every table but 7 (H^8, the Horner table every lane reads at the same window) window-major
+// (ghash.h: entry (p, n) at (p >> 4) * 4096 + n * 256 + (p & 15) * 16 instead of p * 256 + n * 16).
 template <typename KeyPtr>  // a KeyEntry in global memory, or its copy staged in LDS (the chunked kernel)
 __device__ void build_ghash_tables(lds_u8 *lds, KeyPtr key, u32 ntables = ENGINE_G, u32 src8 = 8, u32 first = 0, u32 tid0 = 0,
-                                   u32 nthr = 0, bool ct = false)
+                                   u32 nthr = 0, bool ct = false, bool wl = false)
 {
     const u32 stride = nthr != 0 ? nthr : blockDim.x;
     for (u32 idx = first * 32 + threadIdx.x - tid0; idx < ntables * 32; idx += stride) {
@@ -125,22 +144,17 @@ __device__ void build_ghash_tables(lds_u8 *lds, KeyPtr key, u32 ntables = ENGINE
         for (int m = 0; m < 4; ++m)
             if ((c >> (3 - m)) & 1u)
                 ec ^= v[m];
-        lds_u32x4 *row = (lds_u32x4 *)(lds + LDS_AES_BYTES + t * GHASH_TABLE_BYTES + p * 256);
-#pragma unroll
-        for (u32 n = 0; n < 16; ++n) {
-            u32x4 e = ec;
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-                if ((n >> (3 - m)) & 1u)
-                    e ^= v[m];
-            row[n ^ c] = e;
-        }
+        const u32 T = LDS_AES_BYTES + t * GHASH_TABLE_BYTES;
+        if (wl && t != 7)
+            store_window<true>(lds + T + (p >> 4) * 4096 + (p & 15) * 16, v, ec, c);
+        else
+            store_window<false>(lds + T + p * 256, v, ec, c);
     }
 }
 
-// The 4-bit window table of one GHASH element at LDS offset `base` (a multiple of 256), by threads [tid0, tid0 + 32):
-// the same construction as build_ghash_tables for an element given by value.
-__device__ __forceinline__ void build_elem_table(lds_u8 *lds, u32 base, u32x4 h, u32 tid0 = 0)
+// The 4-bit window table of one GHASH element at LDS offset `base` (a multiple of 256; window-major with wl: a multiple
+// of 64), by threads [tid0, tid0 + 32): the same construction as build_ghash_tables for an element given by value.
+__device__ __forceinline__ void build_elem_table(lds_u8 *lds, u32 base, u32x4 h, u32 tid0 = 0, bool wl = false)
 {
     const u32 p = threadIdx.x - tid0;
     if (p >= 32)
@@ -163,16 +177,10 @@ __device__ __forceinline__ void build_elem_table(lds_u8 *lds, u32 base, u32x4 h,
     for (int m = 0; m < 4; ++m)
         if ((c >> (3 - m)) & 1u)
             ec ^= v[m];
-    lds_u32x4 *row = (lds_u32x4 *)(lds + base + p * 256);
-#pragma unroll
-    for (u32 n = 0; n < 16; ++n) {
-        u32x4 e = ec;
-#pragma unroll
-        for (int m = 0; m < 4; ++m)
-            if ((n >> (3 - m)) & 1u)
-                e ^= v[m];
-        row[n ^ c] = e;
-    }
+    if (wl)
+        store_window<true>(lds + base + (p >> 4) * 4096 + (p & 15) * 16, v, ec, c);
+    else
+        store_window<false>(lds + base + p * 256, v, ec, c);
 }
 
 #endif  // PTLS_MI355X_ENGINE_LDS_TABLES_H

@@ -37,6 +37,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                                             u32 &okw, bool aligned, u32 ekslot = 0)
 {
     constexpr int G = ENGINE_G;
+    constexpr bool COOP = !CT && SEG_COOP;  // the default mode's conflict-free segment end (coop_last_powers)
     constexpr bool SEAL_FRAME = FRAME == 1 && !OPEN, OPEN_FRAME = FRAME == 1 && OPEN, TLS12 = FRAME == 2;
     const u32 L = gcm_text_len<OPEN, FRAME>(r), A = gcm_aad_len<OPEN, FRAME>(r);
     // bytes of text readable at src (a framed seal reads len payload bytes; its last text byte is the content type)
@@ -199,7 +200,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             X[1] = bswap32((u32)abits);
             X[2] = bswap32((u32)(cbits >> 32));
             X[3] = bswap32((u32)cbits);
-            if (CT && CT_TREE)  // (kept in LDS until the tree: live through the loop, it was spilled to scratch)
+            if (COOP || (CT && CT_TREE))  // (kept in LDS until after the loop: live through it, it was spilled)
                 *(lds_u32x4 *)(const_cast<lds_u8 *>(lds) + ekslot) = ks;
             else
                 ek0 = ks;
@@ -282,6 +283,16 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             if (!last_here || e_last == (u32)G)
                 t = prod;
             prod = t;
+        } else if (COOP) {
+            // every lane multiplies by H^8, the uniform Horner table, except at its last position, which takes its
+            // power H^e_last after the loop (coop_last_powers); in the wave's last step no lane needs the multiply
+            const u32x4 t = acc ^ X;
+            prod = t;
+            if (s0 + 1 < Smax) {
+                prod = gmul_tab(lds, t, tsel_horner);
+                if (last_here)
+                    prod = t;
+            }
         } else {
             prod = gmul_tab(lds, acc ^ X, !CT && last_here ? tsel_last : tsel_horner);
         }
@@ -317,10 +328,18 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         if (valid && m_hi * G >= N && j == jl)  // the segment holds the length block: E(K, J0), on its lane
             acc ^= u32x4(*(const lds_u32x4 *)(lds + ekslot));
     } else {
+        if constexpr (COOP) {  // the lanes' powers H^(e_last - 1), conflict-free (ghash.h); ranks rotated by N mod 8
+            const u32 rank = valid ? (u32)G - e_last : j;
+            acc = coop_last_powers(lds, acc, lane_here(), (j - rank) & (G - 1));
+        }
         // XOR over the G lanes of the group
 #pragma unroll
         for (int c = 0; c < 4; ++c)
             acc[c] = dpp_xor8(acc[c]);
+        if constexpr (COOP)  // the group's sum times H (table 0, window-major)
+            acc = gmul_group_w(lds, acc, LDS_AES_BYTES, lane_here());
+        if (COOP && valid && m_hi * G >= N && j == jl)  // the segment holds the length block: E(K, J0), on its lane
+            acc ^= u32x4(*(const lds_u32x4 *)(lds + ekslot));
     }
     // whole record (finish): tag = GHASH ^ E(K, J0), written after the ciphertext (seal) or compared with the
     // received one (open)

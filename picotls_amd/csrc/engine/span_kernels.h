@@ -32,7 +32,8 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     const u32 wave = threadIdx.x >> 6;
     // AES tables on waves 0..10, H^1..H^8 and H^128 (slot 8) on waves 11..15
     if (wave >= EARLY_GHASH_WAVE)
-        build_ghash_tables(lds, args.keys, 9, 8, 0, EARLY_GHASH_WAVE * 64, ENGINE_WG - EARLY_GHASH_WAVE * 64);
+        build_ghash_tables(lds, args.keys, 9, 8, 0, EARLY_GHASH_WAVE * 64, ENGINE_WG - EARLY_GHASH_WAVE * 64, false,
+                           !CT && SEG_COOP);
     else
         build_aes_tables(lds, 0, EARLY_GHASH_WAVE * 64);
     __syncthreads();
@@ -71,7 +72,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         if (lane < G) {
             u32x4 g = s_part[n - 1];
             for (u32 i = n - 1; i-- > 0;)
-                g = (CT ? gmul_tab(lds, g, tsel_chunk) : gmul_group(lds, g, tsel_chunk, j)) ^ s_part[i];
+                g = gmul_combine<CT>(lds, g, tsel_chunk, lane) ^ s_part[i];
             if (j == 0)
                 part[blockIdx.x] = g;
         }
