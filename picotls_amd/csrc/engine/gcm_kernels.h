@@ -108,7 +108,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         }
         if (key_idx != loaded_key) {
             __syncthreads();  // no wave still reads the previous key's tables
-            build_ghash_tables(lds, args.keys + key_idx, ENGINE_G, 8, 0, 0, 0, false, SEG_COOP);
+            build_ghash_tables(lds, args.keys + key_idx, ENGINE_G, 8, 0, 0, 0, false, GHASH_WMASK(false));
             __syncthreads();
             loaded_key = key_idx;
         }
@@ -548,7 +548,7 @@ __device__ __attribute__((noinline)) void spread_pieces(BatchArgs args, u32 w, u
     u32 loaded_key = args.multi_key ? args.recs[piece_record(w)].key_idx : 0u;
     if (wave >= EARLY_GHASH_WAVE)
         build_ghash_tables(lds, args.keys + loaded_key, 9, src8, 0, EARLY_GHASH_WAVE * 64, ENGINE_WG - EARLY_GHASH_WAVE * 64,
-                           false, !CT && SEG_COOP);
+                           false, GHASH_WMASK(CT));
     else
         build_aes_tables(lds, 0, EARLY_GHASH_WAVE * 64);
     __syncthreads();
@@ -559,7 +559,7 @@ __device__ __attribute__((noinline)) void spread_pieces(BatchArgs args, u32 w, u
         const ptls_mi355x_record_t r = args.recs[t];
         const u32 kidx = args.multi_key ? __builtin_amdgcn_readfirstlane(r.key_idx) : 0u;  // (< nkeys: spread_long)
         if (kidx != loaded_key) {
-            build_ghash_tables(lds, args.keys + kidx, 9, src8, 0, 0, 0, false, !CT && SEG_COOP);  // (freed by the last barrier)
+            build_ghash_tables(lds, args.keys + kidx, 9, src8, 0, 0, 0, false, GHASH_WMASK(CT));  // (freed by the last barrier)
             __syncthreads();
             loaded_key = kidx;
         }
@@ -785,7 +785,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     const bool early_combine = early && args.unit_log2 < CHUNK_LOG2;
     if (early && wave >= EARLY_GHASH_WAVE) {
         build_ghash_tables(lds, args.keys, early_combine ? 9u : 8u, fixed_usrc, 0, EARLY_GHASH_WAVE * 64,
-                           ENGINE_WG - EARLY_GHASH_WAVE * 64, CT && CT_COMBINE_TREE, !CT && SEG_COOP);
+                           ENGINE_WG - EARLY_GHASH_WAVE * 64, CT && CT_COMB_TREE_ON, GHASH_WMASK(CT));
     } else if (wave == 0) {
         if (beg < end)
             scan_run<OPEN, FRAME, true, EXT>(args, recs, beg, end, (lds_u32 *)(lds + CLDS_RUN0));
@@ -855,8 +855,8 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         if (key_idx != loaded_key || (!whole && usrc != loaded_usrc)) {
             // H^1..H^8 and the unit combine power (only the latter when just the unit length changed; constant-time
             // mode: its powers in tables 4..6 too)
-            constexpr bool CTT = CT && CT_COMBINE_TREE;
-            build_ghash_tables(lds, key, 9, usrc, key_idx != loaded_key ? 0u : CTT ? 4u : 8u, 0, 0, CTT, !CT && SEG_COOP);
+            constexpr bool CTT = CT && CT_COMB_TREE_ON;
+            build_ghash_tables(lds, key, 9, usrc, key_idx != loaded_key ? 0u : CTT ? 4u : 8u, 0, 0, CTT, GHASH_WMASK(CT));
             __syncthreads();
             loaded_key = key_idx;
             loaded_usrc = usrc;
@@ -984,7 +984,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                     // (CT: each lane forms the whole product from the same table rows, instead of a share of it from
                     // its own window rows)
                     u32x4 g;
-                    if (CT && CT_COMBINE_TREE && mul == 1) {
+                    if (CT && CT_COMB_TREE_ON && mul == 1) {
                         g = ct_combine_tree(lds, s_part + first, unc, j);
                     } else {
                         g = s_part[first];

@@ -114,11 +114,11 @@ __device__ __forceinline__ u32 ct_chain_elem(u32 src8, u32 k)
     return 8u + pos + k;
 }
 
-// wl (the default mode): every table but 7 (H^8, the Horner table every lane reads at the same window) window-major
-// (ghash.h: entry (p, n) at (p >> 4) * 4096 + n * 256 + (p & 15) * 16 instead of p * 256 + n * 16).
+// wmask: bit t set = table t window-major (GHASH_WMASK; ghash.h: entry (p, n) at (p >> 4) * 4096 + n * 256 + (p & 15) * 16
+// instead of p * 256 + n * 16).
 template <typename KeyPtr>  // a KeyEntry in global memory, or its copy staged in LDS (the chunked kernel)
 __device__ void build_ghash_tables(lds_u8 *lds, KeyPtr key, u32 ntables = ENGINE_G, u32 src8 = 8, u32 first = 0, u32 tid0 = 0,
-                                   u32 nthr = 0, bool ct = false, bool wl = false)
+                                   u32 nthr = 0, bool ct = false, u32 wmask = 0)
 {
     const u32 stride = nthr != 0 ? nthr : blockDim.x;
     for (u32 idx = first * 32 + threadIdx.x - tid0; idx < ntables * 32; idx += stride) {
@@ -145,7 +145,7 @@ __device__ void build_ghash_tables(lds_u8 *lds, KeyPtr key, u32 ntables = ENGINE
             if ((c >> (3 - m)) & 1u)
                 ec ^= v[m];
         const u32 T = LDS_AES_BYTES + t * GHASH_TABLE_BYTES;
-        if (wl && t != 7)
+        if ((wmask >> t) & 1u)
             store_window<true>(lds + T + (p >> 4) * 4096 + (p & 15) * 16, v, ec, c);
         else
             store_window<false>(lds + T + p * 256, v, ec, c);

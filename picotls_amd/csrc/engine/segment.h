@@ -37,7 +37,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                                             u32 &okw, bool aligned, u32 ekslot = 0)
 {
     constexpr int G = ENGINE_G;
-    constexpr bool COOP = !CT && SEG_COOP;  // the default mode's conflict-free segment end (coop_last_powers)
+    constexpr bool COOP = SEG_COOP;  // the conflict-free segment end (coop_last_powers), both modes
     constexpr bool SEAL_FRAME = FRAME == 1 && !OPEN, OPEN_FRAME = FRAME == 1 && OPEN, TLS12 = FRAME == 2;
     const u32 L = gcm_text_len<OPEN, FRAME>(r), A = gcm_aad_len<OPEN, FRAME>(r);
     // bytes of text readable at src (a framed seal reads len payload bytes; its last text byte is the content type)
@@ -260,14 +260,14 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         __builtin_amdgcn_sched_barrier(0);
         const bool last_here = (int)m0 == m_last;
         u32x4 prod;
-        if (CT && CT_TREE) {
+        if (!COOP && CT && CT_TREE) {
             // every lane multiplies by H^8, the uniform Horner table; a lane's last position stays unmultiplied and
             // takes its power H^e_last in the tree after the loop
             const u32x4 t = acc ^ X;
             prod = gmul_tab(lds, t, tsel_horner);
             if (last_here)
                 prod = t;
-        } else if (CT && __any(last_here)) {
+        } else if (!COOP && CT && __any(last_here)) {
             // H^8 (the Horner step, and a last power of 8), then H^4, H^2, H^1 kept on the bits of e_last; one
             // multiply site in a loop, so the branch costs no more registers than a plain step
             u32x4 t = acc ^ X;
@@ -302,7 +302,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     }
 
     static_assert(G == 8, "dpp_xor8 reduces groups of 8 lanes");
-    if constexpr (CT && CT_TREE) {
+    if constexpr (!COOP && CT && CT_TREE) {
         // sum over the group of a_l H^(e_l) (a_l: lane l's partial with its last position unmultiplied, e_l in 1..8 a
         // permutation over the lanes), as a butterfly over the ranks t = 8 - e: level k pairs rank t (bit k clear) with
         // rank t + k as v_t H^k + v_(t+k); every lane multiplies by the same table (H, H^2, H^4, then H once more) and

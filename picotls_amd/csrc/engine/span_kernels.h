@@ -33,7 +33,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     // AES tables on waves 0..10, H^1..H^8 and H^128 (slot 8) on waves 11..15
     if (wave >= EARLY_GHASH_WAVE)
         build_ghash_tables(lds, args.keys, 9, 8, 0, EARLY_GHASH_WAVE * 64, ENGINE_WG - EARLY_GHASH_WAVE * 64, false,
-                           !CT && SEG_COOP);
+                           GHASH_WMASK(CT));
     else
         build_aes_tables(lds, 0, EARLY_GHASH_WAVE * 64);
     __syncthreads();

@@ -64,8 +64,8 @@ exit 0
   )
   ;;
 coop)
-  # round 3: the window-major default mode (coop_last_powers, gmul_group_w): GPU suite, then the LDS counters of the
-  # default mode for two keys x two payloads, batch kernels (tls16k, quic1200, mixed) and per-record calls
+  # round 3: window-major power tables (coop_last_powers, gmul_group_w): GPU suite, then the LDS counters of the default
+  # mode for two keys x two payloads (batch kernels: tls16k, quic1200, mixed), and of both modes for per-record calls
   (
 bash tools/gpu_tests.sh || exit 1
 R=$GRAFT_REPO_ROOT; cd /tmp && export TMPDIR=/tmp
@@ -74,12 +74,12 @@ for k in 1 2; do for pl in zero random; do
   timeout -k 10 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS --output-format csv -d $R/gpurun_out/ct4/$1_default_k${k}_$pl -o p -- python3 $R/tools/ct_probe.py --workload $1 --records $2 --key-seed $k --payload $pl > $R/gpurun_out/ct4_$1_k${k}_$pl.log 2>&1
   rc=$?; echo "$1 $k $pl rc=$rc"; [ $rc -ne 0 ] && { tail -5 $R/gpurun_out/ct4_$1_k${k}_$pl.log; exit $rc; }
 done; done; done
-export PTLS_MI355X_CONSTANT_TIME=0
+for mode in ct default; do [ $mode = default ] && export PTLS_MI355X_CONSTANT_TIME=0 || unset PTLS_MI355X_CONSTANT_TIME
 for ln in 1200 16384 1048576; do
 for k in 1 2; do for pl in zero random; do
-  timeout -k 10 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS --output-format csv -d $R/gpurun_out/ct4pr/${ln}_default_k${k}_$pl -o p -- python3 $R/tools/ct_probe_perrec.py --len $ln --key-seed $k --payload $pl --calls 4 > $R/gpurun_out/ct4pr_${ln}_k${k}_$pl.log 2>&1
-  rc=$?; echo "$ln $k $pl rc=$rc"; [ $rc -ne 0 ] && { tail -5 $R/gpurun_out/ct4pr_${ln}_k${k}_$pl.log; exit $rc; }
-done; done; done
+  timeout -k 10 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS --output-format csv -d $R/gpurun_out/ct4pr/${ln}_${mode}_k${k}_$pl -o p -- python3 $R/tools/ct_probe_perrec.py --len $ln --key-seed $k --payload $pl --calls 4 > $R/gpurun_out/ct4pr_${ln}_${mode}_k${k}_$pl.log 2>&1
+  rc=$?; echo "$ln $mode $k $pl rc=$rc"; [ $rc -ne 0 ] && { tail -5 $R/gpurun_out/ct4pr_${ln}_${mode}_k${k}_$pl.log; exit $rc; }
+done; done; done; done
 unset PTLS_MI355X_CONSTANT_TIME
 cd $R
 python3 tools/ct_summary.py gpurun_out/ct4 > gpurun_out/ct4_batch.txt; python3 tools/ct_summary.py gpurun_out/ct4pr > gpurun_out/ct4_perrec.txt
