@@ -59,7 +59,7 @@ __device__ __forceinline__ u32x4 gmul_group(const lds_u8 *, u32x4 a, u32 tsel, u
 // read different rows in one instruction (each lane its own power, or its own windows of a shared product) conflict
 // whenever two of them meet the same nibble: a count that follows the data (profiles/r2_ct_evidence.txt).
 //
-// Window-major tables (WTAB: H^1..H^7 in slots 0..6 and the unit combine power in slot 8 in the default mode) put entry
+// Window-major tables (H^1..H^7 in slots 0..6 in both modes, the unit combine power in slot 8 in the default mode) put entry
 // (w, n) at T + (w >> 4) * 4096 + n * 256 + (w & 15) * 16: the bank group is (w & 15), whatever the data. Lane `lane`
 // of an 8-lane group (index y = lane & 7) handles the four windows 4y..4y+3 of the operand's halfword y, window
 // 4y + (i ^ f) at its i-th lookup, f = (lane >> 2) & 3. At every lookup the 16 lanes of a ds_read_b128 phase (16
@@ -108,7 +108,7 @@ __device__ __forceinline__ u32x4 gmul_combine(const lds_u8 *lds, u32x4 a, u32 ts
         return gmul_group(lds, a, tsel, lane % ENGINE_G);
 }
 
-// The default mode's segment end (gcm_segment): lane j of a group holds a_j, its partial with its last stream position
+// The segment end (gcm_segment, both modes): lane j of a group holds a_j, its partial with its last stream position
 // unmultiplied, and owes it the power H^(e_j), e_j = 8 - rank_j (the ranks are the lanes rotated by rot, uniform over the
 // group). Returns this lane's share of sum_j a_j H^(e_j - 1) (the caller XOR-reduces the group and multiplies the sum by
 // H): the value of rank r moves to lane r (ds_bpermute, only when some group of the wave has rot != 0), an 8 x 8

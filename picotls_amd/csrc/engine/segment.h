@@ -22,9 +22,12 @@
 // writes and 2 % of seal time on 16 KiB records, profiles/r2_write_align.txt). Its stream ends where it ends (N any):
 // lanes past the length block in the last step are idle, and each lane's last position p multiplies by H^(N - p), 1..G.
 //
-// CT (constant-time LDS access): a lane's last multiply by its own power H^e, from its own table, reads another table
-// row than the lanes beside it, so its bank conflicts depend on the data (profiles/r2_ct_counters.txt). With CT
-// (CT_TREE, round 3), every step multiplies by the uniform Horner table, a lane's last position stays unmultiplied, and
+// Segment end (SEG_COOP, both modes, late round 3): a lane's last multiply by its own power H^e from its own
+// nibble-major table read another table row than the lanes beside it, so its bank conflicts depended on the data
+// (profiles/r2_ct_counters.txt). Now every lane keeps its last position unmultiplied, the wave's last step skips the
+// Horner multiply, and coop_last_powers (ghash.h) applies the powers from window-major tables after the loop: 32
+// conflict-free lookups per lane, E(K, J0) waiting in the caller's LDS slot (ekslot) and added on the length lane.
+// Without SEG_COOP: CT (constant-time LDS access) with CT_TREE (round 3), every step multiplies by the uniform Horner table, a lane's last position stays unmultiplied, and
 // after the loop a butterfly over the group's lanes applies the powers H^e (three levels with the tables H, H^2, H^4,
 // then H once more: four uniform-table multiplies per segment). E(K, J0) then waits in an LDS slot of the caller's
 // (ekslot) until the tree is done, and is added on the length lane only (lane jl: the lane the tag or the unit partial
