@@ -80,9 +80,9 @@ __device__ __forceinline__ u32 lane_here()
 #define SEG_COOP 1                 // window-major power tables, the lanes' last powers by coop_last_powers (both modes)
 #endif
 // GHASH table layouts (build_ghash_tables `wmask`: bit t = table t window-major, ghash.h). With SEG_COOP the power
-// tables H^1..H^7 (slots 0..6) in both modes, and the unit combine power (slot 8) in the default mode (gmul_group_w; the
-// constant-time mode combines with gmul_tab, nibble-major). H^8 (slot 7, the Horner table) stays nibble-major.
-#define GHASH_WMASK(ct) (SEG_COOP ? ((ct) ? 0x7Fu : 0x17Fu) : 0u)
+// tables H^1..H^7 (slots 0..6) and the unit combine power (slot 8, gmul_group_w) in both modes; H^8 (slot 7, the
+// Horner table every lane reads at the same window) stays nibble-major.
+#define GHASH_WMASK(ct) (SEG_COOP ? 0x17Fu : 0u)
 // the constant-time mode's combine tree keeps combine powers in tables 4..6: only without SEG_COOP (H^5..H^7 there)
 #define CT_COMB_TREE_ON (CT_COMBINE_TREE && !SEG_COOP)
 

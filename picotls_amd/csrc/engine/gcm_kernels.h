@@ -601,7 +601,7 @@ __device__ __attribute__((noinline)) void spread_pieces(BatchArgs args, u32 w, u
         if (split) {
             if (wave == 1)
                 build_elem_table(lds, tsel_ml, u32x4{key->h[key_pow2_idx(mL)][0], key->h[key_pow2_idx(mL)][1],
-                                                     key->h[key_pow2_idx(mL)][2], key->h[key_pow2_idx(mL)][3]}, 64, !CT && SEG_COOP);
+                                                     key->h[key_pow2_idx(mL)][2], key->h[key_pow2_idx(mL)][3]}, 64, SEG_COOP);
             if (wave == 0) {
                 const u32 lane = lane_here(), c = lane / G, L = 1u << (e - 3), ulo = c * L, uhi = min(ulo + L, nu);
                 u32x4 g = {0, 0, 0, 0};

@@ -95,15 +95,16 @@ __device__ __forceinline__ u32x4 gmul_group_w(const lds_u8 *, u32x4 a, u32 tsel,
     return r;
 }
 
-// A group's product by the unit combine power (table 8) or another combine element: constant-time mode gmul_tab (every
-// lane the whole product from the same rows of a nibble-major table), the default mode gmul_group_w (window-major)
+// A group's product by the unit combine power (table 8) or another combine element: with SEG_COOP gmul_group_w
+// (window-major, conflict-free by construction) in both modes; without it, the constant-time mode gmul_tab (every lane
+// the whole product from the same rows of a nibble-major table) and the default mode gmul_group
 template <bool CT>
 __device__ __forceinline__ u32x4 gmul_combine(const lds_u8 *lds, u32x4 a, u32 tsel, u32 lane)
 {
-    if constexpr (CT)
-        return gmul_tab(lds, a, tsel);
-    else if constexpr (SEG_COOP)
+    if constexpr (SEG_COOP)
         return gmul_group_w(lds, a, tsel, lane);
+    else if constexpr (CT)
+        return gmul_tab(lds, a, tsel);
     else
         return gmul_group(lds, a, tsel, lane % ENGINE_G);
 }
