@@ -131,12 +131,11 @@ int ptls_mi355x_keyset_set_schedule(ptls_mi355x_keyset_t *ks, int schedule);
 
 /**
  * Constant-time LDS access (no reference counterpart: fusion's AES-NI / PCLMUL code is constant-time by construction).
- * The AES T-table lookups, the GHASH Horner steps and (since late round 3, window-major power tables) each lane's last
- * block position have bank-conflict patterns that do not depend on keys or data in either mode; the modes differ in the
- * unit combine of records longer than one unit. With on != 0 the keyset's batches and per-record calls
- * use the variant in which every LDS access has a data-independent pattern by construction (SQ_LDS_BANK_CONFLICT equal
- * for any key and payload; the combines read one uniform table per product), at 0 % (records of one unit) to 4 % (the
- * mixed-length many-key batch) of throughput. The environment variable PTLS_MI355X_CONSTANT_TIME=1 (read when a device
+ * With on != 0 the keyset's batches and per-record calls use the variant in which every LDS access has a
+ * data-independent pattern by construction (SQ_LDS_BANK_CONFLICT equal for any key and payload). Since
+ * the window-major power tables (late round 3) the AES T-table lookups, the GHASH Horner steps, each lane's last block
+ * position and the unit combines are built that way in both settings, so the two run the same kernels and the setting
+ * costs no throughput. The environment variable PTLS_MI355X_CONSTANT_TIME=1 (read when a device
  * is first used) sets it for every keyset created afterwards. The picotls AEAD objects (mi355x_picotls.h) turn it on for
  * their keysets by default, as they replace a constant-time backend; PTLS_MI355X_CONSTANT_TIME=0 turns that off.
  * Returns 0, or -1.
