@@ -169,6 +169,10 @@ static int set_kernel_attrs(void)
     CHUNKED_ATTR_X(14, true, 0, 1);
     CHUNKED_ATTR_X(10, false, 0, 2);
     CHUNKED_ATTR_X(14, false, 0, 2);
+    CHUNKED_ATTR_X(10, false, 0, 3);
+    CHUNKED_ATTR_X(10, true, 0, 3);
+    CHUNKED_ATTR_X(14, false, 0, 3);
+    CHUNKED_ATTR_X(14, true, 0, 3);
     CHUNKED_ATTR(10, false, 0);
     CHUNKED_ATTR(10, true, 0);
     CHUNKED_ATTR(14, false, 0);
@@ -851,6 +855,15 @@ static void launch_chunked(bool ct, unsigned grid, hipStream_t s, const BatchArg
                 launch_chunked_x<NR, false, 0, 2>(ct, grid, s, a);
                 return;
             }
+        }
+        // whole-record runs of long records go to their own instantiation (EXT 3: the 8-bit Horner table), the other
+        // runs to the plain one; each skips the other's runs (a batch of fewer records than a whole run has none)
+        if (W8_HORNER && !a.one_inline && a.nrecs >= WHOLE_MIN_RECS) {
+            BatchArgs b = a;
+            b.w8_split = 1;
+            launch_chunked_x<NR, OPEN, 0>(ct, grid, s, b);
+            launch_chunked_x<NR, OPEN, 0, 3>(ct, grid, s, b);
+            return;
         }
     }
     launch_chunked_x<NR, OPEN, FRAME>(ct, grid, s, a);

@@ -141,8 +141,19 @@ __device__ __forceinline__ u32 lane_here()
 #define CLDS_PART (CLDS_RUN1 + 4 * RUN_WORDS)                    // 16 B per unit: GHASH partial
 #define CLDS_ONE (CLDS_PART + 16 * CRUN_UNITS)                   // a lone record's descriptor (BatchArgs::one)
 #define CLDS_ALLOC (CLDS_ONE + 48)
+// W8 runs (whole records of at least W8_MIN_STEPS steps, gcm_chunked_kernel): H^8 as an 8-bit table over slots 0..7,
+// H in slot 8, H^2 in the partial region after the E(K, J0) slots of the groups
+#ifndef W8_HORNER
+#define W8_HORNER 0  // (late round 3: +13 % on 16 KiB records in an interleaved A/B; on by default once its suite has run)
+#endif
+#ifndef W8_MIN_STEPS
+#define W8_MIN_STEPS 64
+#endif
+#define W8_TAB_H (LDS_AES_BYTES + 8 * GHASH_TABLE_BYTES)
+#define W8_TAB_H2 (CLDS_PART + 16 * (ENGINE_WG / ENGINE_G))
 #define SPAN_MAX_UNITS CRUN_UNITS  // units per span of a long record (span_kernels.h, spread_pieces): the LDS partials
 static_assert(CLDS_ALLOC <= 160 * 1024, "chunked schedule LDS budget");
+static_assert(W8_TAB_H2 % 256 == 0 && W8_TAB_H2 + GHASH_TABLE_BYTES <= CLDS_ONE, "W8 tables inside the partial region");
 static_assert(CHUNK_BLOCKS % ENGINE_G == 0, "units are whole steps");
 static_assert((CHUNK_STEPS & (CHUNK_STEPS - 1)) == 0 && CHUNK_STEPS <= 32, "unit lengths are powers of two up to 32 steps");
 

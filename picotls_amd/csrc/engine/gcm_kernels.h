@@ -711,6 +711,22 @@ __device__ __noinline__ u32x4 ct_combine_tree(const lds_u8 *lds, const lds_u32x4
     return g;
 }
 
+// The W8 tables of the run's key (staged in LDS): H^8's 4-bit table into slot 8 as the source of its 8-bit table over
+// slots 0..7, then H into slot 8 and H^2 beside the E(K, J0) slots. Out of line: inlined into the run loop it cost the
+// kernel's other runs registers (-4 % on 1200-byte records).
+__device__ __noinline__ void w8_build_tables(lds_u8 *lds, const lds_u8 *keyp)
+{
+    typedef __attribute__((address_space(3))) const KeyEntry lds_key_t;
+    lds_key_t *key = (lds_key_t *)keyp;
+    build_ghash_tables(lds, key, 9, 7u, 8u, 0, 0, false, 0u);
+    __syncthreads();
+    build_h8_byte_table(lds, W8_TAB_H);
+    __syncthreads();
+    build_ghash_tables(lds, key, 9, 0u, 8u, 0, 0, false, 0u);
+    build_elem_table(lds, W8_TAB_H2, u32x4{key->h[1][0], key->h[1][1], key->h[1][2], key->h[1][3]}, 64);
+    __syncthreads();
+}
+
 template <int NR, bool OPEN, int FRAME, bool CT = false, int EXT = 0>
 __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGINE_WAVES_PER_SIMD, ENGINE_WAVES_PER_SIMD))) void gcm_chunked_kernel(BatchArgs args)
 {
@@ -741,6 +757,8 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     u64 end = SPREAD ? (u64)blockIdx.x + 1 : args.bounds != nullptr ? args.bounds[blockIdx.x + 1] : C != 0 ? min(n, beg + C) : n * (blockIdx.x + 1) / gridDim.x;
     u64 cstart = beg;
     u32 loaded_key = 0xffffffffu, loaded_usrc = 0xffffffffu;
+    bool loaded_w8 = false;  // the LDS holds the W8 tables (an 8-bit H^8 table, H, H^2) instead of the nine 4-bit ones
+    constexpr bool W8K = W8_HORNER && FRAME == 0 && EXT == 3;  // the launch pair's W8 half (launch_chunked)
     // the descriptors in batch order, or (an ungrouped many-key batch) the key-grouped copy built on the device; ok
     // bytes go to the record's batch index either way
     const ptls_mi355x_record_t *recs = args.recs;
@@ -780,7 +798,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     // the AES tables. A one-key launch knows its key before the scan: waves EARLY_GHASH_WAVE.. build its GHASH tables
     // H^1..H^8 meanwhile (and the unit combine table when the launch fixes the unit length: the per-record path),
     // instead of after the prologue barrier; the AES copy keeps the waves in between.
-    const bool early = EARLY_GHASH && !args.multi_key;
+    const bool early = EARLY_GHASH && !args.multi_key && !W8K;
     const u32 fixed_usrc = args.unit_log2 == CHUNK_LOG2 ? 8u : args.unit_log2 == 0 ? 7u : 8u + args.unit_log2;
     const bool early_combine = early && args.unit_log2 < CHUNK_LOG2;
     if (early && wave >= EARLY_GHASH_WAVE) {
@@ -833,6 +851,20 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         }
         PROF_STAMP(t1);
 
+        // the launch pair (args.w8_split): W8 runs (whole, long records, valid key) belong to the EXT 3 kernel, the
+        // rest to the EXT 0 one; each scans past the other's runs
+        if (W8_HORNER && (FRAME == 0 && EXT == 0 ? args.w8_split != 0 : W8K)) {
+            const bool w8 = whole && key_idx < args.nkeys &&
+                            __builtin_amdgcn_readfirstlane(gcm_steps<OPEN, FRAME>(recs[pos]) >= W8_MIN_STEPS ? 1u : 0u) != 0;
+            if (w8 != W8K) {
+                if (wave == 0 && nxt < nxt_end)
+                    scan_run<OPEN, FRAME, false, EXT>(args, recs, nxt, nxt_end, rs_next);
+                __syncthreads();
+                pos = nxt, end = nxt_end, cstart = nxt_cstart;
+                rb ^= 1;
+                continue;
+            }
+        }
         if (key_idx >= args.nkeys) {  // invalid key: nothing is written except a failed ok byte
             if (OPEN)
                 for (u64 t = pos + threadIdx.x; t < run_end; t += blockDim.x)
@@ -852,14 +884,27 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         }
         typedef __attribute__((address_space(3))) const KeyEntry lds_key_t;
         lds_key_t *key = (lds_key_t *)(rs + RUN_KEY_OFF);  // staged by the scanner
-        if (key_idx != loaded_key || (!whole && usrc != loaded_usrc)) {
+        // the EXT 3 kernel's runs (all W8: the others were skipped above) take the 8-bit Horner table (ghash.h)
+        constexpr bool w8run = W8K;
+        if (w8run && (key_idx != loaded_key || !loaded_w8)) {
+            // H^8's 4-bit table into slot 8 as the source of its 8-bit table over slots 0..7, then H into slot 8 and
+            // H^2 beside the E(K, J0) slots
+            w8_build_tables(lds, (const lds_u8 *)key);
+            loaded_key = key_idx;
+            loaded_usrc = 0xffffffffu;
+            loaded_w8 = true;
+            if (threadIdx.x == 0)
+                PROF_ADD(7, 1);
+        } else if (!w8run && (key_idx != loaded_key || loaded_w8 || (!whole && usrc != loaded_usrc))) {
             // H^1..H^8 and the unit combine power (only the latter when just the unit length changed; constant-time
             // mode: its powers in tables 4..6 too)
             constexpr bool CTT = CT && CT_COMB_TREE_ON;
-            build_ghash_tables(lds, key, 9, usrc, key_idx != loaded_key ? 0u : CTT ? 4u : 8u, 0, 0, CTT, GHASH_WMASK(CT));
+            build_ghash_tables(lds, key, 9, usrc, key_idx != loaded_key || loaded_w8 ? 0u : CTT ? 4u : 8u, 0, 0, CTT,
+                               GHASH_WMASK(CT));
             __syncthreads();
             loaded_key = key_idx;
             loaded_usrc = usrc;
+            loaded_w8 = false;
             if (threadIdx.x == 0)
                 PROF_ADD(7, 1);
         }
@@ -954,8 +999,8 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 // (constant-time mode: E(K, J0) waits in the slot of the record's last unit partial, or of the group
                 // in a whole-record run, which has no partials)
                 const u32 ekslot = CLDS_PART + 16u * (whole ? threadIdx.x / G : first + unc - 1);
-                gcm_segment<NR, OPEN, 1, FRAME, CT>(args, lds, rk, iv0, iv1, iv2, r, live, m_lo, m_hi, j, laneoff, tsel_horner, acc,
-                                                    unc == 1, okw, whole, ekslot);
+                gcm_segment<NR, OPEN, 1, FRAME, CT, W8K>(args, lds, rk, iv0, iv1, iv2, r, live, m_lo, m_hi, j, laneoff,
+                                                         tsel_horner, acc, unc == 1, okw, whole, ekslot);
             }
             // from here on everything is read again (run state, descriptor), not carried across the segment
             asm volatile("" ::: "memory");

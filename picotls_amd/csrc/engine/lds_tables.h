@@ -152,6 +152,18 @@ __device__ void build_ghash_tables(lds_u8 *lds, KeyPtr key, u32 ntables = ENGINE
     }
 }
 
+// W8 runs (ghash.h): the 8-bit window-major H^8 table at LDS_AES_BYTES from H^8's 4-bit nibble-major table at `scratch`
+// (entry (w, n) = e4(2w, n >> 4) ^ e4(2w + 1, n & 15): byte w of the operand is 4-bit windows 2w and 2w + 1)
+__device__ __forceinline__ void build_h8_byte_table(lds_u8 *lds, u32 scratch)
+{
+    for (u32 i = threadIdx.x; i < 4096; i += blockDim.x) {
+        const u32 w = i & 15, n = i >> 4;
+        const u32x4 e = u32x4(*(const lds_u32x4 *)(lds + scratch + (2 * w) * 256 + (n >> 4) * 16)) ^
+                        u32x4(*(const lds_u32x4 *)(lds + scratch + (2 * w + 1) * 256 + (n & 15) * 16));
+        *(lds_u32x4 *)(lds + LDS_AES_BYTES + n * 256 + w * 16) = e;
+    }
+}
+
 // The 4-bit window table of one GHASH element at LDS offset `base` (a multiple of 256; window-major with wl: a multiple
 // of 64), by threads [tid0, tid0 + 32): the same construction as build_ghash_tables for an element given by value.
 __device__ __forceinline__ void build_elem_table(lds_u8 *lds, u32 base, u32x4 h, u32 tid0 = 0, bool wl = false)

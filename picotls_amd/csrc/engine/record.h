@@ -85,6 +85,9 @@ struct BatchArgs {
     u32 spread;
     u32x4 *spread_part;
     u32 *spread_cnt;
+    // chunked kernel, FRAME 0: the launch is a pair (launch_chunked): EXT 0 skips the W8 runs (whole-record runs of
+    // records of W8_MIN_STEPS steps or more), EXT 3 processes only those
+    u32 w8_split;
 };
 
 #define RUN_SCAN_CAP 256  // records examined per key-run scan (multi-key batches)

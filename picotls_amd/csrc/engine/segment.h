@@ -33,14 +33,20 @@
 // (ekslot) until the tree is done, and is added on the length lane only (lane jl: the lane the tag or the unit partial
 // is taken from). The round-2 form (CT_TREE 0) ran four multiplies, H^8, H^4, H^2, H^1 kept on the bits of e, in every
 // step in which some lane of the wave was at its last position (two or more steps per segment).
-template <int NR, bool OPEN, int NB, int FRAME = 0, bool CT = false>
+template <int NR, bool OPEN, int NB, int FRAME = 0, bool CT = false, bool W8 = false>
 __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 *lds, const u32 (&rk)[NR + 1][4], u32 iv0,
                                             u32 iv1, u32 iv2, const ptls_mi355x_record_t &r, bool valid, u32 m_lo,
                                             u32 m_hi, u32 j, u32 laneoff, u32 tsel_horner, u32x4 &acc, bool finish,
                                             u32 &okw, bool aligned, u32 ekslot = 0)
 {
     constexpr int G = ENGINE_G;
-    constexpr bool COOP = SEG_COOP;  // the conflict-free segment end (coop_last_powers), both modes
+    // W8 (a whole-record run of long records, gcm_chunked_kernel): Horner on the 8-bit H^8 table (gmul8), the lanes'
+    // last powers by the uniform-table tree with H (W8_TAB_H) and H^2 (W8_TAB_H2; H^4 as two of it)
+    constexpr bool COOP = SEG_COOP && !W8;  // the conflict-free segment end (coop_last_powers), both modes
+    constexpr bool TREE = W8 || (!SEG_COOP && CT && CT_TREE);
+    W8Lane w8 = {};
+    if constexpr (W8)
+        w8 = w8_lane(lane_here());
     constexpr bool SEAL_FRAME = FRAME == 1 && !OPEN, OPEN_FRAME = FRAME == 1 && OPEN, TLS12 = FRAME == 2;
     const u32 L = gcm_text_len<OPEN, FRAME>(r), A = gcm_aad_len<OPEN, FRAME>(r);
     // bytes of text readable at src (a framed seal reads len payload bytes; its last text byte is the content type)
@@ -203,7 +209,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             X[1] = bswap32((u32)abits);
             X[2] = bswap32((u32)(cbits >> 32));
             X[3] = bswap32((u32)cbits);
-            if (COOP || (CT && CT_TREE))  // (kept in LDS until after the loop: live through it, it was spilled)
+            if (COOP || TREE)  // (kept in LDS until after the loop: live through it, it was spilled)
                 *(lds_u32x4 *)(const_cast<lds_u8 *>(lds) + ekslot) = ks;
             else
                 ek0 = ks;
@@ -244,7 +250,10 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                 const u32x4 o = cur ^ u32x4{st[0][0], st[0][1], st[0][2], st[0][3]};
                 *(u32x4_u *)(dst + off) = o;
                 __builtin_amdgcn_sched_barrier(0);
-                acc = gmul_tab(lds, acc ^ (OPEN ? cur : o), tsel_horner);
+                if constexpr (W8)
+                    acc = gmul8(lds, acc ^ (OPEN ? cur : o), lane_here(), w8);
+                else
+                    acc = gmul_tab(lds, acc ^ (OPEN ? cur : o), tsel_horner);
                 __builtin_amdgcn_sched_barrier(0);
                 ctr += G;
                 off += 16 * G;
@@ -263,14 +272,14 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         __builtin_amdgcn_sched_barrier(0);
         const bool last_here = (int)m0 == m_last;
         u32x4 prod;
-        if (!COOP && CT && CT_TREE) {
+        if (!W8 && !COOP && CT && CT_TREE) {
             // every lane multiplies by H^8, the uniform Horner table; a lane's last position stays unmultiplied and
             // takes its power H^e_last in the tree after the loop
             const u32x4 t = acc ^ X;
             prod = gmul_tab(lds, t, tsel_horner);
             if (last_here)
                 prod = t;
-        } else if (!COOP && CT && __any(last_here)) {
+        } else if (!W8 && !COOP && CT && __any(last_here)) {
             // H^8 (the Horner step, and a last power of 8), then H^4, H^2, H^1 kept on the bits of e_last; one
             // multiply site in a loop, so the branch costs no more registers than a plain step
             u32x4 t = acc ^ X;
@@ -286,13 +295,16 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             if (!last_here || e_last == (u32)G)
                 t = prod;
             prod = t;
-        } else if (COOP) {
+        } else if (COOP || W8) {
             // every lane multiplies by H^8, the uniform Horner table, except at its last position, which takes its
             // power H^e_last after the loop (coop_last_powers); in the wave's last step no lane needs the multiply
             const u32x4 t = acc ^ X;
             prod = t;
             if (s0 + 1 < Smax) {
-                prod = gmul_tab(lds, t, tsel_horner);
+                if constexpr (W8)
+                    prod = gmul8(lds, t, lane_here(), w8);
+                else
+                    prod = gmul_tab(lds, t, tsel_horner);
                 if (last_here)
                     prod = t;
             }
@@ -305,7 +317,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     }
 
     static_assert(G == 8, "dpp_xor8 reduces groups of 8 lanes");
-    if constexpr (!COOP && CT && CT_TREE) {
+    if constexpr (TREE) {
         // sum over the group of a_l H^(e_l) (a_l: lane l's partial with its last position unmultiplied, e_l in 1..8 a
         // permutation over the lanes), as a butterfly over the ranks t = 8 - e: level k pairs rank t (bit k clear) with
         // rank t + k as v_t H^k + v_(t+k); every lane multiplies by the same table (H, H^2, H^4, then H once more) and
@@ -317,7 +329,14 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
 #pragma unroll 1
         for (u32 lv = 0; lv < 3; ++lv) {
             const u32 k = 1u << lv;
-            const u32x4 y = gmul_tab(lds, v, 0x10000u + (k - 1u) * GHASH_TABLE_BYTES);  // H^k
+            u32x4 y;
+            if constexpr (W8) {  // H, H^2, H^2 twice
+                y = gmul_tab(lds, v, lv == 0 ? (u32)W8_TAB_H : (u32)W8_TAB_H2);
+                if (lv == 2)
+                    y = gmul_tab(lds, y, W8_TAB_H2);
+            } else {
+                y = gmul_tab(lds, v, 0x10000u + (k - 1u) * GHASH_TABLE_BYTES);  // H^k
+            }
             const bool hi = (rank & k) != 0;
             const u32x4 send = hi ? v : y;
             const int src = (int)(((lane & ~(u32)(G - 1)) | (((rank ^ k) + rot) & (G - 1))) * 4);
@@ -327,7 +346,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                 recv[c] = (u32)__builtin_amdgcn_ds_bpermute(src, (int)send[c]);
             v = hi ? (recv ^ v) : (y ^ recv);
         }
-        acc = gmul_tab(lds, v, 0x10000u);  // * H
+        acc = gmul_tab(lds, v, W8 ? (u32)W8_TAB_H : 0x10000u);  // * H
         if (valid && m_hi * G >= N && j == jl)  // the segment holds the length block: E(K, J0), on its lane
             acc ^= u32x4(*(const lds_u32x4 *)(lds + ekslot));
     } else {
