@@ -135,9 +135,9 @@ int ptls_mi355x_keyset_set_schedule(ptls_mi355x_keyset_t *ks, int schedule);
  * data-independent pattern by construction (SQ_LDS_BANK_CONFLICT equal for any key and payload). Since
  * the window-major power tables (late round 3) the AES T-table lookups, the GHASH Horner steps, each lane's last block
  * position and the unit combines are built that way in both settings, so the two run the same kernels and the setting
- * costs no throughput. The environment variable PTLS_MI355X_CONSTANT_TIME=1 (read when a device
- * is first used) sets it for every keyset created afterwards. The picotls AEAD objects (mi355x_picotls.h) turn it on for
- * their keysets by default, as they replace a constant-time backend; PTLS_MI355X_CONSTANT_TIME=0 turns that off.
+ * costs no throughput. Every keyset is constant-time when created (round 4; fusion, which this replaces, is constant-time
+ * for every context); the environment variable PTLS_MI355X_CONSTANT_TIME=0 (read when a device is first used) creates
+ * keysets with the setting off, and on = 0 turns it off for one keyset. Off, a keyset may take the lockstep schedule.
  * Returns 0, or -1.
  */
 int ptls_mi355x_keyset_set_constant_time(ptls_mi355x_keyset_t *ks, int on);

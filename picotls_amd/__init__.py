@@ -26,7 +26,8 @@ from .records import (CID_DTYPE, HP_DTYPE, QUICLB_MAX_LEN, QUICLB_MIN_LEN, RECOR
                       TLS_UNEXPECTED_MESSAGE, RecordBatch, shard_ranges)
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "_lib", "libptls_mi355x.so")
+# PTLS_MI355X_LIB: another build of the same engine (an A/B variant under tools/variants/) for the GPU suite
+LIB_PATH = os.environ.get("PTLS_MI355X_LIB") or os.path.join(_PKG, "_lib", "libptls_mi355x.so")
 PICOTLS_LIB_PATH = os.path.join(_PKG, "_lib", "libptls_mi355x_picotls.so")
 
 # every function of include/picotls/mi355x.h (tests check the .so exports exactly these)
@@ -206,9 +207,15 @@ class Keyset:
     SCHEDULES = {"auto": 0, "lockstep": 1, "chunked": 2}
 
     def set_schedule(self, schedule: str) -> None:
-        """Batch schedule (ptls_mi355x_keyset_set_schedule): "auto", "lockstep" or "chunked"."""
+        """Batch schedule (ptls_mi355x_keyset_set_schedule): "auto", "lockstep" or "chunked".
+
+        The lockstep schedule (the round-1 kernel, kept for comparison) is not offered to constant-time keysets, which
+        every keyset is by default since round 4: asking for it here also turns the keyset's constant-time setting off,
+        so that the lockstep kernel is the one that runs."""
         if schedule not in self.SCHEDULES:
             raise ValueError(f"unknown schedule {schedule!r}")
+        if schedule == "lockstep":
+            self.set_constant_time(False)
         if load_library().ptls_mi355x_keyset_set_schedule(self.handle, self.SCHEDULES[schedule]) != 0:
             raise _err("set_schedule")
 

@@ -131,8 +131,10 @@ struct DeviceState {
     int priority = 0;             // the device's greatest stream priority: the engine's own streams (setup, teardown,
                                   // per-record round trips) are dispatched ahead of bulk batches on ordinary streams
     bool force_copy = false;      // PTLS_MI355X_STAGE_COPY=1: the staging round trip copies instead of mapping
+    bool stage_coherent = true;   // staging buffers fine-grained (hipHostMallocCoherent); PTLS_MI355X_STAGE_COHERENT=0: the
+                                  // HIP default (coarse-grained), kept only to reproduce the round-3 race
     size_t stage_limit = 0;       // PTLS_MI355X_MAX_STAGE_BYTES: the largest staging buffer one call may use
-    bool ct_default = false;      // PTLS_MI355X_CONSTANT_TIME=1: new keysets use the constant-time GHASH variant
+    bool ct_default = true;       // new keysets are constant-time (PTLS_MI355X_CONSTANT_TIME=0: not, for an A/B)
     bool fault_order = false;     // PTLS_MI355X_FAULT_ORDER=1 (tests only): keyset teardown cannot order itself on the device
     std::mutex mu;                // the pools below
     Stager *stagers[STAGE_CLASSES] = {};
@@ -225,8 +227,13 @@ static DeviceState *device_state(int dev)
     ds->device = dev;
     const char *copy = getenv("PTLS_MI355X_STAGE_COPY"), *limit = getenv("PTLS_MI355X_MAX_STAGE_BYTES");
     ds->force_copy = copy != nullptr && strcmp(copy, "1") == 0;
+    const char *coh = getenv("PTLS_MI355X_STAGE_COHERENT");
+    ds->stage_coherent = !(coh != nullptr && strcmp(coh, "0") == 0);
     const char *ct = getenv("PTLS_MI355X_CONSTANT_TIME");
-    ds->ct_default = ct != nullptr && strcmp(ct, "1") == 0;
+    // (round 4) every keyset constant-time unless PTLS_MI355X_CONSTANT_TIME=0: since the window-major segment ends
+    // (SEG_COOP) both modes run the same code, whose LDS accesses have data-independent bank patterns, at the same
+    // rate; the flag only keeps such keysets off the lockstep schedule
+    ds->ct_default = !(ct != nullptr && strcmp(ct, "0") == 0);
     const char *comb = getenv("PTLS_MI355X_COMBINE");
     if (comb != nullptr)
         ds->combine = atoi(comb) < 0 ? 0 : atoi(comb);
@@ -316,6 +323,7 @@ static KeyEntry *slot_get(DeviceState *ds, KeyEntry **slab_of)
                     ds->pending[i] = ds->pending.back();
                     ds->pending.pop_back();
                 } else {
+                    (void)hipGetLastError();  // (not ready: not an error for the launches that follow)
                     ++i;
                 }
             }
@@ -377,11 +385,18 @@ static Stager *stager_get(DeviceState *ds, size_t bytes)
     }
     if (stream == nullptr) {
         if (hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, ds->priority) != hipSuccess) {
-            fail("%s", "staging: stream creation failed");
-            return nullptr;
+            // (round 4) a stream that cannot be created now is no reason to fail the call: share an existing one
+            (void)hipGetLastError();
+            std::lock_guard<std::mutex> lk(ds->mu);
+            if (ds->stage_streams.empty()) {
+                fail("%s", "staging: stream creation failed");
+                return nullptr;
+            }
+            stream = ds->stage_streams[ds->stage_rr++ % ds->stage_streams.size()];
+        } else {
+            std::lock_guard<std::mutex> lk(ds->mu);
+            ds->stage_streams.push_back(stream);
         }
-        std::lock_guard<std::mutex> lk(ds->mu);
-        ds->stage_streams.push_back(stream);
     }
     Stager *s = new (std::nothrow) Stager();
     if (s == nullptr) {
@@ -391,13 +406,26 @@ static Stager *stager_get(DeviceState *ds, size_t bytes)
     s->stream = stream;
     s->cap = (size_t)4096 << cls;
     s->cls = cls;
-    if (hipHostMalloc((void **)&s->h, s->cap, hipHostMallocDefault) != hipSuccess) {
-        delete s;
-        fail("%s", "staging: pinned host allocation failed");
-        return nullptr;
+    // Fine-grained (coherent) pinned memory: kernels read the staged input and write the results in place over PCIe,
+    // and the host rewrites the same bytes for the next call right after it sees the completion words. Coarse-grained
+    // host memory (hipHostMallocDefault under HIP_HOST_COHERENT=0) may be cached in the GPU's L2, where a later
+    // kernel on this buffer can read lines of the previous call's input.
+    const unsigned hflags = ds->stage_coherent ? hipHostMallocCoherent : hipHostMallocDefault;
+    if (hipHostMalloc((void **)&s->h, s->cap, hflags) != hipSuccess) {
+        // (round 4) the pinned memory of idle buffers of other sizes is what this one may need: free them, try again
+        (void)hipGetLastError();
+        ptls_mi355x_release_staging();
+        if (hipHostMalloc((void **)&s->h, s->cap, hflags) != hipSuccess) {
+            (void)hipGetLastError();
+            delete s;
+            fail("%s", "staging: pinned host allocation failed");
+            return nullptr;
+        }
     }
-    if (ds->force_copy || hipHostGetDevicePointer((void **)&s->h_dev, s->h, 0) != hipSuccess)
+    if (ds->force_copy || hipHostGetDevicePointer((void **)&s->h_dev, s->h, 0) != hipSuccess) {
+        (void)hipGetLastError();  // (handled: the copy path)
         s->h_dev = nullptr;
+    }
     if (s->h_dev == nullptr && hipMalloc((void **)&s->d, s->cap) != hipSuccess) {
         (void)hipHostFree(s->h);
         delete s;
@@ -494,14 +522,15 @@ static int wait_ready(ptls_mi355x_keyset_t *ks, hipStream_t s)
     }
     if (q != hipErrorNotReady)
         return fail("keyset setup failed: %s", hipGetErrorString(q));
+    (void)hipGetLastError();  // (not an error: launches after this are checked with hipGetLastError)
     HIP_TRY(hipStreamWaitEvent(s, ks->ready, 0));
     return 0;
 }
 
-// records that the keyset's entries were used by work just launched on `s` (teardown and rekey wait for it)
-static int note_use(ptls_mi355x_keyset_t *ks, hipStream_t s)
+// records that the keyset's entries were used by work just launched on `s` (teardown and rekey wait for it); the
+// caller holds ks->mu
+static int note_use_locked(ptls_mi355x_keyset_t *ks, hipStream_t s)
 {
-    std::lock_guard<std::mutex> lk(ks->mu);
     for (auto &u : ks->uses)
         if (u.first == s)
             return hipEventRecord(u.second, s) == hipSuccess ? 0 : fail("%s", "hipEventRecord failed");
@@ -511,6 +540,12 @@ static int note_use(ptls_mi355x_keyset_t *ks, hipStream_t s)
     ks->uses.emplace_back(s, e);
     HIP_TRY(hipEventRecord(e, s));
     return 0;
+}
+
+static int note_use(ptls_mi355x_keyset_t *ks, hipStream_t s)
+{
+    std::lock_guard<std::mutex> lk(ks->mu);
+    return note_use_locked(ks, s);
 }
 
 // orders the maintenance stream after every launch that used the keyset and after its last setup
@@ -858,7 +893,9 @@ static void launch_chunked(bool ct, unsigned grid, hipStream_t s, const BatchArg
         }
         // whole-record runs of long records go to their own instantiation (EXT 3: the 8-bit Horner table), the other
         // runs to the plain one; each skips the other's runs (a batch of fewer records than a whole run has none)
-        if (W8_HORNER && !a.one_inline && a.nrecs >= WHOLE_MIN_RECS) {
+        // (not for a per-record launch that publishes completion words: the host would see them when the first kernel
+        // of the pair ends, before the second has sealed its runs)
+        if (W8_HORNER && !a.one_inline && a.done_flag == nullptr && a.nrecs >= WHOLE_MIN_RECS) {
             BatchArgs b = a;
             b.w8_split = 1;
             launch_chunked_x<NR, OPEN, 0>(ct, grid, s, b);
@@ -916,10 +953,11 @@ static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int sche
                       hipStream_t s, int frame, u32 unit_log2, const ptls_mi355x_record_t *grouped = nullptr,
                       const u32 *perm = nullptr, const u32 *perm_on = nullptr, const ptls_mi355x_record_t *one = nullptr,
                       u32 *done_flag = nullptr, const u64 *bounds = nullptr, const HpLaunch *hpl = nullptr,
-                      uint8_t *spread = nullptr)
+                      uint8_t *spread = nullptr, u32 done_token = 0)
 {
     BatchArgs a = {keys, recs, (u64)nrecs, (const uint8_t *)in, (const uint8_t *)aad, (uint8_t *)out, ok,
                    nkeys > 1 ? 1u : 0u, nkeys, unit_log2, grouped, perm, perm_on, 0u, {}, done_flag, 0, bounds};
+    a.done_token = done_token;
     if (hpl != nullptr) {
         if (open || frame != 0 || !(ct || use_chunked(schedule)))
             return fail("%s", "launch_gcm: header-protection masks need the chunked seal of unframed records");
@@ -995,10 +1033,11 @@ static void launch_span_kernel(bool ct, u32 nspans, hipStream_t s, const BatchAr
 
 static int launch_span(const KeyEntry *key, int nr, bool ct, bool open, const ptls_mi355x_record_t &one, const void *in,
                        const void *aad, void *out, uint8_t *ok, u32 units, u32 e, u32 nspans, void *part, u32 *done_flag,
-                       hipStream_t s)
+                       u32 done_token, hipStream_t s)
 {
     BatchArgs a = {key, nullptr, 1, (const uint8_t *)in, (const uint8_t *)aad, (uint8_t *)out, ok, 0u, 1u, CHUNK_LOG2,
                    nullptr, nullptr, nullptr, 1u, one, done_flag, 0, nullptr};
+    a.done_token = done_token;
     const u32 span = 1u << e;
     if (nr == 10) {
         if (open)
@@ -1027,16 +1066,18 @@ static size_t spread_bytes(int ncu)
     return SPREAD_CNT_BYTES + 16 * ((size_t)ncu + (size_t)SPREAD_MAX_RECS * (8192 / SPREAD_UNIT_STEPS + 1));
 }
 
-// the keyset's spread scratch for a launch on `s` (allocated and zeroed in stream order on first use); nullptr when the
-// batch cannot take the spread launch (spread_done records the use afterwards)
-static uint8_t *spread_scratch(ptls_mi355x_keyset_t *ks, hipStream_t s, size_t nrecs, int frame)
+static bool spread_eligible(const ptls_mi355x_keyset_t *ks, size_t nrecs, int frame)
 {
-    if (frame != 0 || nrecs < 2 || nrecs >= (size_t)ks->ds->ncu || nrecs > SPREAD_MAX_RECS ||
-        !(ks->ct || use_chunked(ks->schedule)))
-        return nullptr;
-    std::lock_guard<std::mutex> lk(ks->mu);
+    return frame == 0 && nrecs >= 2 && nrecs < (size_t)ks->ds->ncu && nrecs <= SPREAD_MAX_RECS && (ks->ct || use_chunked(ks->schedule));
+}
+
+// the keyset's spread scratch for a launch on `s` (allocated and zeroed in stream order on first use); nullptr on
+// failure. The caller holds ks->mu from here through the launch and the use event recorded after it (launch_batch),
+// so a launch on another stream always finds the previous user's event recorded.
+static uint8_t *spread_scratch_locked(ptls_mi355x_keyset_t *ks, hipStream_t s)
+{
     // a launch on another stream than the last user waits for that launch (its use event, recorded after it by
-    // note_use); back-to-back launches on one stream add no event packets (a wait and a record per launch cost a
+    // note_use_locked); back-to-back launches on one stream add no event packets (a wait and a record per launch cost a
     // 23 us small-batch launch 7 us)
     if (ks->spread_used && ks->spread_stream != s) {
         for (auto &u : ks->uses)
@@ -1079,10 +1120,18 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
     const bool group = false;
 #endif
     int ret;
-    // small batches with long records: the spread scratch (taken before the group scratch: both lock ks->mu)
-    uint8_t *spread = hpl == nullptr ? spread_scratch(ks, s, nrecs, frame) : nullptr;
+    // the keyset's scratch (spread pieces, key grouping) is shared by its launches on every stream: ks->mu is held from
+    // taking it through the launch and the use event after it
+    std::unique_lock<std::mutex> lk(ks->mu, std::defer_lock);
+    // small batches with long records: the spread scratch
+    uint8_t *spread = nullptr;
+    if (hpl == nullptr && spread_eligible(ks, nrecs, frame)) {
+        lk.lock();
+        spread = spread_scratch_locked(ks, s);
+    }
     if (group) {
-        std::lock_guard<std::mutex> lk(ks->mu);
+        if (!lk.owns_lock())
+            lk.lock();
         // scratch: ctl[2] | counts[nkeys + 1] | perm[n] | (8-byte aligned) grouped descriptors[n] | balance tiles | bounds
         const bool balance = BALANCE && nrecs >= BALANCE_MIN_RECS;
         const size_t ntiles = (nrecs + BALANCE_TILE - 1) / BALANCE_TILE, ncu = (size_t)ks->ds->ncu;
@@ -1126,7 +1175,7 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
     }
     if (ret != 0)
         return -1;
-    return note_use(ks, s);
+    return lk.owns_lock() ? note_use_locked(ks, s) : note_use(ks, s);
 }
 
 static unsigned aux_grid(size_t n, int ncu)
@@ -1149,12 +1198,14 @@ static int launch_ecb(const KeyEntry *keys, u32 nkeys, int nr, int ncu, const ui
 }
 
 static int launch_hp(const KeyEntry *keys, u32 nkeys, int nr, int ncu, const ptls_mi355x_hp_t *hp, size_t n, const void *base,
-                     void *masks, hipStream_t s, u32 *done_flag = nullptr)
+                     void *masks, hipStream_t s, u32 *done_flag = nullptr, u32 done_token = 0)
 {
     if (nr == 10)
-        hp_kernel<10><<<aux_grid(n, ncu), 256, LDS_AES_BYTES, s>>>(keys, nkeys, hp, (const uint8_t *)base, (uint8_t *)masks, n, done_flag);
+        hp_kernel<10><<<aux_grid(n, ncu), 256, LDS_AES_BYTES, s>>>(keys, nkeys, hp, (const uint8_t *)base, (uint8_t *)masks, n, done_flag,
+                                                                    done_token);
     else
-        hp_kernel<14><<<aux_grid(n, ncu), 256, LDS_AES_BYTES, s>>>(keys, nkeys, hp, (const uint8_t *)base, (uint8_t *)masks, n, done_flag);
+        hp_kernel<14><<<aux_grid(n, ncu), 256, LDS_AES_BYTES, s>>>(keys, nkeys, hp, (const uint8_t *)base, (uint8_t *)masks, n, done_flag,
+                                                                    done_token);
     HIP_TRY(hipGetLastError());
     return 0;
 }
@@ -1354,11 +1405,14 @@ struct StageCall {
     // stream as usual.
     bool mapped() const { return st->h_dev != nullptr; }
     template <typename Launch>
-    int roundtrip(size_t up, Launch launch, size_t flag_off = 0, size_t nflags = 0)
+    int roundtrip(size_t up, Launch launch, size_t flag_off = 0, size_t nflags = 0, u32 token = 0)
     {
         const bool copy = st->h_dev == nullptr;
         if (copy)
             HIP_TRY(hipMemcpyAsync(st->d, st->h, up, hipMemcpyHostToDevice, st->stream));
+        // the launches are checked with hipGetLastError: no error an earlier call of this thread left (and handled)
+        // may pass for theirs
+        (void)hipGetLastError();
         if (launch() != 0) {
             // a kernel of this call may already be queued (the span launch before its combine, the GCM launch before
             // the header-protection one): the buffer is cleared and reused only once nothing of it is in flight
@@ -1368,11 +1422,11 @@ struct StageCall {
         if (copy)
             HIP_TRY(hipMemcpyAsync(st->h + up, st->d + up, total - up, hipMemcpyDeviceToHost, st->stream));
         const auto t0 = std::chrono::steady_clock::now();
-        if (flag_off != 0 && !copy) {
+        if (flag_off != 0 && token != 0 && !copy) {
             const u32 *flag = (const u32 *)(st->h + flag_off);
             size_t seen = 0;  // flags [0, seen) are set
             for (unsigned k = 0;; ++k) {
-                while (seen < nflags && __atomic_load_n(flag + seen, __ATOMIC_ACQUIRE) != 0)
+                while (seen < nflags && __atomic_load_n(flag + seen, __ATOMIC_ACQUIRE) == token)
                     ++seen;
                 if (seen == nflags) {
                     if (g_cstats.on)
@@ -1391,6 +1445,17 @@ struct StageCall {
         return 0;
     }
 };
+
+// completion tokens of per-record calls (StageCall::roundtrip): process-wide, nonzero, and consecutive calls on one
+// staging buffer never share one
+static std::atomic<u32> g_done_token{0};
+static u32 next_done_token(void)
+{
+    u32 t;
+    while ((t = g_done_token.fetch_add(1, std::memory_order_relaxed) + 1) == 0) {
+    }
+    return t;
+}
 
 // after a synchronous call on `ks` completed on a stager stream, its setup is complete too
 static void seen_ready(ptls_mi355x_keyset_t *ks) { ks->ready_seen.store(true, std::memory_order_release); }
@@ -1541,25 +1606,28 @@ static void run_calls(DeviceState *ds, OneCall *const *c, size_t n)
             // the caller need not spend spinning on a core)
             const bool flag = PERREC_FLAG && call.mapped() && c0.ks->schedule != PTLS_MI355X_SCHEDULE_LOCKSTEP &&
                               (total <= PERREC_FLAG_MAX_BYTES || span_n != 0);
+            // this call's completion token (never 0, and never the value an earlier call left in these words)
+            const u32 token = flag ? next_done_token() : 0u;
             if (flag)
                 memset(h + off_flag, 0, 4 * nflags);
             if (ret == 0)
                 ret = call.roundtrip(up, [&] {
                     if (span_n != 0) {
                         if (launch_span(kbase, nr, c0.ks->ct, open, first, d, d, d, d + off_ok, span_units, span_e, span_n, d + off_span,
-                                        flag && !hp ? (u32 *)(d + off_flag) : nullptr, s) != 0)
+                                        flag && !hp ? (u32 *)(d + off_flag) : nullptr, token, s) != 0)
                             return -1;
                     } else {
                         const HpLaunch hpl = {(const ptls_mi355x_hp_t *)(d + off_hp), hbase, hp_nkeys, hp_nr, d + off_mask};
                         if (launch_gcm(kbase, nkeys, nr, ds->ncu, c0.ks->schedule, c0.ks->ct, open, (const ptls_mi355x_record_t *)(d + off_rec),
                                        n, d, d, d, d + off_ok, s, 0, unit_log2, nullptr, nullptr, nullptr, n == 1 ? &first : nullptr,
-                                       flag && (!hp || hp_fused) ? (u32 *)(d + off_flag) : nullptr, nullptr, hp_fused ? &hpl : nullptr) != 0)
+                                       flag && (!hp || hp_fused) ? (u32 *)(d + off_flag) : nullptr, nullptr, hp_fused ? &hpl : nullptr,
+                                       nullptr, token) != 0)
                             return -1;
                     }
                     return !hp || hp_fused ? 0
                                : launch_hp(hbase, hp_nkeys, hp_nr, ds->ncu, (const ptls_mi355x_hp_t *)(d + off_hp), n, d, d + off_mask, s,
-                                           flag ? (u32 *)(d + off_flag) : nullptr);
-                }, flag ? off_flag : 0, nflags);
+                                           flag ? (u32 *)(d + off_flag) : nullptr, token);
+                }, flag ? off_flag : 0, nflags, token);
             if (ret == 0) {
                 out_at = up;
                 for (size_t i = 0; i < n; ++i) {

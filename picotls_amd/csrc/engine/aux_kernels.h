@@ -213,7 +213,7 @@ __global__ __launch_bounds__(256) void ecb_kernel(const KeyEntry *keys, u32 nkey
 // sample at base + hp[i].sample_off). Runs after the seal kernel on the same stream, so the sample may cover the tag.
 template <int NR>
 __global__ __launch_bounds__(256) void hp_kernel(const KeyEntry *keys, u32 nkeys, const ptls_mi355x_hp_t *hp, const uint8_t *base,
-                                                 uint8_t *masks, u64 n, u32 *done_flag)
+                                                 uint8_t *masks, u64 n, u32 *done_flag, u32 done_token)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     lds_u8 *lds = (lds_u8 *)smem;
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(256) void hp_kernel(const KeyEntry *keys, u32 nkeys
         }
         *(u32x4_u *)(masks + 16 * i) = o;
     }
-    publish_done(done_flag);  // (the per-record path: see gcm_chunked_kernel)
+    publish_done(done_flag, done_token);  // (the per-record path: see gcm_chunked_kernel)
 }
 
 // QUIC-LB connection-ID cipher (lib/quiclb-impl.h:100-162, behind ptls_fusion_quiclb lib/fusion.c:2186-2233): a 4-round

@@ -267,15 +267,17 @@ __device__ __forceinline__ void gf_mulx_be(u32 &b0, u32 &b1, u32 &b2, u32 &b3)
 }
 
 // The per-record path's completion words (BatchArgs::done_flag, hp_kernel): every wave's stores of the workgroup complete
-// at system scope, then one store per workgroup tells the host thread polling the mapped staging buffer
-__device__ __forceinline__ void publish_done(u32 *flags)
+// at system scope, then one store per workgroup tells the host thread polling the mapped staging buffer. The word is
+// the call's token (BatchArgs::done_token, never 0), not a constant: a word left set by an earlier call on the same
+// staging buffer cannot pass for this call's completion.
+__device__ __forceinline__ void publish_done(u32 *flags, u32 token)
 {
     if (flags == nullptr)
         return;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     __syncthreads();
     if (threadIdx.x == 0)
-        __hip_atomic_store(flags + blockIdx.x, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(flags + blockIdx.x, token, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 #endif  // PTLS_MI355X_ENGINE_COMMON_H

@@ -1083,7 +1083,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     }
     if (with_hp && hp_n != 0)  // the last run's masks
         HP_PASS(hp_pos, hp_pos + hp_n, threadIdx.x, blockDim.x);
-    publish_done(args.done_flag);  // the per-record path polls these instead of waiting for the stream
+    publish_done(args.done_flag, args.done_token);  // the per-record path polls these instead of waiting for the stream
 #undef HP_PASS
 }
 

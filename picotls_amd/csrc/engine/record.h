@@ -62,7 +62,7 @@ struct BatchArgs {
     // the kernel arguments; `recs` is not read)
     u32 one_inline;
     ptls_mi355x_record_t one;
-    // chunked kernel on the per-record path: workgroup w sets done_flag[w] to 1 (system scope) once every output byte
+    // chunked kernel on the per-record path: workgroup w sets done_flag[w] to done_token (system scope) once every output byte
     // it writes is written, for the host thread that polls them (null: none)
     u32 *done_flag;
     // chunked kernel: 0 = workgroup w walks the contiguous records [n*w/grid, n*(w+1)/grid); else it walks the chunks
@@ -88,6 +88,8 @@ struct BatchArgs {
     // chunked kernel, FRAME 0: the launch is a pair (launch_chunked): EXT 0 skips the W8 runs (whole-record runs of
     // records of W8_MIN_STEPS steps or more), EXT 3 processes only those
     u32 w8_split;
+    // the value each workgroup stores into done_flag[w] (the calling host thread's token for this call, never 0)
+    u32 done_token;
 };
 
 #define RUN_SCAN_CAP 256  // records examined per key-run scan (multi-key batches)

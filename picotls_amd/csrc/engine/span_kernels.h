@@ -82,6 +82,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
 // One workgroup: GHASH = sum_s part[s] M^s with M = (H^128)^(2^e), the record's tag: written after the ciphertext
 // (seal) or compared with the received one (open, ok[0]). Constant-time as it stands: every product is a gmul_tab in
 // which all threads read the same window row of the same table.
+static_assert(CHUNK_BLOCKS == 128, "span_combine_kernel takes M = H^(CHUNK_BLOCKS 2^e) from the keyset's H^128 .. H^1024");
 template <bool OPEN>
 __global__ __launch_bounds__(256) void span_combine_kernel(BatchArgs args, u32 nspans, u32 e, const u32x4 *part)
 {
@@ -134,7 +135,7 @@ __global__ __launch_bounds__(256) void span_combine_kernel(BatchArgs args, u32 n
             *(u32x4_u *)(args.out + r.out_off + r.len) = tag;
         }
     }
-    publish_done(args.done_flag);
+    publish_done(args.done_flag, args.done_token);
 }
 
 #endif  // PTLS_MI355X_ENGINE_SPAN_KERNELS_H

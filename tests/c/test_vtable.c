@@ -241,10 +241,39 @@ static int tls12_receive(ptls_aead_algorithm_t *aead, ptls_hash_algorithm_t *has
     return ret;
 }
 
-static void tls12_test(ptls_aead_algorithm_t *ours, ptls_aead_algorithm_t *ref, ptls_hash_algorithm_t *hash, const char *what)
+/* where two TLS 1.2 wire streams of `len` bytes of application data first differ: the record, the field (header, explicit
+ * nonce, ciphertext, tag) and how many bytes of the record's ciphertext and tag differ, so that a failure names its
+ * mechanism (a stale or partial result, a wrong nonce or key, a tag-only difference) */
+static void tls12_describe_diff(const char *what, const uint8_t *a, size_t alen, const uint8_t *b, size_t blen)
+{
+    size_t off = 0, rec = 0;
+    while (off < alen && off < blen) {
+        size_t rlen = alen - off < 5 ? 0 : ((size_t)a[off + 3] << 8 | a[off + 4]) + 5;
+        if (rlen == 0 || off + rlen > alen || off + rlen > blen)
+            break;
+        if (memcmp(a + off, b + off, rlen) != 0) {
+            size_t first = 0, nct = 0, ntag = 0;
+            while (a[off + first] == b[off + first])
+                ++first;
+            for (size_t i = 13; i < rlen; ++i)
+                if (a[off + i] != b[off + i])
+                    ++*(i < rlen - 16 ? &nct : &ntag);
+            const char *field = first < 5 ? "header" : first < 13 ? "explicit nonce" : first < rlen - 16 ? "ciphertext" : "tag";
+            printf("# %s: record %zu (wire offset %zu, %zu bytes) first differs at record offset %zu (%s); %zu of %zu ciphertext "
+                   "bytes and %zu of 16 tag bytes differ\n",
+                   what, rec, off, rlen, first, field, nct, rlen - 29, ntag);
+            return;
+        }
+        off += rlen, ++rec;
+    }
+    printf("# %s: streams of %zu and %zu bytes agree on their first %zu bytes (%zu records)\n", what, alen, blen, off, rec);
+}
+
+static int tls12_test(ptls_aead_algorithm_t *ours, ptls_aead_algorithm_t *ref, ptls_hash_algorithm_t *hash, const char *what)
 {
     static uint8_t data[40000];
     uint8_t ms[48], randoms[64];
+    const int nfail0 = nfail;
     rnd(ms, sizeof(ms));
     rnd(randoms, sizeof(randoms));
     rnd(data, sizeof(data));
@@ -259,15 +288,80 @@ static void tls12_test(ptls_aead_algorithm_t *ours, ptls_aead_algorithm_t *ref, 
     tls12_send(ours, hash, ms, randoms, data, sizeof(data), &a);
     tls12_send(ref, hash, ms, randoms, data, sizeof(data), &b);
     OK(a.off == b.off && memcmp(a.base, b.base, a.off) == 0, "%s", what);
-    OK(tls12_receive(ours, hash, ms, randoms, b.base, b.off, &pa) == 0 && pa.off == sizeof(data) &&
-           memcmp(pa.base, data, sizeof(data)) == 0,
-       "tls12 receive (mi355x) of fusion's records");
+    if (!(a.off == b.off && memcmp(a.base, b.base, a.off) == 0)) {
+        tls12_describe_diff(what, a.base, a.off, b.base, b.off);
+        printf("# engine's last error: %s\n", ptls_mi355x_last_error());
+    }
+    int rret = tls12_receive(ours, hash, ms, randoms, b.base, b.off, &pa);
+    OK(rret == 0 && pa.off == sizeof(data) && memcmp(pa.base, data, sizeof(data)) == 0, "tls12 receive (mi355x) of fusion's records");
+    if (!(rret == 0 && pa.off == sizeof(data) && memcmp(pa.base, data, sizeof(data)) == 0)) {
+        size_t first = 0;
+        while (first < pa.off && first < sizeof(data) && pa.base[first] == data[first])
+            ++first;
+        printf("# tls12 receive: ptls_receive returned %d after %zu plaintext bytes (%zu of them correct); record %zu failed "
+               "(16384-byte records)\n",
+               rret, pa.off, first, pa.off / 16384);
+        printf("# engine's last error: %s\n", ptls_mi355x_last_error());
+    }
     b.base[100] ^= 1;
     OK(tls12_receive(ours, hash, ms, randoms, b.base, b.off, &pb) == PTLS_ALERT_BAD_RECORD_MAC, "tls12 tampered record rejected");
     ptls_buffer_dispose(&a);
     ptls_buffer_dispose(&b);
     ptls_buffer_dispose(&pa);
     ptls_buffer_dispose(&pb);
+    return nfail - nfail0;
+}
+
+/* run as `test_vtable stress N`: N rounds of back-to-back 16 KiB per-record calls, the pattern of the round-3 failure
+ * (three records of one ptls_send through one staging buffer, then a receive): the TLS 1.2 exchange for both key sizes,
+ * and one context sealing and opening records of 16384, 16384 and 7232 bytes against fusion. Prints the first failures
+ * in detail and a count; exit status 0 iff none. */
+static int stress_main(int rounds)
+{
+    static uint8_t text[16384], aad[13], a[16400], b[16400], dec[16384];
+    int bad_rounds = 0, bad_records = 0;
+    for (int r = 0; r < rounds; ++r) {
+        int bad = tls12_test(&ptls_mi355x_non_temporal_aes128gcm, &ptls_non_temporal_aes128gcm, &ptls_openssl_sha256,
+                             "stress tls12 aes128gcm wire == fusion");
+        bad += tls12_test(&ptls_mi355x_non_temporal_aes256gcm, &ptls_non_temporal_aes256gcm, &ptls_openssl_sha384,
+                          "stress tls12 aes256gcm wire == fusion");
+        uint8_t key[16], iv[12];
+        rnd(key, sizeof(key)), rnd(iv, sizeof(iv));
+        ptls_aead_context_t *e = ptls_aead_new_direct(&ptls_mi355x_aes128gcm, 1, key, iv), *f = ptls_aead_new_direct(&ptls_fusion_aes128gcm, 1, key, iv),
+                            *d = ptls_aead_new_direct(&ptls_mi355x_aes128gcm, 0, key, iv);
+        static const size_t lens[3] = {16384, 16384, 7232};
+        for (int k = 0; k < 3; ++k) {
+            size_t len = lens[k];
+            rnd(text, len), rnd(aad, sizeof(aad));
+            ptls_aead_encrypt(e, a, text, len, (uint64_t)(3 * r + k), aad, sizeof(aad));
+            ptls_aead_encrypt(f, b, text, len, (uint64_t)(3 * r + k), aad, sizeof(aad));
+            int sealed_ok = memcmp(a, b, len + 16) == 0;
+            size_t got = ptls_aead_decrypt(d, dec, b, len + 16, (uint64_t)(3 * r + k), aad, sizeof(aad));
+            int opened_ok = got == len && memcmp(dec, text, len) == 0;
+            if (!sealed_ok || !opened_ok) {
+                ++bad_records;
+                if (bad_records <= 10) {
+                    size_t first = 0, nct = 0, ntag = 0;
+                    if (!sealed_ok) {
+                        while (a[first] == b[first])
+                            ++first;
+                        for (size_t i = 0; i < len + 16; ++i)
+                            if (a[i] != b[i])
+                                ++*(i < len ? &nct : &ntag);
+                    }
+                    printf("# stress round %d record %d (%zu B): seal %s (first diff %zu, %zu ct / %zu tag bytes), open %s; last error: %s\n",
+                           r, k, len, sealed_ok ? "ok" : "DIFFERS", first, nct, ntag, opened_ok ? "ok" : got == SIZE_MAX ? "REJECTED" : "WRONG",
+                           ptls_mi355x_last_error());
+                }
+            }
+        }
+        ptls_aead_free(e), ptls_aead_free(f), ptls_aead_free(d);
+        if (bad != 0)
+            ++bad_rounds;
+    }
+    printf("# stress: %d rounds, %d with a TLS 1.2 failure, %d per-record failures\n", rounds, bad_rounds, bad_records);
+    printf("1..%d\n# %d failed\n", ntest, nfail + bad_records);
+    return nfail == 0 && bad_records == 0 ? 0 : 1;
 }
 
 /* Distinct contexts are independent and need no locking (SURVEY 8(b) Threading, lib/picotls.c:6553-6568): threads that
@@ -411,6 +505,8 @@ int main(int argc, char **argv)
     }
     if (argc > 1 && strcmp(argv[1], "failclosed") == 0)
         return failclosed_main();
+    if (argc > 2 && strcmp(argv[1], "stress") == 0)
+        return stress_main(atoi(argv[2]));
     OK(strcmp(ptls_mi355x_aes128gcm.name, ptls_fusion_aes128gcm.name) == 0 && ptls_mi355x_aes128gcm.key_size == 16 &&
            ptls_mi355x_aes128gcm.iv_size == 12 && ptls_mi355x_aes128gcm.tag_size == 16 &&
            ptls_mi355x_aes128gcm.confidentiality_limit == ptls_fusion_aes128gcm.confidentiality_limit &&

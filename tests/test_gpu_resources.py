@@ -74,9 +74,15 @@ def test_picotls_contexts_are_constant_time_by_default(ref):
     key, iv = rng.bytes(32), rng.bytes(12)
     ctx = pa.aead_new_direct(pa.aes256gcm, True, key, iv)
     assert ctx.ks.constant_time
-    ks = pa.Keyset(key, iv, 32)  # batch keysets keep the engine's default (off unless PTLS_MI355X_CONSTANT_TIME=1)
-    assert ks.constant_time == (os.environ.get("PTLS_MI355X_CONSTANT_TIME") == "1")
+    # batch keysets too (round 4): constant-time unless PTLS_MI355X_CONSTANT_TIME=0, one-key and many-key alike
+    ks = pa.Keyset(key, iv, 32)
+    assert ks.constant_time == (os.environ.get("PTLS_MI355X_CONSTANT_TIME") != "0")
     ks.free()
+    many = pa.Keyset(rng.bytes(16 * 300), rng.bytes(12 * 300), 16)
+    assert many.constant_time == (os.environ.get("PTLS_MI355X_CONSTANT_TIME") != "0")
+    many.set_constant_time(False)  # the opt-out per keyset
+    assert not many.constant_time
+    many.free()
     # lengths around the per-record unit rules and the many-workgroup span path (from 256 KiB), all in CT mode
     for ln in (0, 1, 16, 200, 1200, 16384, 100000, (256 << 10) - 1, 256 << 10, (1 << 20) + 33):
         pt, aad, seq = rng.bytes(ln), rng.bytes(int(rng.integers(0, 30))), int(rng.integers(0, 2**62))

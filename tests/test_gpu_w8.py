@@ -1,0 +1,143 @@
+"""Whole-record runs of long records (the chunked kernel's W8 runs: Horner on an 8-bit window-major H^8 table,
+gcm_segment<..., W8>, launched as the EXT 3 half of a kernel pair beside the plain kernel, each skipping the other's
+runs; engine/common.h W8_HORNER) bit-exact against lib/fusion.c: one key and several, AES-128 and AES-256, the 64-step
+threshold inside one run, seal / open / tamper, in place, and batches that mix W8 runs with whole runs of short records
+and with cut runs of mixed lengths, so that both kernels of the pair do work and skip the other's. The reference's
+per-block GHASH amortisation is lib/fusion.c:515-620 (six blocks per reduction); the tests hold for any build (with
+W8_HORNER 0 the same records take the 4-bit path)."""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+import picotls_amd as pa  # noqa: E402
+from oracle import FusionRef  # noqa: E402
+from picotls_amd.records import RecordBatch  # noqa: E402
+from gpu_util import dev, empty, gpu_open, gpu_seal  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+HAVE_REF = os.path.exists(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
+                                       "libfusion_ref.so"))
+
+
+@pytest.fixture(scope="module")
+def ref():
+    assert torch.cuda.is_available(), "no GPU visible"
+    pa.load_library()
+    if not HAVE_REF:
+        pytest.skip("oracle/_ref/libfusion_ref.so not shipped")
+    return FusionRef()
+
+
+def _check(ref, rng, lens, aads, key_size, nkeys, tamper=8):
+    n = len(lens)
+    key_idx = np.sort(rng.integers(0, nkeys, n)) if nkeys > 1 else None
+    b = RecordBatch.build(np.asarray(lens), np.asarray(aads), seqs=rng.integers(0, 2**62, n, dtype=np.uint64),
+                          key_idx=key_idx)
+    keys = np.frombuffer(rng.bytes(nkeys * key_size), np.uint8)
+    ivs = np.frombuffer(rng.bytes(nkeys * 12), np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(max(b.aad_bytes, 1)), np.uint8)
+    ks = pa.Keyset(keys, ivs, key_size)
+    sealed = gpu_seal(ks, b.seal, pt, aad, b.sealed_bytes)
+    want = np.zeros(b.sealed_bytes, np.uint8)
+    ref.run_batch(True, keys, ivs, key_size, b.seal, pt, aad, want, nthreads=8)
+    bad_recs = [i for i in range(n) if not np.array_equal(
+        sealed[int(b.seal[i]["out_off"]):int(b.seal[i]["out_off"]) + int(lens[i]) + 16],
+        want[int(b.seal[i]["out_off"]):int(b.seal[i]["out_off"]) + int(lens[i]) + 16])]
+    assert bad_recs == [], f"{len(bad_recs)} records differ from fusion, first {bad_recs[:8]}"
+    assert np.array_equal(sealed, want)
+    # open fusion's records with tampering (ciphertext, tag, AAD bits); the plaintext is written either way, as fusion
+    bad, badaad = want.copy(), aad.copy()
+    victims = rng.choice(n, min(tamper, n), replace=False)
+    for t, v in enumerate(victims):
+        o, ln = int(b.open[v]["in_off"]), int(lens[v])
+        if t % 3 == 0:
+            bad[o + int(rng.integers(0, ln + 16))] ^= 1 << int(rng.integers(0, 8))
+        elif t % 3 == 1 or int(b.seal[v]["aad_len"]) == 0:
+            bad[o + ln + int(rng.integers(0, 16))] ^= 0x20
+        else:
+            badaad[int(b.seal[v]["aad_off"]) + int(rng.integers(0, int(b.seal[v]["aad_len"])))] ^= 2
+    back, ok = gpu_open(ks, b.open, bad, badaad, b.pt_bytes)
+    expect_ok = np.ones(n, np.uint8)
+    expect_ok[victims] = 0
+    assert np.array_equal(ok, expect_ok)
+    ref_back = np.zeros(b.pt_bytes, np.uint8)
+    ref.run_batch(False, keys, ivs, key_size, b.open, bad, badaad, ref_back, ok=np.zeros(n, np.uint8), nthreads=8)
+    assert np.array_equal(back, ref_back)
+    ks.free()
+
+
+@pytest.mark.parametrize("key_size,nkeys,n", [(16, 1, 2000), (32, 1, 700), (16, 5, 3000), (32, 3, 1500)])
+def test_w8_uniform_long_records_vs_fusion(ref, key_size, nkeys, n):
+    # 16 KiB TLS records (129 steps), one key (runs of up to 4096 records) and a few keys (runs cut at key changes)
+    rng = np.random.default_rng(8000 + key_size * 10 + nkeys)
+    _check(ref, rng, np.full(n, 16384), np.full(n, 13), key_size, nkeys)
+
+
+def test_w8_threshold_inside_a_run_vs_fusion(ref):
+    # lengths of 62..66 steps inside one uniform run (within its 2-step slack): the run's first record decides W8
+    rng = np.random.default_rng(8101)
+    n = 3000
+    lens = rng.integers(7800, 8400, n)
+    _check(ref, rng, lens, rng.integers(0, 30, n), 16, 1)
+
+
+def test_w8_mixed_with_short_and_cut_runs_vs_fusion(ref):
+    # blocks of 16 KiB records (W8 runs), of 1200-byte records (whole runs below 64 steps: the plain kernel) and of
+    # U[64, 16384] lengths (cut runs: the plain kernel), interleaved over the batch, so that every workgroup of both
+    # kernels of the pair meets both kinds of runs
+    rng = np.random.default_rng(8102)
+    blocks = []
+    for i in range(60):
+        kind = i % 3
+        blocks.append(np.full(300, 16384) if kind == 0 else np.full(300, 1200) if kind == 1 else rng.integers(64, 16385, 300))
+    lens = np.concatenate(blocks)
+    _check(ref, rng, lens, rng.integers(0, 20, len(lens)), 16, 1, tamper=30)
+
+
+def test_w8_aes256_many_keys_mixed_vs_fusion(ref):
+    rng = np.random.default_rng(8103)
+    lens = np.concatenate([np.full(1000, 16384), rng.integers(64, 16385, 1000), np.full(1000, 12000)])
+    _check(ref, rng, lens, np.full(len(lens), 13), 32, 7, tamper=20)
+
+
+def test_w8_in_place_vs_fusion(ref):
+    # seal in place (ciphertext over plaintext, tag after it) and open in place, 16 KiB records at odd offsets
+    rng = np.random.default_rng(8104)
+    n = 600
+    recs = np.zeros(n, dtype=pa.RECORD_DTYPE)
+    off, aoff = 5, 3
+    for i in range(n):
+        recs[i]["in_off"] = recs[i]["out_off"] = off
+        recs[i]["len"] = 16384
+        recs[i]["aad_off"], recs[i]["aad_len"] = aoff, 13
+        recs[i]["seq"] = 1000 + i
+        off += 16384 + 16 + int(rng.integers(0, 40))
+        aoff += 13 + int(rng.integers(0, 3))
+    keys, ivs = np.frombuffer(rng.bytes(16), np.uint8), np.frombuffer(rng.bytes(12), np.uint8)
+    arena = np.frombuffer(rng.bytes(off + 16), np.uint8).copy()
+    aad = np.frombuffer(rng.bytes(aoff + 1), np.uint8)
+    want = arena.copy()
+    ref.run_batch(True, keys, ivs, 16, recs, arena, aad, want, nthreads=8)
+    ks = pa.Keyset(keys, ivs, 16)
+    d_arena, d_recs, d_aad = dev(arena), dev(recs), dev(aad)
+    pa.seal_batch(ks, d_recs.data_ptr(), n, d_arena.data_ptr(), d_aad.data_ptr(), d_arena.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(d_arena.cpu().numpy(), want)
+    d_ok = empty(n, 0x55)
+    pa.open_batch(ks, d_recs.data_ptr(), n, d_arena.data_ptr(), d_aad.data_ptr(), d_arena.data_ptr(), d_ok.data_ptr())
+    torch.cuda.synchronize()
+    assert d_ok.cpu().numpy().all()
+    assert np.array_equal(d_arena.cpu().numpy()[:off], np.where(_record_mask(recs, off), arena[:off], want[:off]))
+    ks.free()
+
+
+def _record_mask(recs, size):
+    m = np.zeros(size, bool)
+    for r in recs:
+        m[int(r["in_off"]):int(r["in_off"]) + int(r["len"])] = True
+    return m

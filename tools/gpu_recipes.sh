@@ -9,6 +9,40 @@ set +e
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 recipe=$1; shift
 case "$recipe" in
+lasterr)
+  # HIP last-error semantics (tools/mb/lasterr.hip), then the full C vtable suite N times in fresh processes with the
+  # round-3 engine (its TLS 1.2 failure of GPUTEST_r03 came in one of three such processes)
+  (
+timeout -k 10 60 tools/variants/lasterr || exit $?
+N=${1:-20}; f=0
+for i in $(seq 1 $N); do
+  LD_LIBRARY_PATH=$PWD/tools/variants/r3 PTLS_MI355X_COMBINE=4 timeout -k 10 120 tests/c/_bin/test_vtable > gpurun_out/lasterr_r3_$i.log 2>&1; rc=$?
+  [ $rc -ne 0 ] && { f=$((f+1)); echo "== run $i rc=$rc"; grep -E '^(not ok|#)' gpurun_out/lasterr_r3_$i.log | head -20; }
+  [ $rc -gt 1 ] && exit $rc
+done
+echo "r3 full suite: $f of $N runs failed"
+exit 0
+  )
+  ;;
+race)
+  # round 4: the TLS 1.2 per-record failure of GPUTEST_r03 (test_vtable.c:261-262). Back-to-back 16 KiB per-record
+  # calls (test_vtable stress N) with the round-3 engine (tools/variants/r3, built from the round-3 sources), this
+  # engine with coarse-grained staging (PTLS_MI355X_STAGE_COHERENT=0) and this engine as shipped; then the full C suite
+  (
+B=tests/c/_bin/test_vtable; N=${1:-3000}
+for v in r3 coarse new; do
+  case $v in
+  r3) LD_LIBRARY_PATH=$PWD/tools/variants/r3 timeout -k 10 240 $B stress $N > gpurun_out/race_$v.log 2>&1; rc=$? ;;
+  coarse) PTLS_MI355X_STAGE_COHERENT=0 timeout -k 10 240 $B stress $N > gpurun_out/race_$v.log 2>&1; rc=$? ;;
+  new) timeout -k 10 240 $B stress $N > gpurun_out/race_$v.log 2>&1; rc=$? ;;
+  esac
+  echo "== $v rc=$rc"; grep '^#' gpurun_out/race_$v.log | tail -14
+  [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
+done
+timeout -k 10 300 $B > gpurun_out/race_full.log 2>&1; rc=$?; echo "== full suite rc=$rc"; tail -3 gpurun_out/race_full.log
+exit $rc
+  )
+  ;;
 bal)
   # byte-balanced workgroup ranges for many-key batches: GPU suite, then interleaved A/B (BALANCE=0 vs 1)
   (
