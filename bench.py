@@ -175,7 +175,8 @@ def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool
     seal_ms = float(np.mean([a.elapsed_time(bb) for a, bb, _ in ev]))
     open_ms = float(np.mean([bb.elapsed_time(c) for _, bb, c in ev]))
 
-    res = {"records": b.n, "payload_bytes": b.payload_bytes, "wall_s": wall, "seal_ms": seal_ms, "open_ms": open_ms}
+    res = {"records": b.n, "payload_bytes": b.payload_bytes, "wall_s": wall, "seal_ms": seal_ms, "open_ms": open_ms,
+           "shard": [begin, end]}
     lens = b.seal["len"]
     res["seal_alg_bytes"] = algorithmic_bytes(lens, b.seal["aad_len"], True)
     res["open_alg_bytes"] = algorithmic_bytes(lens, b.seal["aad_len"], False)
@@ -617,6 +618,7 @@ def main():
         "dtype": "u8",
         "data": "synthetic: splitmix64 payload (seed 0x5eed) generated on device; random-key AES-GCM",
         "config": {"workload": wl.name, "desc": wl.desc, "records_per_gpu": res["records"],
+                   "shards": [[int(a), int(z)] for a, z in R.gather(res["shard"])] if shard_global else None,
                    "record_len": wl.rec_len or "U[64,16384]", "aad_len": wl.aad_len,
                    "aead": f"AES-{8 * wl.key_size}-GCM", "keys": wl.nkeys,
                    "parallelism": f"{R.world} independent per-GPU record shards, no data-path collective",
@@ -662,6 +664,8 @@ def main():
                        "scaling": "strong" if name == "shard1200" else "weak", "n_gpus": R.world,
                        "records_total": int(R.sum(float(r2["records"]))),
                        "records_per_gpu": r2["records"], "record_len": w2.rec_len or "U[64,16384]",
+                       # every rank's [begin, end) of the global batch (strong scaling: together exactly [0, total))
+                       "shards": [[int(a), int(z)] for a, z in R.gather(r2["shard"])] if name == "shard1200" else None,
                        "aead": f"AES-{8 * w2.key_size}-GCM", "keys": w2.nkeys, "key_order": w2.key_order,
                        "seal_GiBps": round(r2["payload_bytes"] / (r2["seal_ms"] / 1e3) / 2**30, 3),
                        "open_GiBps": round(r2["payload_bytes"] / (r2["open_ms"] / 1e3) / 2**30, 3),

@@ -64,6 +64,11 @@ static int fail(const char *fmt, const char *detail)
     return -1;
 }
 
+// Kernel launches are checked with hipGetLastError, which also returns the error of any earlier call of this thread
+// whose failure was handled (a failed hipHostGetDevicePointer, for one: tools/mb/lasterr.hip showed that error reported
+// after a good launch). LAUNCH_CLEAR() before a launch makes the check after it about that launch only.
+#define LAUNCH_CLEAR() ((void)hipGetLastError())
+
 #define HIP_TRY(expr)                                                                                                         \
     do {                                                                                                                      \
         hipError_t e_ = (expr);                                                                                               \
@@ -484,6 +489,9 @@ struct st_ptls_mi355x_keyset_t {
     uint8_t *d_spread;
     hipStream_t spread_stream;
     bool spread_used;
+    // W8 launch pairs (launch_chunked, W8_HORNER): one word per workgroup from the pair's first kernel to its second,
+    // allocated on first use; ordered across streams like the spread scratch (spread_stream / spread_used)
+    u32 *d_w8flags;
 };
 
 static int mark_ready(ptls_mi355x_keyset_t *ks, hipStream_t s);
@@ -497,6 +505,7 @@ static int setup_now(ptls_mi355x_keyset_t *ks, hipStream_t s)
     std::lock_guard<std::mutex> lk(ks->mu);
     if (!ks->pending.load(std::memory_order_relaxed))
         return 0;
+    LAUNCH_CLEAR();
     keyset_setup_one_kernel<<<1, 64, 0, s>>>(ks->raw, ks->d_keys);
     if (hipGetLastError() != hipSuccess)
         return fail("%s", "keyset setup launch failed");
@@ -646,6 +655,7 @@ ptls_mi355x_keyset_t *ptls_mi355x_keyset_new(const void *keys, const void *ivs, 
               hipMemcpyAsync(d_raw, keys, nkeys * key_size, hipMemcpyHostToDevice, ds->setup) == hipSuccess &&
               hipMemcpyAsync(d_raw + nkeys * key_size, ivs, nkeys * 12, hipMemcpyHostToDevice, ds->setup) == hipSuccess;
     if (ok) {
+        LAUNCH_CLEAR();
         keyset_setup_kernel<<<(unsigned)((nkeys + 127) / 128), 128, 0, ds->setup>>>(d_raw, d_raw + nkeys * key_size, ks->d_keys,
                                                                                    (u32)nkeys, (u32)key_size);
         ok = hipGetLastError() == hipSuccess;
@@ -693,6 +703,7 @@ int ptls_mi355x_keyset_update(ptls_mi355x_keyset_t *ks, const uint32_t *key_idx,
     if (hipMemcpyAsync(d, keys, kb, hipMemcpyHostToDevice, ds->maint) == hipSuccess &&
         hipMemcpyAsync(d + kb, ivs, ib, hipMemcpyHostToDevice, ds->maint) == hipSuccess &&
         hipMemcpyAsync(d + kb + ib, key_idx, sb, hipMemcpyHostToDevice, ds->maint) == hipSuccess) {
+        LAUNCH_CLEAR();
         keyset_setup_kernel<<<(unsigned)((n + 127) / 128), 128, 0, ds->maint>>>(d, d + kb, ks->d_keys, (u32)n, (u32)ks->key_size,
                                                                                (const u32 *)(d + kb + ib));
         if (hipGetLastError() == hipSuccess && mark_ready(ks, ds->maint) == 0)
@@ -745,6 +756,8 @@ void ptls_mi355x_keyset_free(ptls_mi355x_keyset_t *ks)
         (void)hipFreeAsync(ks->d_group, ds->maint);
     if (ks->d_spread != nullptr)
         (void)hipFreeAsync(ks->d_spread, ds->maint);
+    if (ks->d_w8flags != nullptr)
+        (void)hipFreeAsync(ks->d_w8flags, ds->maint);
     if (ks->slot) {
         // back to the pool once the clear has run (slot_get checks the event)
         hipEvent_t cleared = event_get(ds);
@@ -851,6 +864,7 @@ int ptls_mi355x_keyset_set_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, const vo
         return -1;
     u32 w[3];
     memcpy(w, iv, 12);
+    LAUNCH_CLEAR();
     keyset_set_iv_kernel<<<1, 1, 0, ks->ds->maint>>>(ks->d_keys + key_idx, w[0], w[1], w[2]);
     HIP_TRY(hipGetLastError());
     if (mark_ready(ks, ks->ds->maint) != 0)
@@ -953,11 +967,12 @@ static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int sche
                       hipStream_t s, int frame, u32 unit_log2, const ptls_mi355x_record_t *grouped = nullptr,
                       const u32 *perm = nullptr, const u32 *perm_on = nullptr, const ptls_mi355x_record_t *one = nullptr,
                       u32 *done_flag = nullptr, const u64 *bounds = nullptr, const HpLaunch *hpl = nullptr,
-                      uint8_t *spread = nullptr, u32 done_token = 0)
+                      uint8_t *spread = nullptr, u32 done_token = 0, u32 *w8_flags = nullptr)
 {
     BatchArgs a = {keys, recs, (u64)nrecs, (const uint8_t *)in, (const uint8_t *)aad, (uint8_t *)out, ok,
                    nkeys > 1 ? 1u : 0u, nkeys, unit_log2, grouped, perm, perm_on, 0u, {}, done_flag, 0, bounds};
     a.done_token = done_token;
+    a.w8_flags = w8_flags;
     if (hpl != nullptr) {
         if (open || frame != 0 || !(ct || use_chunked(schedule)))
             return fail("%s", "launch_gcm: header-protection masks need the chunked seal of unframed records");
@@ -1071,10 +1086,15 @@ static bool spread_eligible(const ptls_mi355x_keyset_t *ks, size_t nrecs, int fr
     return frame == 0 && nrecs >= 2 && nrecs < (size_t)ks->ds->ncu && nrecs <= SPREAD_MAX_RECS && (ks->ct || use_chunked(ks->schedule));
 }
 
-// the keyset's spread scratch for a launch on `s` (allocated and zeroed in stream order on first use); nullptr on
-// failure. The caller holds ks->mu from here through the launch and the use event recorded after it (launch_batch),
-// so a launch on another stream always finds the previous user's event recorded.
-static uint8_t *spread_scratch_locked(ptls_mi355x_keyset_t *ks, hipStream_t s)
+// a batch that may launch the W8 pair (launch_chunked): unframed, chunked, at least one whole-record run's worth
+static bool w8_eligible(const ptls_mi355x_keyset_t *ks, size_t nrecs, int frame)
+{
+    return W8_HORNER && frame == 0 && nrecs >= WHOLE_MIN_RECS && (ks->ct || use_chunked(ks->schedule));
+}
+
+// orders a launch on `s` that uses the keyset's scratch (spread pieces, W8 flags) after the last launch that used it;
+// the caller holds ks->mu from here through the launch and the use event recorded after it (launch_batch)
+static int scratch_order_locked(ptls_mi355x_keyset_t *ks, hipStream_t s)
 {
     // a launch on another stream than the last user waits for that launch (its use event, recorded after it by
     // note_use_locked); back-to-back launches on one stream add no event packets (a wait and a record per launch cost a
@@ -1082,10 +1102,33 @@ static uint8_t *spread_scratch_locked(ptls_mi355x_keyset_t *ks, hipStream_t s)
     if (ks->spread_used && ks->spread_stream != s) {
         for (auto &u : ks->uses)
             if (u.first == ks->spread_stream && hipStreamWaitEvent(s, u.second, 0) != hipSuccess)
-                return nullptr;
+                return -1;
     }
     ks->spread_stream = s;
     ks->spread_used = true;
+    return 0;
+}
+
+// the keyset's W8 flag words for a launch on `s` (allocated in stream order on first use; every word is written by
+// the pair's first kernel before its second reads it); nullptr on failure (the pair then runs without them)
+static u32 *w8_flags_locked(ptls_mi355x_keyset_t *ks, hipStream_t s)
+{
+    if (scratch_order_locked(ks, s) != 0)
+        return nullptr;
+    if (ks->d_w8flags == nullptr && hipMallocAsync((void **)&ks->d_w8flags, 4 * (size_t)ks->ds->ncu, s) != hipSuccess) {
+        (void)hipGetLastError();
+        ks->d_w8flags = nullptr;
+    }
+    return ks->d_w8flags;
+}
+
+// the keyset's spread scratch for a launch on `s` (allocated and zeroed in stream order on first use); nullptr on
+// failure. The caller holds ks->mu from here through the launch and the use event recorded after it (launch_batch),
+// so a launch on another stream always finds the previous user's event recorded.
+static uint8_t *spread_scratch_locked(ptls_mi355x_keyset_t *ks, hipStream_t s)
+{
+    if (scratch_order_locked(ks, s) != 0)
+        return nullptr;
     if (ks->d_spread == nullptr) {
         const size_t bytes = spread_bytes(ks->ds->ncu);
         if (hipMallocAsync((void **)&ks->d_spread, bytes, s) != hipSuccess)
@@ -1112,6 +1155,7 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
     hipStream_t s = (hipStream_t)stream;
     if (wait_ready(ks, s) != 0)
         return -1;
+    LAUNCH_CLEAR();  // (the grouping kernels and launch_gcm's launch are checked after this)
     // ungrouped many-key batches: group the records by key on the device first (see key_hist_kernel)
 #ifndef KEY_GROUP_DISABLE
     const bool group = use_chunked(ks->schedule) && ks->nkeys > 1 && ks->nkeys <= KEY_GROUP_MAX_KEYS && nrecs > 1 &&
@@ -1125,9 +1169,13 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
     std::unique_lock<std::mutex> lk(ks->mu, std::defer_lock);
     // small batches with long records: the spread scratch
     uint8_t *spread = nullptr;
+    u32 *w8flags = nullptr;
     if (hpl == nullptr && spread_eligible(ks, nrecs, frame)) {
         lk.lock();
         spread = spread_scratch_locked(ks, s);
+    } else if (hpl == nullptr && w8_eligible(ks, nrecs, frame)) {  // (a spread launch never takes the W8 pair)
+        lk.lock();
+        w8flags = w8_flags_locked(ks, s);
     }
     if (group) {
         if (!lk.owns_lock())
@@ -1166,12 +1214,12 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
             balance_bounds_kernel<<<1, 1024, 0, s>>>(tiles, nrecs, grid, bounds);
         }
         ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, ks->ct, open, recs, nrecs, in, aad, out, ok, s,
-                         frame, CHUNK_LOG2, grouped, perm, ctl + 1, nullptr, nullptr, bounds, hpl, spread);
+                         frame, CHUNK_LOG2, grouped, perm, ctl + 1, nullptr, nullptr, bounds, hpl, spread, 0, w8flags);
         if (ret == 0)
             HIP_TRY(hipEventRecord(ks->group_ev, s));
     } else {
         ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, ks->ct, open, recs, nrecs, in, aad, out, ok,
-                         s, frame, CHUNK_LOG2, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, hpl, spread);
+                         s, frame, CHUNK_LOG2, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, hpl, spread, 0, w8flags);
     }
     if (ret != 0)
         return -1;
@@ -1187,6 +1235,7 @@ static unsigned aux_grid(size_t n, int ncu)
 static int launch_ecb(const KeyEntry *keys, u32 nkeys, int nr, int ncu, const uint32_t *key_idx, const void *in, void *out,
                       size_t nblocks, hipStream_t s)
 {
+    LAUNCH_CLEAR();
     if (nr == 10)
         ecb_kernel<10><<<aux_grid(nblocks, ncu), 256, LDS_AES_BYTES, s>>>(keys, nkeys, key_idx, (const uint8_t *)in, (uint8_t *)out,
                                                                           nblocks);
@@ -1200,6 +1249,7 @@ static int launch_ecb(const KeyEntry *keys, u32 nkeys, int nr, int ncu, const ui
 static int launch_hp(const KeyEntry *keys, u32 nkeys, int nr, int ncu, const ptls_mi355x_hp_t *hp, size_t n, const void *base,
                      void *masks, hipStream_t s, u32 *done_flag = nullptr, u32 done_token = 0)
 {
+    LAUNCH_CLEAR();
     if (nr == 10)
         hp_kernel<10><<<aux_grid(n, ncu), 256, LDS_AES_BYTES, s>>>(keys, nkeys, hp, (const uint8_t *)base, (uint8_t *)masks, n, done_flag,
                                                                     done_token);
@@ -1252,6 +1302,7 @@ int ptls_mi355x_open_tls_records(ptls_mi355x_keyset_t *ks, const ptls_mi355x_rec
     if (nrecs == 0)
         return 0;
     DeviceScope scope(ks->device);
+    LAUNCH_CLEAR();
     tls_unpad_kernel<<<aux_grid(nrecs, ks->ds->ncu), 256, 0, (hipStream_t)stream>>>(recs, nrecs, (const uint8_t *)in,
                                                                                      (const uint8_t *)out, ok, results);
     HIP_TRY(hipGetLastError());
@@ -1272,6 +1323,7 @@ int ptls_mi355x_open_tls12_records(ptls_mi355x_keyset_t *ks, const ptls_mi355x_r
     if (nrecs == 0)
         return 0;
     DeviceScope scope(ks->device);
+    LAUNCH_CLEAR();
     tls12_check_kernel<<<aux_grid(nrecs, ks->ds->ncu), 256, 0, (hipStream_t)stream>>>(recs, nrecs, (const uint8_t *)in, ok,
                                                                                        results);
     HIP_TRY(hipGetLastError());
@@ -1330,6 +1382,7 @@ int ptls_mi355x_quiclb_batch(ptls_mi355x_keyset_t *ks, const ptls_mi355x_cid_t *
     hipStream_t s = (hipStream_t)stream;
     if (wait_ready(ks, s) != 0)
         return -1;
+    LAUNCH_CLEAR();
     quiclb_kernel<10><<<aux_grid(n, ks->ds->ncu), 256, LDS_AES_BYTES, s>>>(ks->d_keys, (u32)ks->nkeys, cids, (const uint8_t *)in,
                                                                             (uint8_t *)out, n);
     HIP_TRY(hipGetLastError());
@@ -1410,9 +1463,7 @@ struct StageCall {
         const bool copy = st->h_dev == nullptr;
         if (copy)
             HIP_TRY(hipMemcpyAsync(st->d, st->h, up, hipMemcpyHostToDevice, st->stream));
-        // the launches are checked with hipGetLastError: no error an earlier call of this thread left (and handled)
-        // may pass for theirs
-        (void)hipGetLastError();
+        LAUNCH_CLEAR();  // (the launches below are checked with hipGetLastError)
         if (launch() != 0) {
             // a kernel of this call may already be queued (the span launch before its combine, the GCM launch before
             // the header-protection one): the buffer is cleared and reused only once nothing of it is in flight

@@ -144,7 +144,7 @@ __device__ __forceinline__ u32 lane_here()
 // W8 runs (whole records of at least W8_MIN_STEPS steps, gcm_chunked_kernel): H^8 as an 8-bit table over slots 0..7,
 // H in slot 8, H^2 in the partial region after the E(K, J0) slots of the groups
 #ifndef W8_HORNER
-#define W8_HORNER 0  // (late round 3: +13 % on 16 KiB records in an interleaved A/B; on by default once its suite has run)
+#define W8_HORNER 1  // (round 4: on; interleaved A/B +13.1 % tls16k, +8.5 % AES-256 16 KiB, quic1200 and mixed within ±0.4 %, profiles/r4/w8_ab.txt)
 #endif
 #ifndef W8_MIN_STEPS
 #define W8_MIN_STEPS 64

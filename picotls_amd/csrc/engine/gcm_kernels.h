@@ -744,6 +744,12 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     const u32 tsel_chunk = 0x10000u + 8u * GHASH_TABLE_BYTES;
 
     const u64 n = args.nrecs, C = args.bounds != nullptr ? 0 : args.chunk;
+    constexpr bool W8K = W8_HORNER && FRAME == 0 && EXT == 3;  // the launch pair's W8 half (launch_chunked)
+    if constexpr (W8K) {  // none of this workgroup's runs is a W8 run (the EXT 0 kernel saw them all): nothing to do
+        if (args.w8_flags != nullptr && args.w8_flags[blockIdx.x] == 0)
+            return;
+    }
+    bool skipped_w8 = false;  // (the EXT 0 kernel of a pair: this workgroup left a W8 run to the EXT 3 one)
     constexpr bool SPREAD = FRAME == 0 && EXT == 1;
     if constexpr (SPREAD) {  // a small one-key batch (spread_pieces): workgroup w < n takes record w unless it is long
         if (blockIdx.x >= n) {
@@ -758,7 +764,6 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     u64 cstart = beg;
     u32 loaded_key = 0xffffffffu, loaded_usrc = 0xffffffffu;
     bool loaded_w8 = false;  // the LDS holds the W8 tables (an 8-bit H^8 table, H, H^2) instead of the nine 4-bit ones
-    constexpr bool W8K = W8_HORNER && FRAME == 0 && EXT == 3;  // the launch pair's W8 half (launch_chunked)
     // the descriptors in batch order, or (an ungrouped many-key batch) the key-grouped copy built on the device; ok
     // bytes go to the record's batch index either way
     const ptls_mi355x_record_t *recs = args.recs;
@@ -857,6 +862,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             const bool w8 = whole && key_idx < args.nkeys &&
                             __builtin_amdgcn_readfirstlane(gcm_steps<OPEN, FRAME>(recs[pos]) >= W8_MIN_STEPS ? 1u : 0u) != 0;
             if (w8 != W8K) {
+                skipped_w8 = true;
                 if (wave == 0 && nxt < nxt_end)
                     scan_run<OPEN, FRAME, false, EXT>(args, recs, nxt, nxt_end, rs_next);
                 __syncthreads();
@@ -1083,6 +1089,10 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     }
     if (with_hp && hp_n != 0)  // the last run's masks
         HP_PASS(hp_pos, hp_pos + hp_n, threadIdx.x, blockDim.x);
+    if constexpr (W8_HORNER && FRAME == 0 && EXT == 0) {  // for the EXT 3 kernel of the pair (workgroup-uniform)
+        if (args.w8_split && args.w8_flags != nullptr && threadIdx.x == 0)
+            args.w8_flags[blockIdx.x] = skipped_w8 ? 1u : 0u;
+    }
     publish_done(args.done_flag, args.done_token);  // the per-record path polls these instead of waiting for the stream
 #undef HP_PASS
 }

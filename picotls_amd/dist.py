@@ -73,6 +73,20 @@ class RankContext:
     def sum(self, x: float) -> float:
         return self._reduce(x, None if self.dist is None else self.dist.ReduceOp.SUM)
 
+    def gather(self, values) -> list:
+        """Every rank's `values` (a few numbers), in rank order, on every rank: a sum reduction of a world x k array in
+        which each rank fills its own row (used to report the shards' record ranges; not a data-path collective)."""
+        vals = [float(v) for v in values]
+        if self.dist is None:
+            return [vals]
+        import torch
+
+        dev = self.device if (self.device is not None and self.dist.get_backend() == "nccl") else "cpu"
+        t = torch.zeros((self.world, len(vals)), dtype=torch.float64, device=dev)
+        t[self.rank] = torch.tensor(vals, dtype=torch.float64, device=dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return t.cpu().tolist()
+
     @property
     def backend(self):
         return self.dist.get_backend() if self.dist is not None else None

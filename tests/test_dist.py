@@ -57,8 +57,26 @@ def _worker(rank, world, port, workload, nrecs, q):
     value, wall = aggregate_throughput(ctx, b.payload_bytes, float(ctx.rank + 1), 1)
     gathered = [None] * ctx.world
     ctx.dist.all_gather_object(gathered, (begin, end, sealed_records, b.payload_bytes))
+    ranges = ctx.gather([begin, end])  # what bench.py reports as "shards"
     if ctx.rank == 0:
-        q.put((gathered, value, wall))
+        q.put((gathered, value, wall, ranges))
+    ctx.close()
+
+
+def _ranges_worker(rank, world, port, nrecs, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from picotls_amd.dist import RankContext, shard_for_rank
+
+    ctx = RankContext.from_env("gloo")
+    begin, end = shard_for_rank(nrecs, ctx.rank, ctx.world)
+    ranges = ctx.gather([begin, end])
+    total = ctx.sum(float(end - begin))
+    if ctx.rank == 0:
+        q.put((ranges, total))
     ctx.close()
 
 
@@ -76,12 +94,13 @@ def test_two_rank_shards_reproduce_single_process(workload, nrecs):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, workload, nrecs, q)) for r in range(2)]
     for p in procs:
         p.start()
-    gathered, value, wall = q.get(timeout=240)
+    gathered, value, wall, ranges = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     # shards are disjoint, ordered and cover the batch
     assert gathered[0][0] == 0 and gathered[0][1] == gathered[1][0] and gathered[1][1] == nrecs
+    assert [[int(a), int(z)] for a, z in ranges] == [[g[0], g[1]] for g in gathered]
     # bit-identical to the single-process batch
     wl = WORKLOADS[workload].scaled(nrecs)
     gb = wl.descriptors(0, nrecs)
@@ -95,3 +114,22 @@ def test_two_rank_shards_reproduce_single_process(workload, nrecs):
     total = gathered[0][3] + gathered[1][3]
     assert wall == 2.0
     assert value == pytest.approx(2 * total / 2.0 / 2**30)
+
+
+def test_eight_rank_shards_cover_configs4_once():
+    """configs[4]'s record index space (here 32M / 2^10 records) over eight gloo ranks: contiguous shards, each index
+    exactly once, gathered on rank 0 as bench.py reports them (the 8-GPU line's "shards")."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    nrecs = (32 << 20) >> 10
+    procs = [ctx.Process(target=_ranges_worker, args=(r, 8, port, nrecs, q)) for r in range(8)]
+    for p in procs:
+        p.start()
+    ranges, total = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ranges = [[int(a), int(z)] for a, z in ranges]
+    assert ranges[0][0] == 0 and ranges[-1][1] == nrecs and total == nrecs
+    assert all(ranges[i][1] == ranges[i + 1][0] for i in range(7))

@@ -45,6 +45,27 @@ def test_bench_self_launches_two_ranks_with_shard1200_leg():
     assert out["cpu_baseline"] is None  # rank 0 at N = 1 only
 
 
+def test_bench_eight_ranks_shard_the_configs4_index_space_once():
+    """The driver's N = 8 run rehearsed on one GPU: `bench.py --gpus 8` through the
+    self-launcher, eight gloo ranks on cuda:0. The configs[4] leg's global batch is split into eight contiguous shards
+    that cover its record index space exactly once, every rank's shard round-trips, and the line reports all ranks."""
+    records = 1024
+    out = _run(["--gpus", "8", "--steps", "1", "--warmup", "1", "--records", str(records), "--extra", "shard1200",
+                "--no-cpu-baseline", "--no-e2e"], timeout=600)
+    assert out["n_gpus"] == 8 and out["config"]["dist_backend"] == "gloo"
+    assert out["verified"]["roundtrip"] is True
+    sh = out["extra"]["shard1200"]
+    assert sh["n_gpus"] == 8 and sh["scaling"] == "strong" and sh["verified"]["roundtrip"] is True
+    total = records * 16384 // 1200
+    assert sh["records_total"] == total
+    shards = sh["shards"]
+    assert len(shards) == 8
+    assert shards[0][0] == 0 and shards[-1][1] == total
+    assert all(shards[i][1] == shards[i + 1][0] for i in range(7))  # contiguous: every index exactly once
+    assert all(z - a in (total // 8, total - 7 * (total // 8)) for a, z in shards)
+    assert sh["value"] > 0 and out["value"] > 0
+
+
 def test_bench_single_gpu_line_has_shard1200_by_default():
     """The default --extra list includes configs[4] (N = 1 anchor of the scaling curve)."""
     out = _run(["--steps", "1", "--warmup", "1", "--records", "1024", "--no-cpu-baseline", "--extra", "shard1200"])

@@ -9,6 +9,18 @@ set +e
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 recipe=$1; shift
 case "$recipe" in
+w8ab)
+  # round 4: the 8-bit Horner table (W8_HORNER=1, tools/variants/lib_w8.so) against the same source without it
+  # (lib_now8.so), interleaved in one process per workload (tools/ab.py: identical sealed output checked)
+  (
+V="tools/variants/lib_now8.so tools/variants/lib_w8.so"
+for w in "tls16k 1048576" "quic1200 4194304" "mixed 4194304" "mixedrand 4194304" "tls16k256 524288" "mixed1key 2097152"; do set -- $w
+  timeout -k 10 300 python tools/ab.py $V --workload $1 --records $2 --rounds 6 --reps 2 > gpurun_out/w8ab_$1.log 2>&1; rc=$?
+  echo "== $1 rc=$rc"; grep -v amdgpu.ids gpurun_out/w8ab_$1.log | tail -3; [ $rc -ne 0 ] && exit $rc
+done
+exit 0
+  )
+  ;;
 lasterr)
   # HIP last-error semantics (tools/mb/lasterr.hip), then the full C vtable suite N times in fresh processes with the
   # round-3 engine (its TLS 1.2 failure of GPUTEST_r03 came in one of three such processes)
