@@ -909,7 +909,10 @@ static void launch_chunked(bool ct, unsigned grid, hipStream_t s, const BatchArg
         // runs to the plain one; each skips the other's runs (a batch of fewer records than a whole run has none)
         // (not for a per-record launch that publishes completion words: the host would see them when the first kernel
         // of the pair ends, before the second has sealed its runs)
-        if (W8_HORNER && !a.one_inline && a.done_flag == nullptr && a.nrecs >= WHOLE_MIN_RECS) {
+        // (and only when some workgroup can hold a whole-record run: a batch of fewer than WHOLE_MIN_RECS records per
+        // workgroup in contiguous ranges has none, and the pair's second launch would cost such a small batch ~9 %)
+        const bool whole_possible = a.chunk != 0 || a.bounds != nullptr || (a.nrecs + grid - 1) / grid >= WHOLE_MIN_RECS;
+        if (W8_HORNER && !a.one_inline && a.done_flag == nullptr && whole_possible) {
             BatchArgs b = a;
             b.w8_split = 1;
             launch_chunked_x<NR, OPEN, 0>(ct, grid, s, b);

@@ -9,6 +9,31 @@ set +e
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 recipe=$1; shift
 case "$recipe" in
+prof4)
+  # round 4, the shipped build (W8 on, constant-time default) at the full BASELINE sizes: kernel trace + stats and the
+  # separate PMC passes of tools/gpu_prof.sh for each batch config
+  (
+for wn in "tls16k 1048576" "quic1200 4194304" "mixed 4194304"; do set -- $wn
+  bash tools/gpu_prof.sh $1 $2 r4 || exit $?
+done
+exit 0
+  )
+  ;;
+ct5)
+  # round 4: every keyset constant-time by default; LDS counters of the batch kernels at the full BASELINE sizes for
+  # two keys x two payloads (one rocprofv3 pass per process, 2 dispatches each of seal and open)
+  (
+R=$GRAFT_REPO_ROOT; cd /tmp && export TMPDIR=/tmp
+for wn in "tls16k 1048576" "quic1200 4194304" "mixed 4194304"; do set -- $wn
+for k in 1 2; do for pl in zero random; do
+  timeout -k 10 240 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS --output-format csv -d $R/gpurun_out/ct5/$1_k${k}_$pl -o p -- python3 $R/tools/ct_probe.py --workload $1 --records $2 --key-seed $k --payload $pl --reps 2 > $R/gpurun_out/ct5_$1_k${k}_$pl.log 2>&1
+  rc=$?; echo "$1 $k $pl rc=$rc"; [ $rc -ne 0 ] && { tail -5 $R/gpurun_out/ct5_$1_k${k}_$pl.log; exit $rc; }
+done; done; done
+cd $R
+python3 tools/ct_summary.py gpurun_out/ct5 > gpurun_out/ct5_batch.txt; cat gpurun_out/ct5_batch.txt
+exit 0
+  )
+  ;;
 w8ab)
   # round 4: the 8-bit Horner table (W8_HORNER=1, tools/variants/lib_w8.so) against the same source without it
   # (lib_now8.so), interleaved in one process per workload (tools/ab.py: identical sealed output checked)
