@@ -627,6 +627,9 @@ def main():
         "open_GiBps": round(res["payload_bytes"] / open_s / 2**30, 3),
         "roofline": {"bound": "hbm", "kernel": f"{'gcm_batch_kernel' if args.schedule == 'lockstep' else 'gcm_chunked_kernel'}"
                                                f"<{10 if wl.key_size == 16 else 14},seal>",
+                     # (one seal launch is the W8 pair, EXT 0 + EXT 3, when a workgroup can hold whole-record runs:
+                     # avg_launch_ms covers both, and profiles/pmc_<workload>.json sums their bytes)
+                     "launch": "w8 pair" if args.schedule != "lockstep" and res["records"] >= 256 * 128 else "single",
                      "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic_from_profiles(wl.name, res["records"]),
                      "alg_bytes_per_launch": res["seal_alg_bytes"], "avg_launch_ms": round(res["seal_ms"], 4),

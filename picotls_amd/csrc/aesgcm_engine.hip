@@ -487,6 +487,7 @@ struct st_ptls_mi355x_keyset_t {
     // between launches), allocated on first use; spread_stream: the stream of the last launch that used them (a launch
     // on another stream waits for that one's use event, note_use)
     uint8_t *d_spread;
+    size_t spread_cap;  // its bytes (sized for the batches seen so far, spread_bytes)
     hipStream_t spread_stream;
     bool spread_used;
     // W8 launch pairs (launch_chunked, W8_HORNER): one word per workgroup from the pair's first kernel to its second,
@@ -1079,9 +1080,9 @@ static int launch_span(const KeyEntry *key, int nr, bool ct, bool open, const pt
 }
 
 // (pieces of a record: at most its units / 2^10 + 1, 2^23 / SPREAD_UNIT_STEPS / 2^10 + 1 for the longest record)
-static size_t spread_bytes(int ncu)
+static size_t spread_bytes(int ncu, size_t nrecs)
 {
-    return SPREAD_CNT_BYTES + 16 * ((size_t)ncu + (size_t)SPREAD_MAX_RECS * (8192 / SPREAD_UNIT_STEPS + 1));
+    return SPREAD_CNT_BYTES + 16 * ((size_t)ncu + nrecs * (8192 / SPREAD_UNIT_STEPS + 1));
 }
 
 static bool spread_eligible(const ptls_mi355x_keyset_t *ks, size_t nrecs, int frame)
@@ -1128,19 +1129,31 @@ static u32 *w8_flags_locked(ptls_mi355x_keyset_t *ks, hipStream_t s)
 // the keyset's spread scratch for a launch on `s` (allocated and zeroed in stream order on first use); nullptr on
 // failure. The caller holds ks->mu from here through the launch and the use event recorded after it (launch_batch),
 // so a launch on another stream always finds the previous user's event recorded.
-static uint8_t *spread_scratch_locked(ptls_mi355x_keyset_t *ks, hipStream_t s)
+static uint8_t *spread_scratch_locked(ptls_mi355x_keyset_t *ks, hipStream_t s, size_t nrecs)
 {
     if (scratch_order_locked(ks, s) != 0)
         return nullptr;
+    // sized for this batch's records (16 B x (CUs + 1025 pieces per record), 164 KiB for 10 records
+    // instead of 4.2 MB for the largest batch), grown in stream order when a batch needs more
+    const size_t bytes = spread_bytes(ks->ds->ncu, nrecs);
+    if (ks->d_spread != nullptr && ks->spread_cap < bytes) {
+        (void)hipFreeAsync(ks->d_spread, s);  // (ordered after its last user: scratch_order_locked)
+        ks->d_spread = nullptr;
+    }
     if (ks->d_spread == nullptr) {
-        const size_t bytes = spread_bytes(ks->ds->ncu);
-        if (hipMallocAsync((void **)&ks->d_spread, bytes, s) != hipSuccess)
+        ks->spread_cap = 0;
+        if (hipMallocAsync((void **)&ks->d_spread, bytes, s) != hipSuccess) {
+            (void)hipGetLastError();
+            ks->d_spread = nullptr;
             return nullptr;
+        }
         if (hipMemsetAsync(ks->d_spread, 0, SPREAD_CNT_BYTES, s) != hipSuccess) {
+            (void)hipGetLastError();
             (void)hipFreeAsync(ks->d_spread, s);
             ks->d_spread = nullptr;
             return nullptr;
         }
+        ks->spread_cap = bytes;
     }
     return ks->d_spread;
 }
@@ -1175,7 +1188,7 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
     u32 *w8flags = nullptr;
     if (hpl == nullptr && spread_eligible(ks, nrecs, frame)) {
         lk.lock();
-        spread = spread_scratch_locked(ks, s);
+        spread = spread_scratch_locked(ks, s, nrecs);
     } else if (hpl == nullptr && w8_eligible(ks, nrecs, frame)) {  // (a spread launch never takes the W8 pair)
         lk.lock();
         w8flags = w8_flags_locked(ks, s);

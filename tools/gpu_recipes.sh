@@ -34,6 +34,18 @@ python3 tools/ct_summary.py gpurun_out/ct5 > gpurun_out/ct5_batch.txt; cat gpuru
 exit 0
   )
   ;;
+coh)
+  # round 4: per-record latency with coarse-grained (HIP default) vs coherent staging buffers, alternating processes,
+  # then the spread and lifecycle tests with the batch-sized spread scratch
+  (
+for i in 1 2 3; do for c in 0 1; do
+  PTLS_MI355X_STAGE_COHERENT=$c timeout -k 10 120 python tools/latency.py > gpurun_out/coh_${c}_$i.log 2>&1; rc=$?
+  echo "== coherent=$c run $i rc=$rc"; grep -v amdgpu.ids gpurun_out/coh_${c}_$i.log | head -12; [ $rc -ne 0 ] && exit $rc
+done; done
+timeout -k 10 600 python -u -m pytest tests/test_gpu_lifecycle.py tests/test_gpu_w8.py -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/coh_tests.log 2>&1; rc=$?
+echo "tests rc=$rc"; tail -3 gpurun_out/coh_tests.log; exit $rc
+  )
+  ;;
 w8ab)
   # round 4: the 8-bit Horner table (W8_HORNER=1, tools/variants/lib_w8.so) against the same source without it
   # (lib_now8.so), interleaved in one process per workload (tools/ab.py: identical sealed output checked)

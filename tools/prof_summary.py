@@ -44,15 +44,15 @@ def main(src, dst_prefix, records=None):
             if "GRBM_GUI_ACTIVE" in c:
                 k["effective_clock_GHz"] = c["GRBM_GUI_ACTIVE"] / 8 / (st["avg_ns"])
         out["kernels"][name] = k
-    # the seal instantiation: gcm_*_kernel<NR, false[, FRAME]>
-    seal = next((v for n, v in out["kernels"].items() if re.search(r"<\d+, false[,>]", n)), None)
-    if seal and "hbm_bytes_per_launch" in seal:
-        out["seal_hbm_bytes_per_launch"] = seal["hbm_bytes_per_launch"]
-        out["seal_hbm_read_bytes"], out["seal_hbm_write_bytes"] = seal["hbm_read_bytes_corrected"], seal["hbm_write_bytes"]
-    opn = next((v for n, v in out["kernels"].items() if re.search(r"<\d+, true[,>]", n)), None)
-    if opn and "hbm_bytes_per_launch" in opn:
-        out["open_hbm_bytes_per_launch"] = opn["hbm_bytes_per_launch"]
-        out["open_hbm_read_bytes"], out["open_hbm_write_bytes"] = opn["hbm_read_bytes_corrected"], opn["hbm_write_bytes"]
+    # the seal instantiations gcm_*_kernel<NR, false[, ...]> of one launch: since round 4 a launch may be the W8 pair
+    # (EXT 0 and EXT 3 kernels, one dispatch each), so the per-launch bytes are the sum over the seal (open) kernels
+    for side, pat in (("seal", r"<\d+, false[,>]"), ("open", r"<\d+, true[,>]")):
+        ks = [v for n, v in out["kernels"].items() if re.search(pat, n) and "hbm_bytes_per_launch" in v]
+        if ks:
+            out[f"{side}_hbm_read_bytes"] = sum(v["hbm_read_bytes_corrected"] for v in ks)
+            out[f"{side}_hbm_write_bytes"] = sum(v["hbm_write_bytes"] for v in ks)
+            out[f"{side}_hbm_bytes_per_launch"] = out[f"{side}_hbm_read_bytes"] + out[f"{side}_hbm_write_bytes"]
+            out[f"{side}_kernel_ms_per_launch"] = sum(v["trace"]["avg_ns"] for v in ks) / 1e6
     json.dump(out, open(dst_prefix + ".json", "w"), indent=1)
     with open(dst_prefix + ".md", "w") as f:
         f.write(f"# rocprofv3 summary: {os.path.basename(dst_prefix)}\n\nsource: `{src}`\n\n")
