@@ -912,12 +912,23 @@ static void launch_chunked(bool ct, unsigned grid, hipStream_t s, const BatchArg
         // of the pair ends, before the second has sealed its runs)
         // (and only when some workgroup can hold a whole-record run: a batch of fewer than WHOLE_MIN_RECS records per
         // workgroup in contiguous ranges has none, and the pair's second launch would cost such a small batch ~9 %)
+        if (W8_HORNER && W8_ALL && !a.one_inline && a.done_flag == nullptr) {  // every run W8, in one kernel
+            BatchArgs b = a;
+            b.w8_split = 1;  // (the W8 map's run capacity)
+            launch_chunked_x<NR, OPEN, 0, 3>(ct, grid, s, b);
+            return;
+        }
         const bool whole_possible = a.chunk != 0 || a.bounds != nullptr || (a.nrecs + grid - 1) / grid >= WHOLE_MIN_RECS;
         if (W8_HORNER && !a.one_inline && a.done_flag == nullptr && whole_possible) {
             BatchArgs b = a;
             b.w8_split = 1;
-            launch_chunked_x<NR, OPEN, 0>(ct, grid, s, b);
-            launch_chunked_x<NR, OPEN, 0, 3>(ct, grid, s, b);
+            if (W8_FIRST) {
+                launch_chunked_x<NR, OPEN, 0, 3>(ct, grid, s, b);
+                launch_chunked_x<NR, OPEN, 0>(ct, grid, s, b);
+            } else {
+                launch_chunked_x<NR, OPEN, 0>(ct, grid, s, b);
+                launch_chunked_x<NR, OPEN, 0, 3>(ct, grid, s, b);
+            }
             return;
         }
     }

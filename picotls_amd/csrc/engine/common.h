@@ -141,19 +141,34 @@ __device__ __forceinline__ u32 lane_here()
 #define CLDS_PART (CLDS_RUN1 + 4 * RUN_WORDS)                    // 16 B per unit: GHASH partial
 #define CLDS_ONE (CLDS_PART + 16 * CRUN_UNITS)                   // a lone record's descriptor (BatchArgs::one)
 #define CLDS_ALLOC (CLDS_ONE + 48)
-// W8 runs (whole records of at least W8_MIN_STEPS steps, gcm_chunked_kernel): H^8 as an 8-bit table over slots 0..7,
-// H in slot 8, H^2 in the partial region after the E(K, J0) slots of the groups
+// W8 runs (the EXT 3 kernel of a launch pair, gcm_chunked_kernel): whole records of at least W8_MIN_STEPS steps and,
+// since round 4, cut runs of 16-step units. LDS map: AES [0, 64K), H^8 as an 8-bit window-major table over slots 0..7,
+// H window-major in slot 8 (the segment end's serial lane Horner, gcm_segment), the unit partials of at most
+// W8_RUN_UNITS units at CLDS_PART (their first 2 KiB the groups' E(K, J0) slots in whole runs; the table build's
+// scratch before a run), the unit combine power window-major at W8_TAB_COMB
 #ifndef W8_HORNER
 #define W8_HORNER 1  // (round 4: on; interleaved A/B +13.1 % tls16k, +8.5 % AES-256 16 KiB, quic1200 and mixed within ±0.4 %, profiles/r4/w8_ab.txt)
 #endif
 #ifndef W8_MIN_STEPS
 #define W8_MIN_STEPS 64
 #endif
+#ifndef W8_CUT
+#define W8_CUT 1  // cut runs of 16-step units take the W8 kernel too (round 4)
+#endif
+#ifndef W8_ALL
+#define W8_ALL 0  // every run of an unframed chunked batch in the W8 kernel alone (no pair; experiment, round 4)
+#endif
+#ifndef W8_FIRST
+#define W8_FIRST 1  // the pair's W8 kernel (EXT 3) runs first, the plain one (EXT 0) second (it returns at once where no run is its)
+#endif
+#define W8_RUN_UNITS 512  // units per run of a launch pair (both kernels: their runs must be the same)
 #define W8_TAB_H (LDS_AES_BYTES + 8 * GHASH_TABLE_BYTES)
-#define W8_TAB_H2 (CLDS_PART + 16 * (ENGINE_WG / ENGINE_G))
+#define W8_TAB_COMB (CLDS_PART + 16 * W8_RUN_UNITS)
 #define SPAN_MAX_UNITS CRUN_UNITS  // units per span of a long record (span_kernels.h, spread_pieces): the LDS partials
 static_assert(CLDS_ALLOC <= 160 * 1024, "chunked schedule LDS budget");
-static_assert(W8_TAB_H2 % 256 == 0 && W8_TAB_H2 + GHASH_TABLE_BYTES <= CLDS_ONE, "W8 tables inside the partial region");
+static_assert(W8_TAB_COMB % 256 == 0 && W8_TAB_COMB + GHASH_TABLE_BYTES <= CLDS_ONE, "W8 combine table after the partials");
+static_assert(16 * (ENGINE_WG / ENGINE_G) <= 16 * W8_RUN_UNITS && GHASH_TABLE_BYTES <= 16 * W8_RUN_UNITS,
+              "E(K, J0) slots and the table build's scratch inside the W8 partial region");
 static_assert(CHUNK_BLOCKS % ENGINE_G == 0, "units are whole steps");
 static_assert((CHUNK_STEPS & (CHUNK_STEPS - 1)) == 0 && CHUNK_STEPS <= 32, "unit lengths are powers of two up to 32 steps");
 

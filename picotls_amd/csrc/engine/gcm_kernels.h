@@ -3,13 +3,20 @@
 #ifndef PTLS_MI355X_ENGINE_GCM_KERNELS_H
 #define PTLS_MI355X_ENGINE_GCM_KERNELS_H
 
-// Unit length multiplier of a record of `steps` steps: 1, or for a record that would need more than CHUNK_MAX_UNITS units
-// of 2^log2 steps the least factor that fits it in CHUNK_MAX_UNITS (its partials are then combined with the unit power
-// applied mul times). Records up to PTLS_MI355X_MAX_RECORD_LEN thus always spread over the workgroup.
-__device__ __forceinline__ u32 unit_mul(u32 steps, u32 log2)
+// Unit length multiplier of a record of `steps` steps: 1, or for a record that would need more than `cap` units (the
+// run's unit capacity: CHUNK_MAX_UNITS, or W8_RUN_UNITS in a launch pair) of 2^log2 steps the least factor that fits it
+// in `cap` (its partials are then combined with the unit power applied mul times). Records up to
+// PTLS_MI355X_MAX_RECORD_LEN thus always spread over the workgroup.
+__device__ __forceinline__ u32 unit_mul(u32 steps, u32 log2, u32 cap)
 {
     const u32 nc = (steps + (1u << log2) - 1) >> log2;
-    return nc > CHUNK_MAX_UNITS ? (nc + CHUNK_MAX_UNITS - 1) / CHUNK_MAX_UNITS : 1u;
+    return nc > cap ? (nc + cap - 1) / cap : 1u;
+}
+// the unit capacity of a launch's runs: the two kernels of a W8 pair cut their runs at W8_RUN_UNITS (the W8 kernel's
+// partial region), identically, since each skips exactly the other's runs
+__device__ __forceinline__ u32 run_unit_cap(const BatchArgs &args)
+{
+    return W8_HORNER && args.w8_split ? (u32)W8_RUN_UNITS : (u32)CRUN_UNITS;
 }
 
 // Descriptors whose len exceeds PTLS_MI355X_MAX_RECORD_LEN, whose AAD exceeds PTLS_MI355X_MAX_AAD_LEN or whose key_idx
@@ -264,7 +271,7 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
         for (u32 q = 0; q < Q; ++q) {
             // front-unit size bucket: 0 = a record too long for CHUNK_MAX_UNITS units (it takes units of a multiple
             // length, unit_mul), else ustep + 1 - size of the record's first unit (1 = a full unit, ustep = one step)
-            const u32 mul = unit_mul(steps[q], log2);
+            const u32 mul = unit_mul(steps[q], log2, run_unit_cap(args));
             nc[q] = (steps[q] + ustep - 1) >> log2;
             if (mul > 1)  // rare: the only division
                 nc[q] = (steps[q] + mul * ustep - 1) / (mul * ustep);
@@ -281,7 +288,7 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
             const u32 incl = carry + wave_incl_sum(t < n ? nc[q] : 0u);
             if (t < n)
                 ubase[t + 1] = incl;
-            const u64 c = __ballot(t < n && incl > CRUN_UNITS);
+            const u64 c = __ballot(t < n && incl > run_unit_cap(args));
             if (c != 0)
                 cut = min(cut, q * 64 + (u32)__builtin_ctzll(c));
             carry = (u32)__builtin_amdgcn_readlane((int)incl, 63);
@@ -711,19 +718,21 @@ __device__ __noinline__ u32x4 ct_combine_tree(const lds_u8 *lds, const lds_u32x4
     return g;
 }
 
-// The W8 tables of the run's key (staged in LDS): H^8's 4-bit table into slot 8 as the source of its 8-bit table over
-// slots 0..7, then H into slot 8 and H^2 beside the E(K, J0) slots. Out of line: inlined into the run loop it cost the
-// kernel's other runs registers (-4 % on 1200-byte records).
-__device__ __noinline__ void w8_build_tables(lds_u8 *lds, const lds_u8 *keyp)
+// The W8 tables of the run's key (staged in LDS), by three waves at once: H^8's 4-bit nibble-major table into the
+// partial region (free between runs) as the source of its 8-bit table over slots 0..7, H window-major into slot 8, and
+// (a cut run: usrc = the key element of its unit combine power) that power window-major at W8_TAB_COMB; then the 8-bit
+// table. Out of line: inlined into the run loop it cost the kernel's other runs registers (-4 % on 1200-byte records).
+__device__ __noinline__ void w8_build_tables(lds_u8 *lds, const lds_u8 *keyp, u32 usrc)
 {
     typedef __attribute__((address_space(3))) const KeyEntry lds_key_t;
     lds_key_t *key = (lds_key_t *)keyp;
-    build_ghash_tables(lds, key, 9, 7u, 8u, 0, 0, false, 0u);
+    auto el = [&](u32 i) { return u32x4{key->h[i][0], key->h[i][1], key->h[i][2], key->h[i][3]}; };
+    build_elem_table(lds, CLDS_PART, el(7), 0, false);
+    build_elem_table(lds, W8_TAB_H, el(0), 64, true);
+    if (usrc != 0xffffffffu)
+        build_elem_table(lds, W8_TAB_COMB, el(usrc), 128, true);
     __syncthreads();
-    build_h8_byte_table(lds, W8_TAB_H);
-    __syncthreads();
-    build_ghash_tables(lds, key, 9, 0u, 8u, 0, 0, false, 0u);
-    build_elem_table(lds, W8_TAB_H2, u32x4{key->h[1][0], key->h[1][1], key->h[1][2], key->h[1][3]}, 64);
+    build_h8_byte_table(lds, CLDS_PART);
     __syncthreads();
 }
 
@@ -741,15 +750,20 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     // (the lane index and what derives from it are computed in the unit loop, lane_here())
     const u32 wave = threadIdx.x >> 6;
     const u32 tsel_horner = 0x10000u + (u32)(G - 1) * GHASH_TABLE_BYTES;
-    const u32 tsel_chunk = 0x10000u + 8u * GHASH_TABLE_BYTES;
+    constexpr bool W8K = W8_HORNER && FRAME == 0 && EXT == 3;  // the launch pair's W8 half (launch_chunked)
+    // the unit combine table: slot 8, or in the W8 kernel's map W8_TAB_COMB
+    const u32 tsel_chunk = W8K ? (u32)W8_TAB_COMB : 0x10000u + 8u * GHASH_TABLE_BYTES;
 
     const u64 n = args.nrecs, C = args.bounds != nullptr ? 0 : args.chunk;
-    constexpr bool W8K = W8_HORNER && FRAME == 0 && EXT == 3;  // the launch pair's W8 half (launch_chunked)
-    if constexpr (W8K) {  // none of this workgroup's runs is a W8 run (the EXT 0 kernel saw them all): nothing to do
-        if (args.w8_flags != nullptr && args.w8_flags[blockIdx.x] == 0)
+    // the pair's second kernel (W8_FIRST: EXT 0, else EXT 3): none of this workgroup's runs is its kind (the first
+    // kernel saw them all): nothing to do
+    constexpr bool PAIR_FIRST = W8_HORNER && FRAME == 0 && (W8_FIRST ? EXT == 3 : EXT == 0);
+    constexpr bool PAIR_SECOND = W8_HORNER && FRAME == 0 && (W8_FIRST ? EXT == 0 : EXT == 3);
+    if constexpr (PAIR_SECOND) {
+        if (args.w8_split && args.w8_flags != nullptr && args.w8_flags[blockIdx.x] == 0)
             return;
     }
-    bool skipped_w8 = false;  // (the EXT 0 kernel of a pair: this workgroup left a W8 run to the EXT 3 one)
+    bool skipped_w8 = false;  // (the pair's first kernel: this workgroup left a run to the second one)
     constexpr bool SPREAD = FRAME == 0 && EXT == 1;
     if constexpr (SPREAD) {  // a small one-key batch (spread_pieces): workgroup w < n takes record w unless it is long
         if (blockIdx.x >= n) {
@@ -856,11 +870,12 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         }
         PROF_STAMP(t1);
 
-        // the launch pair (args.w8_split): W8 runs (whole, long records, valid key) belong to the EXT 3 kernel, the
-        // rest to the EXT 0 one; each scans past the other's runs
-        if (W8_HORNER && (FRAME == 0 && EXT == 0 ? args.w8_split != 0 : W8K)) {
-            const bool w8 = whole && key_idx < args.nkeys &&
-                            __builtin_amdgcn_readfirstlane(gcm_steps<OPEN, FRAME>(recs[pos]) >= W8_MIN_STEPS ? 1u : 0u) != 0;
+        // the launch pair (args.w8_split): W8 runs (a valid key, and whole records of at least W8_MIN_STEPS steps or
+        // cut 16-step units) belong to the EXT 3 kernel, the rest to the EXT 0 one; each scans past the other's runs
+        if (W8_HORNER && !W8_ALL && (FRAME == 0 && EXT == 0 ? args.w8_split != 0 : W8K)) {
+            const bool w8 = key_idx < args.nkeys &&
+                            (whole ? __builtin_amdgcn_readfirstlane(gcm_steps<OPEN, FRAME>(recs[pos]) >= W8_MIN_STEPS ? 1u : 0u) != 0
+                                   : W8_CUT && ulog2 == CHUNK_LOG2);
             if (w8 != W8K) {
                 skipped_w8 = true;
                 if (wave == 0 && nxt < nxt_end)
@@ -893,14 +908,17 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         // the EXT 3 kernel's runs (all W8: the others were skipped above) take the 8-bit Horner table (ghash.h)
         constexpr bool w8run = W8K;
         if (w8run && (key_idx != loaded_key || !loaded_w8)) {
-            // H^8's 4-bit table into slot 8 as the source of its 8-bit table over slots 0..7, then H into slot 8 and
-            // H^2 beside the E(K, J0) slots
-            w8_build_tables(lds, (const lds_u8 *)key);
+            // the 8-bit H^8 table over slots 0..7, H in slot 8, and a cut run's combine power at W8_TAB_COMB
+            w8_build_tables(lds, (const lds_u8 *)key, whole ? 0xffffffffu : usrc);
             loaded_key = key_idx;
-            loaded_usrc = 0xffffffffu;
+            loaded_usrc = whole ? 0xffffffffu : usrc;
             loaded_w8 = true;
             if (threadIdx.x == 0)
                 PROF_ADD(7, 1);
+        } else if (w8run && !whole && usrc != loaded_usrc) {  // the same key, another unit length: its combine power
+            build_elem_table(lds, W8_TAB_COMB, u32x4{key->h[usrc][0], key->h[usrc][1], key->h[usrc][2], key->h[usrc][3]}, 0, true);
+            __syncthreads();
+            loaded_usrc = usrc;
         } else if (!w8run && (key_idx != loaded_key || loaded_w8 || (!whole && usrc != loaded_usrc))) {
             // H^1..H^8 and the unit combine power (only the latter when just the unit length changed; constant-time
             // mode: its powers in tables 4..6 too)
@@ -993,7 +1011,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 }
                 const u32 steps = gcm_steps<OPEN, FRAME>(r);
                 // unit [m_lo, m_hi) of the record's steps (whole mode: the record); huge records take longer units
-                const u32 mul = whole ? 1u : unit_mul(steps, ulog2);
+                const u32 mul = whole ? 1u : unit_mul(steps, ulog2, run_unit_cap(args));
                 u32 m_hi = steps, m_lo = 0;
                 if (!whole) {
                     const u32 ulen = mul * ustep;
@@ -1029,7 +1047,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 last = dpp_bcast7(last, lane);
                 if (last) {
                     const ptls_mi355x_record_t r = recs[pos + lo];
-                    const u32 mul = unit_mul(gcm_steps<OPEN, FRAME>(r), ulog2);
+                    const u32 mul = unit_mul(gcm_steps<OPEN, FRAME>(r), ulog2, run_unit_cap(args));
                     // last unit of the record: GHASH = Horner over the partials with H^(G * ulen) = (H^(G * ustep))^mul
                     // (whole group)
                     // (CT: each lane forms the whole product from the same table rows, instead of a share of it from
@@ -1089,7 +1107,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     }
     if (with_hp && hp_n != 0)  // the last run's masks
         HP_PASS(hp_pos, hp_pos + hp_n, threadIdx.x, blockDim.x);
-    if constexpr (W8_HORNER && FRAME == 0 && EXT == 0) {  // for the EXT 3 kernel of the pair (workgroup-uniform)
+    if constexpr (PAIR_FIRST) {  // for the pair's second kernel (workgroup-uniform)
         if (args.w8_split && args.w8_flags != nullptr && threadIdx.x == 0)
             args.w8_flags[blockIdx.x] = skipped_w8 ? 1u : 0u;
     }

@@ -232,4 +232,45 @@ __device__ __forceinline__ u32x4 coop_last_powers(const lds_u8 *lds, u32x4 v, u3
     return sum;
 }
 
+// a * (window-major table at tsel) + sum over the group of x (x: this lane's term, zero in all lanes but one): gmul_group_w
+// with x folded into the lane's share before the group's reduction, at no extra instruction
+__device__ __forceinline__ u32x4 gmul_group_w_add(const lds_u8 *, u32x4 a, u32 tsel, u32 lane, u32x4 x)
+{
+    const u32 y = lane & 7, f = (lane >> 2) & 3, q = y >> 1;
+    const u32 w = q == 0 ? a[0] : q == 1 ? a[1] : q == 2 ? a[2] : a[3];
+    const u32 W = wtab_lane_base(tsel, lane), sh = 4u * f + 16u * (y & 1);
+    u32x4 e[4];
+#pragma unroll
+    for (u32 i = 0; i < 4; ++i) {
+        const u32 n = (w >> (sh ^ (4u * (i ^ 1u)))) & 15u;
+        e[i] = lds_load128((n << 8) + (W ^ (i << 4)));
+    }
+    u32x4 r;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        r[c] = dpp_xor8(xor3(xor3(e[0][c], e[1][c], e[2][c]), e[3][c], x[c]));
+    return r;
+}
+
+// The W8 segment end (gcm_segment, W8 runs): lane j of a group holds a_j, its partial with its last stream position
+// unmultiplied, owing H^(8 - rank_j). Returns sum_j a_j H^(8 - rank_j) in every lane of the group, as the Horner
+// ((v_0 H + v_1) H + ... + v_7) H over the ranks (v_r: the value of the lane of rank r) by eight group multiplies with
+// the window-major H table at W8_TAB_H; the lane of rank r folds its value into its share of the r-th product, so the
+// values never move between lanes. The W8 map has room for that one table only (the 8-bit H^8 table takes slots
+// 0..7), where coop_last_powers needs seven: the lookups are the same 32 per lane, conflict-free, the price is a
+// chain of eight dependent products.
+__device__ __forceinline__ u32x4 w8_lane_end(const lds_u8 *lds, u32x4 v, u32 lane, u32 rank)
+{
+    static_assert(ENGINE_G == 8, "a chain over 8 lanes");
+    const u32x4 z = {0, 0, 0, 0};
+    u32x4 g;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        g[c] = dpp_xor8(rank == 0 ? v[c] : 0u);
+#pragma unroll
+    for (u32 r = 1; r < 8; ++r)
+        g = gmul_group_w_add(lds, g, W8_TAB_H, lane, rank == r ? v : z);
+    return gmul_group_w(lds, g, W8_TAB_H, lane);
+}
+
 #endif  // PTLS_MI355X_ENGINE_GHASH_H

@@ -154,10 +154,13 @@ __device__ void build_ghash_tables(lds_u8 *lds, KeyPtr key, u32 ntables = ENGINE
 
 // W8 runs (ghash.h): the 8-bit window-major H^8 table at LDS_AES_BYTES from H^8's 4-bit nibble-major table at `scratch`
 // (entry (w, n) = e4(2w, n >> 4) ^ e4(2w + 1, n & 15): byte w of the operand is 4-bit windows 2w and 2w + 1)
+// Lane w of a 16-lane phase takes value n = k ^ (w << 4) ^ w (k = i >> 4): its two reads land in bank groups
+// (n >> 4) and (n & 15), both distinct across w, and its store in group w (round 4: the plain order n = k read one bank
+// group from 16 rows at once, 1.44M conflict cycles per tls16k dispatch).
 __device__ __forceinline__ void build_h8_byte_table(lds_u8 *lds, u32 scratch)
 {
     for (u32 i = threadIdx.x; i < 4096; i += blockDim.x) {
-        const u32 w = i & 15, n = i >> 4;
+        const u32 w = i & 15, n = (i >> 4) ^ (w << 4) ^ w;
         const u32x4 e = u32x4(*(const lds_u32x4 *)(lds + scratch + (2 * w) * 256 + (n >> 4) * 16)) ^
                         u32x4(*(const lds_u32x4 *)(lds + scratch + (2 * w + 1) * 256 + (n & 15) * 16));
         *(lds_u32x4 *)(lds + LDS_AES_BYTES + n * 256 + w * 16) = e;

@@ -40,10 +40,10 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                                             u32 &okw, bool aligned, u32 ekslot = 0)
 {
     constexpr int G = ENGINE_G;
-    // W8 (a whole-record run of long records, gcm_chunked_kernel): Horner on the 8-bit H^8 table (gmul8), the lanes'
-    // last powers by the uniform-table tree with H (W8_TAB_H) and H^2 (W8_TAB_H2; H^4 as two of it)
+    // W8 (a W8 run of the pair's EXT 3 kernel, gcm_chunked_kernel): Horner on the 8-bit H^8 table (gmul8), the lanes'
+    // last powers by a serial Horner over the group's ranks with the window-major H table (W8_TAB_H, w8_lane_end)
     constexpr bool COOP = SEG_COOP && !W8;  // the conflict-free segment end (coop_last_powers), both modes
-    constexpr bool TREE = W8 || (!SEG_COOP && CT && CT_TREE);
+    constexpr bool TREE = !W8 && !SEG_COOP && CT && CT_TREE;
     W8Lane w8 = {};
     if constexpr (W8)
         w8 = w8_lane(lane_here());
@@ -209,7 +209,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             X[1] = bswap32((u32)abits);
             X[2] = bswap32((u32)(cbits >> 32));
             X[3] = bswap32((u32)cbits);
-            if (COOP || TREE)  // (kept in LDS until after the loop: live through it, it was spilled)
+            if (COOP || TREE || W8)  // (kept in LDS until after the loop: live through it, it was spilled)
                 *(lds_u32x4 *)(const_cast<lds_u8 *>(lds) + ekslot) = ks;
             else
                 ek0 = ks;
@@ -317,7 +317,14 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     }
 
     static_assert(G == 8, "dpp_xor8 reduces groups of 8 lanes");
-    if constexpr (TREE) {
+    if constexpr (W8) {
+        // sum over the group of a_l H^(e_l) (rank r = 8 - e owes H^(8 - r)): ((v_0 H + v_1) H + ... + v_7) H by eight
+        // group multiplies with the one window-major table H (4 conflict-free lookups per lane each: 32, as
+        // coop_last_powers, with one table instead of seven)
+        acc = w8_lane_end(lds, acc, lane_here(), valid ? (u32)G - e_last : j);
+        if (valid && m_hi * G >= N && j == jl)  // the segment holds the length block: E(K, J0), on its lane
+            acc ^= u32x4(*(const lds_u32x4 *)(lds + ekslot));
+    } else if constexpr (TREE) {
         // sum over the group of a_l H^(e_l) (a_l: lane l's partial with its last position unmultiplied, e_l in 1..8 a
         // permutation over the lanes), as a butterfly over the ranks t = 8 - e: level k pairs rank t (bit k clear) with
         // rank t + k as v_t H^k + v_(t+k); every lane multiplies by the same table (H, H^2, H^4, then H once more) and
@@ -329,14 +336,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
 #pragma unroll 1
         for (u32 lv = 0; lv < 3; ++lv) {
             const u32 k = 1u << lv;
-            u32x4 y;
-            if constexpr (W8) {  // H, H^2, H^2 twice
-                y = gmul_tab(lds, v, lv == 0 ? (u32)W8_TAB_H : (u32)W8_TAB_H2);
-                if (lv == 2)
-                    y = gmul_tab(lds, y, W8_TAB_H2);
-            } else {
-                y = gmul_tab(lds, v, 0x10000u + (k - 1u) * GHASH_TABLE_BYTES);  // H^k
-            }
+            const u32x4 y = gmul_tab(lds, v, 0x10000u + (k - 1u) * GHASH_TABLE_BYTES);  // H^k
             const bool hi = (rank & k) != 0;
             const u32x4 send = hi ? v : y;
             const int src = (int)(((lane & ~(u32)(G - 1)) | (((rank ^ k) + rot) & (G - 1))) * 4);
@@ -346,7 +346,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                 recv[c] = (u32)__builtin_amdgcn_ds_bpermute(src, (int)send[c]);
             v = hi ? (recv ^ v) : (y ^ recv);
         }
-        acc = gmul_tab(lds, v, W8 ? (u32)W8_TAB_H : 0x10000u);  // * H
+        acc = gmul_tab(lds, v, 0x10000u);  // * H
         if (valid && m_hi * G >= N && j == jl)  // the segment holds the length block: E(K, J0), on its lane
             acc ^= u32x4(*(const lds_u32x4 *)(lds + ekslot));
     } else {

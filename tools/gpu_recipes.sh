@@ -46,6 +46,36 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_lifecycle.py tests/test_gpu
 echo "tests rc=$rc"; tail -3 gpurun_out/coh_tests.log; exit $rc
   )
   ;;
+w8cut)
+  # round 4: W8 for cut runs of 16-step units (lib_w8cut) against the shipped W8 (whole runs only, lib_base4) and the
+  # same source with W8_CUT=0 (lib_w8nocut: the 512-unit runs of a pair alone): GPU parity of the new kernel first
+  (
+PTLS_MI355X_LIB=$PWD/tools/variants/${W8CUT_LIB:-lib_w8cut.so} timeout -k 10 600 python -u -m pytest tests/test_gpu_w8.py tests/test_gpu_configs.py tests/test_gpu_parity.py tests/test_gpu_ct.py tests/test_gpu_lifecycle.py -m gpu -x -q --timeout 300 --timeout-method thread -k "not vtable" > gpurun_out/w8cut_tests.log 2>&1; rc=$?
+echo "w8cut suite rc=$rc"; tail -3 gpurun_out/w8cut_tests.log; [ $rc -ne 0 ] && { grep -B5 -A30 "Error\|FAILED" gpurun_out/w8cut_tests.log | head -80; exit $rc; }
+V=${W8CUT_AB:-"tools/variants/lib_base4.so tools/variants/lib_w8nocut.so tools/variants/lib_w8cut.so"}
+for w in "mixed 4194304" "mixedrand 4194304" "mixed1key 2097152" "tls16k 1048576" "quic1200 4194304" "mixedconn 4194304"; do set -- $w
+  timeout -k 10 300 python tools/ab.py $V --workload $1 --records $2 --rounds 6 --reps 2 > gpurun_out/w8cut_$1.log 2>&1; rc=$?
+  echo "== $1 rc=$rc"; grep -v amdgpu.ids gpurun_out/w8cut_$1.log | tail -4 | cut -c1-150; [ $rc -ne 0 ] && exit $rc
+done
+exit 0
+  )
+  ;;
+w8all)
+  # round 4: every run of an unframed batch in the W8 kernel alone (lib_w8all) against the shipped pair (lib_base4)
+  # and W8 cut runs in the reordered pair (lib_w8cut_rev): parity of the new variant, bulk A/B, small batches
+  (
+PTLS_MI355X_LIB=$PWD/tools/variants/lib_w8all.so timeout -k 10 600 python -u -m pytest tests/test_gpu_w8.py tests/test_gpu_configs.py tests/test_gpu_parity.py tests/test_gpu_ct.py tests/test_gpu_lifecycle.py -m gpu -x -q --timeout 300 --timeout-method thread -k "not vtable" > gpurun_out/w8all_tests.log 2>&1; rc=$?
+echo "w8all suite rc=$rc"; tail -3 gpurun_out/w8all_tests.log; [ $rc -ne 0 ] && { grep -B5 -A30 "Error\|FAILED" gpurun_out/w8all_tests.log | head -80; exit $rc; }
+V="tools/variants/lib_base4.so tools/variants/lib_w8cut_rev.so tools/variants/lib_w8all.so"
+for w in "mixed 4194304" "mixedrand 4194304" "mixedconn 4194304" "mixed1key 2097152" "tls16k 1048576" "quic1200 4194304"; do set -- $w
+  timeout -k 10 300 python tools/ab.py $V --workload $1 --records $2 --rounds 6 --reps 2 > gpurun_out/w8all_$1.log 2>&1; rc=$?
+  echo "== $1 rc=$rc"; grep -v amdgpu.ids gpurun_out/w8all_$1.log | tail -3 | cut -c1-150; [ $rc -ne 0 ] && exit $rc
+done
+timeout -k 10 300 python tools/small_batch.py tools/variants/lib_base4.so tools/variants/lib_w8all.so --rounds 3 > gpurun_out/w8all_small.log 2>&1; rc=$?
+echo "== small batches rc=$rc"; grep -v amdgpu.ids gpurun_out/w8all_small.log | tail -30
+exit $rc
+  )
+  ;;
 w8ab)
   # round 4: the 8-bit Horner table (W8_HORNER=1, tools/variants/lib_w8.so) against the same source without it
   # (lib_now8.so), interleaved in one process per workload (tools/ab.py: identical sealed output checked)
