@@ -164,11 +164,17 @@ static int set_kernel_attrs(void)
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<10, true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<14, false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_batch_kernel<14, true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_ALLOC));
+#if SEG_COOP  // (one instantiation for both settings, launch_chunked_x)
+#define CHUNKED_ATTR_X(nr, open, frame, ext)                                                                           \
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_chunked_kernel<nr, open, frame, true, ext>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                CLDS_ALLOC))
+#else
 #define CHUNKED_ATTR_X(nr, open, frame, ext)                                                                           \
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_chunked_kernel<nr, open, frame, false, ext>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                 CLDS_ALLOC));                                                                              \
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_chunked_kernel<nr, open, frame, true, ext>, hipFuncAttributeMaxDynamicSharedMemorySize, \
                                 CLDS_ALLOC))
+#endif
 #define CHUNKED_ATTR(nr, open, frame) CHUNKED_ATTR_X(nr, open, frame, 0)
     CHUNKED_ATTR_X(10, false, 0, 1);
     CHUNKED_ATTR_X(10, true, 0, 1);
@@ -176,10 +182,20 @@ static int set_kernel_attrs(void)
     CHUNKED_ATTR_X(14, true, 0, 1);
     CHUNKED_ATTR_X(10, false, 0, 2);
     CHUNKED_ATTR_X(14, false, 0, 2);
-    CHUNKED_ATTR_X(10, false, 0, 3);
-    CHUNKED_ATTR_X(10, true, 0, 3);
-    CHUNKED_ATTR_X(14, false, 0, 3);
-    CHUNKED_ATTR_X(14, true, 0, 3);
+#define CHUNKED_ATTR_W8(frame)                                                                                         \
+    CHUNKED_ATTR_X(10, false, frame, 3);                                                                               \
+    CHUNKED_ATTR_X(10, true, frame, 3);                                                                                \
+    CHUNKED_ATTR_X(14, false, frame, 3);                                                                               \
+    CHUNKED_ATTR_X(14, true, frame, 3);                                                                                \
+    CHUNKED_ATTR_X(10, false, frame, 4);                                                                               \
+    CHUNKED_ATTR_X(10, true, frame, 4);                                                                                \
+    CHUNKED_ATTR_X(14, false, frame, 4);                                                                               \
+    CHUNKED_ATTR_X(14, true, frame, 4)
+#if W8_HORNER
+    CHUNKED_ATTR_W8(0);
+    CHUNKED_ATTR_W8(1);
+#endif
+#undef CHUNKED_ATTR_W8
     CHUNKED_ATTR(10, false, 0);
     CHUNKED_ATTR(10, true, 0);
     CHUNKED_ATTR(14, false, 0);
@@ -199,9 +215,14 @@ static int set_kernel_attrs(void)
     HIP_TRY(hipFuncSetAttribute((const void *)hp_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
     HIP_TRY(hipFuncSetAttribute((const void *)hp_kernel<14>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
     HIP_TRY(hipFuncSetAttribute((const void *)quiclb_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_AES_BYTES));
+#if SEG_COOP
+#define SPAN_ATTR(nr, open)                                                                                            \
+    HIP_TRY(hipFuncSetAttribute((const void *)gcm_span_kernel<nr, open, true>, hipFuncAttributeMaxDynamicSharedMemorySize, SPAN_LDS))
+#else
 #define SPAN_ATTR(nr, open)                                                                                            \
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_span_kernel<nr, open, false>, hipFuncAttributeMaxDynamicSharedMemorySize, SPAN_LDS)); \
     HIP_TRY(hipFuncSetAttribute((const void *)gcm_span_kernel<nr, open, true>, hipFuncAttributeMaxDynamicSharedMemorySize, SPAN_LDS))
+#endif
     SPAN_ATTR(10, false);
     SPAN_ATTR(10, true);
     SPAN_ATTR(14, false);
@@ -881,13 +902,21 @@ int ptls_mi355x_keyset_set_iv(ptls_mi355x_keyset_t *ks, size_t key_idx, const vo
 // 784 vs 751 on 1200 B), and its chunked runs balance mixed lengths and short key runs.
 static bool use_chunked(int schedule) { return schedule != PTLS_MI355X_SCHEDULE_LOCKSTEP; }
 
+// Since the window-major segment ends (SEG_COOP) the constant-time template argument changes no instruction of the
+// chunked and span kernels: every keyset, constant-time or not, launches the CT instantiation, so the
+// code object holds one set of these kernels
 template <int NR, bool OPEN, int FRAME, int EXT = 0>
 static void launch_chunked_x(bool ct, unsigned grid, hipStream_t s, const BatchArgs &a)
 {
+#if SEG_COOP
+    (void)ct;
+    gcm_chunked_kernel<NR, OPEN, FRAME, true, EXT><<<grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
+#else
     if (ct)
         gcm_chunked_kernel<NR, OPEN, FRAME, true, EXT><<<grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
     else
         gcm_chunked_kernel<NR, OPEN, FRAME, false, EXT><<<grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
+#endif
 }
 
 // the instantiation for the launch: unframed batches with a spread plan (EXT 1) or header-protection masks (EXT 2)
@@ -906,29 +935,25 @@ static void launch_chunked(bool ct, unsigned grid, hipStream_t s, const BatchArg
                 return;
             }
         }
-        // whole-record runs of long records go to their own instantiation (EXT 3: the 8-bit Horner table), the other
-        // runs to the plain one; each skips the other's runs (a batch of fewer records than a whole run has none)
-        // (not for a per-record launch that publishes completion words: the host would see them when the first kernel
-        // of the pair ends, before the second has sealed its runs)
-        // (and only when some workgroup can hold a whole-record run: a batch of fewer than WHOLE_MIN_RECS records per
-        // workgroup in contiguous ranges has none, and the pair's second launch would cost such a small batch ~9 %)
-        if (W8_HORNER && W8_ALL && !a.one_inline && a.done_flag == nullptr) {  // every run W8, in one kernel
+    }
+    // The W8 kernels (the Horner step on an 8-bit H^8 table, ghash.h gmul8) for every run of an unframed or TLS-framed
+    // batch: EXT 4 (segment ends by a serial lane Horner) takes all runs but those of long whole records, which EXT 3
+    // (the butterfly end: on 16 KiB records it measured 1 % above the serial one) takes after it, each skipping the
+    // other's runs and EXT 3 returning at once in the workgroups where EXT 4 saw none (BatchArgs::w8_split, w8_flags).
+    // A batch of fewer than WHOLE_MIN_RECS records per workgroup in contiguous ranges holds no whole-record run: EXT 4
+    // alone. Not for a per-record launch (it publishes completion words, and its 1-16-step units suit the 4-bit path),
+    // a batch of fewer than W8_MIN_RECS records (the table build is not repaid), nor TLS 1.2 framing (its seal kernels
+    // would spill: 96 bytes per lane).
+    if constexpr (W8_HORNER && FRAME != 2) {
+        if (!a.one_inline && a.done_flag == nullptr && a.nrecs >= W8_MIN_RECS) {
+            const bool whole_possible = a.chunk != 0 || a.bounds != nullptr || (a.nrecs + grid - 1) / grid >= WHOLE_MIN_RECS;
             BatchArgs b = a;
-            b.w8_split = 1;  // (the W8 map's run capacity)
-            launch_chunked_x<NR, OPEN, 0, 3>(ct, grid, s, b);
-            return;
-        }
-        const bool whole_possible = a.chunk != 0 || a.bounds != nullptr || (a.nrecs + grid - 1) / grid >= WHOLE_MIN_RECS;
-        if (W8_HORNER && !a.one_inline && a.done_flag == nullptr && whole_possible) {
-            BatchArgs b = a;
-            b.w8_split = 1;
-            if (W8_FIRST) {
-                launch_chunked_x<NR, OPEN, 0, 3>(ct, grid, s, b);
-                launch_chunked_x<NR, OPEN, 0>(ct, grid, s, b);
-            } else {
-                launch_chunked_x<NR, OPEN, 0>(ct, grid, s, b);
-                launch_chunked_x<NR, OPEN, 0, 3>(ct, grid, s, b);
-            }
+            b.w8_split = whole_possible ? 2u : 1u;
+            if (!whole_possible)
+                b.w8_flags = nullptr;
+            launch_chunked_x<NR, OPEN, FRAME, 4>(ct, grid, s, b);
+            if (whole_possible)
+                launch_chunked_x<NR, OPEN, FRAME, 3>(ct, grid, s, b);
             return;
         }
     }
@@ -1055,10 +1080,15 @@ static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int sche
 template <int NR, bool OPEN>
 static void launch_span_kernel(bool ct, u32 nspans, hipStream_t s, const BatchArgs &a, u32 span, u32 units, void *part)
 {
+#if SEG_COOP  // (one instantiation for both settings, as launch_chunked_x)
+    (void)ct;
+    gcm_span_kernel<NR, OPEN, true><<<nspans, ENGINE_WG, SPAN_LDS, s>>>(a, span, units, (u32x4 *)part);
+#else
     if (ct)
         gcm_span_kernel<NR, OPEN, true><<<nspans, ENGINE_WG, SPAN_LDS, s>>>(a, span, units, (u32x4 *)part);
     else
         gcm_span_kernel<NR, OPEN, false><<<nspans, ENGINE_WG, SPAN_LDS, s>>>(a, span, units, (u32x4 *)part);
+#endif
 }
 
 static int launch_span(const KeyEntry *key, int nr, bool ct, bool open, const ptls_mi355x_record_t &one, const void *in,
@@ -1101,10 +1131,11 @@ static bool spread_eligible(const ptls_mi355x_keyset_t *ks, size_t nrecs, int fr
     return frame == 0 && nrecs >= 2 && nrecs < (size_t)ks->ds->ncu && nrecs <= SPREAD_MAX_RECS && (ks->ct || use_chunked(ks->schedule));
 }
 
-// a batch that may launch the W8 pair (launch_chunked): unframed, chunked, at least one whole-record run's worth
+// a batch that may launch the W8 pair (launch_chunked): chunked, at least one whole-record run's worth
 static bool w8_eligible(const ptls_mi355x_keyset_t *ks, size_t nrecs, int frame)
 {
-    return W8_HORNER && frame == 0 && nrecs >= WHOLE_MIN_RECS && (ks->ct || use_chunked(ks->schedule));
+    (void)frame;
+    return W8_HORNER && nrecs >= WHOLE_MIN_RECS && (ks->ct || use_chunked(ks->schedule));
 }
 
 // orders a launch on `s` that uses the keyset's scratch (spread pieces, W8 flags) after the last launch that used it;

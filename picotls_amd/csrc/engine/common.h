@@ -141,25 +141,22 @@ __device__ __forceinline__ u32 lane_here()
 #define CLDS_PART (CLDS_RUN1 + 4 * RUN_WORDS)                    // 16 B per unit: GHASH partial
 #define CLDS_ONE (CLDS_PART + 16 * CRUN_UNITS)                   // a lone record's descriptor (BatchArgs::one)
 #define CLDS_ALLOC (CLDS_ONE + 48)
-// W8 runs (the EXT 3 kernel of a launch pair, gcm_chunked_kernel): whole records of at least W8_MIN_STEPS steps and,
-// since round 4, cut runs of 16-step units. LDS map: AES [0, 64K), H^8 as an 8-bit window-major table over slots 0..7,
-// H window-major in slot 8 (the segment end's serial lane Horner, gcm_segment), the unit partials of at most
-// W8_RUN_UNITS units at CLDS_PART (their first 2 KiB the groups' E(K, J0) slots in whole runs; the table build's
-// scratch before a run), the unit combine power window-major at W8_TAB_COMB
+// W8 kernels (gcm_chunked_kernel EXT 3 and 4: the Horner step on an 8-bit H^8 table): every run of an unframed or
+// TLS-framed batch, EXT 4 with the serial lane-Horner segment end, EXT 3 (long whole records, W8_MIN_STEPS steps and
+// more) with the butterfly end. LDS map: AES [0, 64K), H^8 as an 8-bit window-major table over slots 0..7, H in slot 8
+// (window-major for EXT 4, nibble-major for EXT 3), the unit partials of at most W8_RUN_UNITS units at CLDS_PART
+// (their first 2 KiB the groups' E(K, J0) slots in whole runs; the table build's scratch before a run), at W8_TAB_COMB
+// the unit combine power (window-major, EXT 4) or H^2 (nibble-major, EXT 3)
 #ifndef W8_HORNER
-#define W8_HORNER 1  // (round 4: on; interleaved A/B +13.1 % tls16k, +8.5 % AES-256 16 KiB, quic1200 and mixed within ±0.4 %, profiles/r4/w8_ab.txt)
+#define W8_HORNER 1  // (round 4: on; profiles/r4/w8_ab.txt, w8all_ab.txt)
 #endif
 #ifndef W8_MIN_STEPS
 #define W8_MIN_STEPS 64
 #endif
-#ifndef W8_CUT
-#define W8_CUT 1  // cut runs of 16-step units take the W8 kernel too (round 4)
-#endif
-#ifndef W8_ALL
-#define W8_ALL 0  // every run of an unframed chunked batch in the W8 kernel alone (no pair; experiment, round 4)
-#endif
-#ifndef W8_FIRST
-#define W8_FIRST 1  // the pair's W8 kernel (EXT 3) runs first, the plain one (EXT 0) second (it returns at once where no run is its)
+#ifndef W8_MIN_RECS
+// batches of fewer records keep the 4-bit kernel: the 8-bit table's build is not repaid (256 x 16 KiB -5 %, 1000 x 1200 B
+// -4 %, 1000 x 16 KiB even, 4096 x 16 KiB +7 %; profiles/r4/w8all_ab.txt)
+#define W8_MIN_RECS 2048
 #endif
 #define W8_RUN_UNITS 512  // units per run of a launch pair (both kernels: their runs must be the same)
 #define W8_TAB_H (LDS_AES_BYTES + 8 * GHASH_TABLE_BYTES)

@@ -12,8 +12,8 @@ __device__ __forceinline__ u32 unit_mul(u32 steps, u32 log2, u32 cap)
     const u32 nc = (steps + (1u << log2) - 1) >> log2;
     return nc > cap ? (nc + cap - 1) / cap : 1u;
 }
-// the unit capacity of a launch's runs: the two kernels of a W8 pair cut their runs at W8_RUN_UNITS (the W8 kernel's
-// partial region), identically, since each skips exactly the other's runs
+// the unit capacity of a launch's runs: the W8 kernels cut their runs at W8_RUN_UNITS (their partial region), the two
+// of a pair identically, since each skips exactly the other's runs
 __device__ __forceinline__ u32 run_unit_cap(const BatchArgs &args)
 {
     return W8_HORNER && args.w8_split ? (u32)W8_RUN_UNITS : (u32)CRUN_UNITS;
@@ -722,14 +722,17 @@ __device__ __noinline__ u32x4 ct_combine_tree(const lds_u8 *lds, const lds_u32x4
 // partial region (free between runs) as the source of its 8-bit table over slots 0..7, H window-major into slot 8, and
 // (a cut run: usrc = the key element of its unit combine power) that power window-major at W8_TAB_COMB; then the 8-bit
 // table. Out of line: inlined into the run loop it cost the kernel's other runs registers (-4 % on 1200-byte records).
-__device__ __noinline__ void w8_build_tables(lds_u8 *lds, const lds_u8 *keyp, u32 usrc)
+// tree (the EXT 3 kernel: long whole records): H and H^2 nibble-major at W8_TAB_H and W8_TAB_COMB instead (w8_tree_end).
+__device__ __noinline__ void w8_build_tables(lds_u8 *lds, const lds_u8 *keyp, u32 usrc, bool tree)
 {
     typedef __attribute__((address_space(3))) const KeyEntry lds_key_t;
     lds_key_t *key = (lds_key_t *)keyp;
     auto el = [&](u32 i) { return u32x4{key->h[i][0], key->h[i][1], key->h[i][2], key->h[i][3]}; };
     build_elem_table(lds, CLDS_PART, el(7), 0, false);
-    build_elem_table(lds, W8_TAB_H, el(0), 64, true);
-    if (usrc != 0xffffffffu)
+    build_elem_table(lds, W8_TAB_H, el(0), 64, !tree);
+    if (tree)
+        build_elem_table(lds, W8_TAB_COMB, el(1), 128, false);
+    else if (usrc != 0xffffffffu)
         build_elem_table(lds, W8_TAB_COMB, el(usrc), 128, true);
     __syncthreads();
     build_h8_byte_table(lds, CLDS_PART);
@@ -750,17 +753,15 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     // (the lane index and what derives from it are computed in the unit loop, lane_here())
     const u32 wave = threadIdx.x >> 6;
     const u32 tsel_horner = 0x10000u + (u32)(G - 1) * GHASH_TABLE_BYTES;
-    constexpr bool W8K = W8_HORNER && FRAME == 0 && EXT == 3;  // the launch pair's W8 half (launch_chunked)
+    constexpr bool W8K = W8_HORNER && (EXT == 3 || EXT == 4);  // a W8 kernel (launch_chunked)
+    constexpr bool W8TREE = W8_HORNER && EXT == 3;                  // ... with the butterfly segment end
     // the unit combine table: slot 8, or in the W8 kernel's map W8_TAB_COMB
     const u32 tsel_chunk = W8K ? (u32)W8_TAB_COMB : 0x10000u + 8u * GHASH_TABLE_BYTES;
 
     const u64 n = args.nrecs, C = args.bounds != nullptr ? 0 : args.chunk;
-    // the pair's second kernel (W8_FIRST: EXT 0, else EXT 3): none of this workgroup's runs is its kind (the first
-    // kernel saw them all): nothing to do
-    constexpr bool PAIR_FIRST = W8_HORNER && FRAME == 0 && (W8_FIRST ? EXT == 3 : EXT == 0);
-    constexpr bool PAIR_SECOND = W8_HORNER && FRAME == 0 && (W8_FIRST ? EXT == 0 : EXT == 3);
-    if constexpr (PAIR_SECOND) {
-        if (args.w8_split && args.w8_flags != nullptr && args.w8_flags[blockIdx.x] == 0)
+    // the pair's second kernel (EXT 3): none of this workgroup's runs is its kind (the first kernel saw them all)
+    if constexpr (W8TREE) {
+        if (args.w8_split == 2 && args.w8_flags != nullptr && args.w8_flags[blockIdx.x] == 0)
             return;
     }
     bool skipped_w8 = false;  // (the pair's first kernel: this workgroup left a run to the second one)
@@ -777,7 +778,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     u64 end = SPREAD ? (u64)blockIdx.x + 1 : args.bounds != nullptr ? args.bounds[blockIdx.x + 1] : C != 0 ? min(n, beg + C) : n * (blockIdx.x + 1) / gridDim.x;
     u64 cstart = beg;
     u32 loaded_key = 0xffffffffu, loaded_usrc = 0xffffffffu;
-    bool loaded_w8 = false;  // the LDS holds the W8 tables (an 8-bit H^8 table, H, H^2) instead of the nine 4-bit ones
+    u32 loaded_w8 = 0;  // the LDS holds the nine 4-bit tables (0) or the W8 map: serial segment ends (1), the tree (2)
     // the descriptors in batch order, or (an ungrouped many-key batch) the key-grouped copy built on the device; ok
     // bytes go to the record's batch index either way
     const ptls_mi355x_record_t *recs = args.recs;
@@ -852,7 +853,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         // the scarce resource)
         const u32 key_idx = __builtin_amdgcn_readfirstlane(rs[RC_KEY]);
         const u32 run_n = __builtin_amdgcn_readfirstlane(rs[RC_N]);
-        const bool whole = __builtin_amdgcn_readfirstlane(rs[RC_WHOLE]);
+        const bool whole_run = __builtin_amdgcn_readfirstlane(rs[RC_WHOLE]);
         const u32 total_units = __builtin_amdgcn_readfirstlane(rs[RC_UNITS]);
         const u32 nhuge = __builtin_amdgcn_readfirstlane(rs[RC_HUGE]);
         // the run's unit length in steps (a power of two <= CHUNK_STEPS) and the key element of its combine power
@@ -870,13 +871,12 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         }
         PROF_STAMP(t1);
 
-        // the launch pair (args.w8_split): W8 runs (a valid key, and whole records of at least W8_MIN_STEPS steps or
-        // cut 16-step units) belong to the EXT 3 kernel, the rest to the EXT 0 one; each scans past the other's runs
-        if (W8_HORNER && !W8_ALL && (FRAME == 0 && EXT == 0 ? args.w8_split != 0 : W8K)) {
-            const bool w8 = key_idx < args.nkeys &&
-                            (whole ? __builtin_amdgcn_readfirstlane(gcm_steps<OPEN, FRAME>(recs[pos]) >= W8_MIN_STEPS ? 1u : 0u) != 0
-                                   : W8_CUT && ulog2 == CHUNK_LOG2);
-            if (w8 != W8K) {
+        // a W8 pair (w8_split 2): runs of long whole records (at least W8_MIN_STEPS steps) belong to the EXT 3 kernel,
+        // the others to the EXT 4 one; each scans past the other's runs
+        if (W8K && args.w8_split == 2) {
+            const bool tree = whole_run &&
+                              __builtin_amdgcn_readfirstlane(gcm_steps<OPEN, FRAME>(recs[pos]) >= W8_MIN_STEPS ? 1u : 0u) != 0;
+            if (tree != W8TREE) {
                 skipped_w8 = true;
                 if (wave == 0 && nxt < nxt_end)
                     scan_run<OPEN, FRAME, false, EXT>(args, recs, nxt, nxt_end, rs_next);
@@ -886,6 +886,9 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 continue;
             }
         }
+        // (EXT 3 is launched only as a pair's second kernel, w8_split 2: every run it keeps is whole, and its code for
+        // cut runs goes; -13 VGPRs)
+        const bool whole = W8TREE || whole_run;
         if (key_idx >= args.nkeys) {  // invalid key: nothing is written except a failed ok byte
             if (OPEN)
                 for (u64 t = pos + threadIdx.x; t < run_end; t += blockDim.x)
@@ -907,12 +910,14 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         lds_key_t *key = (lds_key_t *)(rs + RUN_KEY_OFF);  // staged by the scanner
         // the EXT 3 kernel's runs (all W8: the others were skipped above) take the 8-bit Horner table (ghash.h)
         constexpr bool w8run = W8K;
-        if (w8run && (key_idx != loaded_key || !loaded_w8)) {
-            // the 8-bit H^8 table over slots 0..7, H in slot 8, and a cut run's combine power at W8_TAB_COMB
-            w8_build_tables(lds, (const lds_u8 *)key, whole ? 0xffffffffu : usrc);
+        const u32 w8mode = !w8run ? 0u : W8TREE ? 2u : 1u;  // W8 segment ends: the serial chain (1) or the tree (2)
+        if (w8run && (key_idx != loaded_key || loaded_w8 != w8mode)) {
+            // the 8-bit H^8 table over slots 0..7, H in slot 8, and a cut run's combine power (or the tree's H^2) at
+            // W8_TAB_COMB
+            w8_build_tables(lds, (const lds_u8 *)key, whole ? 0xffffffffu : usrc, w8mode == 2);
             loaded_key = key_idx;
             loaded_usrc = whole ? 0xffffffffu : usrc;
-            loaded_w8 = true;
+            loaded_w8 = w8mode;
             if (threadIdx.x == 0)
                 PROF_ADD(7, 1);
         } else if (w8run && !whole && usrc != loaded_usrc) {  // the same key, another unit length: its combine power
@@ -928,7 +933,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             __syncthreads();
             loaded_key = key_idx;
             loaded_usrc = usrc;
-            loaded_w8 = false;
+            loaded_w8 = 0;
             if (threadIdx.x == 0)
                 PROF_ADD(7, 1);
         }
@@ -1024,7 +1029,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 // in a whole-record run, which has no partials)
                 const u32 ekslot = CLDS_PART + 16u * (whole ? threadIdx.x / G : first + unc - 1);
                 gcm_segment<NR, OPEN, 1, FRAME, CT, W8K>(args, lds, rk, iv0, iv1, iv2, r, live, m_lo, m_hi, j, laneoff,
-                                                         tsel_horner, acc, unc == 1, okw, whole, ekslot);
+                                                         tsel_horner, acc, unc == 1, okw, whole, ekslot, W8TREE);
             }
             // from here on everything is read again (run state, descriptor), not carried across the segment
             asm volatile("" ::: "memory");
@@ -1107,8 +1112,8 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     }
     if (with_hp && hp_n != 0)  // the last run's masks
         HP_PASS(hp_pos, hp_pos + hp_n, threadIdx.x, blockDim.x);
-    if constexpr (PAIR_FIRST) {  // for the pair's second kernel (workgroup-uniform)
-        if (args.w8_split && args.w8_flags != nullptr && threadIdx.x == 0)
+    if constexpr (W8K && !W8TREE) {  // the pair's first kernel, for the second (workgroup-uniform)
+        if (args.w8_split == 2 && args.w8_flags != nullptr && threadIdx.x == 0)
             args.w8_flags[blockIdx.x] = skipped_w8 ? 1u : 0u;
     }
     publish_done(args.done_flag, args.done_token);  // the per-record path polls these instead of waiting for the stream

@@ -273,4 +273,31 @@ __device__ __forceinline__ u32x4 w8_lane_end(const lds_u8 *lds, u32x4 v, u32 lan
     return gmul_group_w(lds, g, W8_TAB_H, lane);
 }
 
+// The W8 segment end of a long whole record (at least W8_MIN_STEPS steps, the EXT 3 kernel): the same sum by a butterfly over the
+// ranks, every lane multiplying by the same nibble-major table (H at W8_TAB_H, H^2 at W8_TAB_COMB, H^4 as two of it):
+// level k pairs rank t (bit k clear) with rank t + k as v_t H^k + v_(t+k), each lane taking its partner's product or
+// value through the crossbar; then one more xH. 160 lookups per lane (gmul_tab, conflict-free for any data) against the
+// serial chain's 32, but three short levels of independent products instead of eight dependent ones: on a record this
+// long the chain's latency cost more (-0.7 % on 16 KiB records) than the lookups
+__device__ __forceinline__ u32x4 w8_tree_end(const lds_u8 *lds, u32x4 v, u32 lane, u32 rank)
+{
+    const u32 rot = ((lane & 7u) - rank) & 7u;
+#pragma unroll 1
+    for (u32 lv = 0; lv < 3; ++lv) {
+        const u32 k = 1u << lv;
+        u32x4 y = gmul_tab(lds, v, lv == 0 ? (u32)W8_TAB_H : (u32)W8_TAB_COMB);
+        if (lv == 2)
+            y = gmul_tab(lds, y, W8_TAB_COMB);
+        const bool hi = (rank & k) != 0;
+        const u32x4 send = hi ? v : y;
+        const int src = (int)(((lane & ~7u) | (((rank ^ k) + rot) & 7u)) * 4u);
+        u32x4 recv;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            recv[c] = (u32)__builtin_amdgcn_ds_bpermute(src, (int)send[c]);
+        v = hi ? (recv ^ v) : (y ^ recv);
+    }
+    return gmul_tab(lds, v, W8_TAB_H);  // * H
+}
+
 #endif  // PTLS_MI355X_ENGINE_GHASH_H

@@ -85,10 +85,10 @@ struct BatchArgs {
     u32 spread;
     u32x4 *spread_part;
     u32 *spread_cnt;
-    // chunked kernel, FRAME 0: the launch is a pair (launch_chunked): EXT 0 skips the W8 runs (whole-record runs of
-    // records of W8_MIN_STEPS steps or more), EXT 3 processes only those. w8_flags (grid words, optional): the EXT 0
-    // kernel's workgroup w sets word w to whether it skipped a W8 run; the EXT 3 kernel's workgroup w (same grid, same
-    // records) returns at once when it did not, instead of scanning every run of its records again
+    // chunked kernel, the W8 kernels (EXT 3, 4; launch_chunked): w8_split 1 = the EXT 4 kernel alone, 2 = a pair, in
+    // which EXT 4 takes every run but those of long whole records and EXT 3 (launched after it) those. w8_flags (grid
+    // words, optional): the pair's EXT 4 workgroup w sets word w to whether it left a run to EXT 3; the EXT 3
+    // workgroup w (same grid, same records) returns at once when it did not, instead of scanning every run again
     u32 w8_split;
     u32 *w8_flags;
     // the value each workgroup stores into done_flag[w] (the calling host thread's token for this call, never 0)

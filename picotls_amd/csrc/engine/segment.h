@@ -37,7 +37,7 @@ template <int NR, bool OPEN, int NB, int FRAME = 0, bool CT = false, bool W8 = f
 __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 *lds, const u32 (&rk)[NR + 1][4], u32 iv0,
                                             u32 iv1, u32 iv2, const ptls_mi355x_record_t &r, bool valid, u32 m_lo,
                                             u32 m_hi, u32 j, u32 laneoff, u32 tsel_horner, u32x4 &acc, bool finish,
-                                            u32 &okw, bool aligned, u32 ekslot = 0)
+                                            u32 &okw, bool aligned, u32 ekslot = 0, bool w8tree = false)
 {
     constexpr int G = ENGINE_G;
     // W8 (a W8 run of the pair's EXT 3 kernel, gcm_chunked_kernel): Horner on the 8-bit H^8 table (gmul8), the lanes'
@@ -321,7 +321,12 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         // sum over the group of a_l H^(e_l) (rank r = 8 - e owes H^(8 - r)): ((v_0 H + v_1) H + ... + v_7) H by eight
         // group multiplies with the one window-major table H (4 conflict-free lookups per lane each: 32, as
         // coop_last_powers, with one table instead of seven)
-        acc = w8_lane_end(lds, acc, lane_here(), valid ? (u32)G - e_last : j);
+        // (w8tree, the EXT 3 kernel's long whole records: the butterfly over the ranks with H and H^2 nibble-major)
+        const u32 rank = valid ? (u32)G - e_last : j;
+        if (w8tree)
+            acc = w8_tree_end(lds, acc, lane_here(), rank);
+        else
+            acc = w8_lane_end(lds, acc, lane_here(), rank);
         if (valid && m_hi * G >= N && j == jl)  // the segment holds the length block: E(K, J0), on its lane
             acc ^= u32x4(*(const lds_u32x4 *)(lds + ekslot));
     } else if constexpr (TREE) {

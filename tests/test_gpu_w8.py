@@ -1,10 +1,11 @@
-"""Whole-record runs of long records (the chunked kernel's W8 runs: Horner on an 8-bit window-major H^8 table,
-gcm_segment<..., W8>, launched as the EXT 3 half of a kernel pair beside the plain kernel, each skipping the other's
-runs; engine/common.h W8_HORNER) bit-exact against lib/fusion.c: one key and several, AES-128 and AES-256, the 64-step
-threshold inside one run, seal / open / tamper, in place, and batches that mix W8 runs with whole runs of short records
-and with cut runs of mixed lengths, so that both kernels of the pair do work and skip the other's. The reference's
-per-block GHASH amortisation is lib/fusion.c:515-620 (six blocks per reduction); the tests hold for any build (with
-W8_HORNER 0 the same records take the 4-bit path)."""
+"""The W8 kernels (the Horner step on an 8-bit window-major H^8 table, ghash.h gmul8; round 4) bit-exact against
+lib/fusion.c. Every run of an unframed or TLS 1.3-framed chunked batch takes them: EXT 4 (segment ends by a serial lane
+Horner with one window-major H table, w8_lane_end) for cut runs and whole runs of short records, EXT 3 (the butterfly
+end, w8_tree_end) for whole runs of records of at least W8_MIN_STEPS steps, launched after EXT 4 and skipping its runs
+(the EXT 4 workgroups tell it which have none). Cases: one key and several, AES-128 and AES-256, the 64-step threshold
+inside one run, seal / open / tamper, in place, and batches mixing long whole runs with short whole runs and cut runs, so
+that both kernels work and skip the other's runs. The reference's per-block GHASH amortisation is lib/fusion.c:515-620
+(six blocks per reduction); the tests hold for any build (with W8_HORNER 0 the same records take the 4-bit path)."""
 import os
 
 import numpy as np
@@ -71,7 +72,7 @@ def _check(ref, rng, lens, aads, key_size, nkeys, tamper=8):
     ks.free()
 
 
-@pytest.mark.parametrize("key_size,nkeys,n", [(16, 1, 2000), (32, 1, 700), (16, 5, 3000), (32, 3, 1500)])
+@pytest.mark.parametrize("key_size,nkeys,n", [(16, 1, 2048), (32, 1, 2100), (16, 5, 3000), (32, 3, 2500)])
 def test_w8_uniform_long_records_vs_fusion(ref, key_size, nkeys, n):
     # 16 KiB TLS records (129 steps), one key (runs of up to 4096 records) and a few keys (runs cut at key changes)
     rng = np.random.default_rng(8000 + key_size * 10 + nkeys)
@@ -108,7 +109,7 @@ def test_w8_aes256_many_keys_mixed_vs_fusion(ref):
 def test_w8_in_place_vs_fusion(ref):
     # seal in place (ciphertext over plaintext, tag after it) and open in place, 16 KiB records at odd offsets
     rng = np.random.default_rng(8104)
-    n = 600
+    n = 2048
     recs = np.zeros(n, dtype=pa.RECORD_DTYPE)
     off, aoff = 5, 3
     for i in range(n):

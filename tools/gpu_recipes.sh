@@ -46,16 +46,14 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_lifecycle.py tests/test_gpu
 echo "tests rc=$rc"; tail -3 gpurun_out/coh_tests.log; exit $rc
   )
   ;;
-w8cut)
-  # round 4: W8 for cut runs of 16-step units (lib_w8cut) against the shipped W8 (whole runs only, lib_base4) and the
-  # same source with W8_CUT=0 (lib_w8nocut: the 512-unit runs of a pair alone): GPU parity of the new kernel first
+trace2)
+  # kernel trace of tools/ab.py with one library each (args: lib1 lib2 workload records)
   (
-PTLS_MI355X_LIB=$PWD/tools/variants/${W8CUT_LIB:-lib_w8cut.so} timeout -k 10 600 python -u -m pytest tests/test_gpu_w8.py tests/test_gpu_configs.py tests/test_gpu_parity.py tests/test_gpu_ct.py tests/test_gpu_lifecycle.py -m gpu -x -q --timeout 300 --timeout-method thread -k "not vtable" > gpurun_out/w8cut_tests.log 2>&1; rc=$?
-echo "w8cut suite rc=$rc"; tail -3 gpurun_out/w8cut_tests.log; [ $rc -ne 0 ] && { grep -B5 -A30 "Error\|FAILED" gpurun_out/w8cut_tests.log | head -80; exit $rc; }
-V=${W8CUT_AB:-"tools/variants/lib_base4.so tools/variants/lib_w8nocut.so tools/variants/lib_w8cut.so"}
-for w in "mixed 4194304" "mixedrand 4194304" "mixed1key 2097152" "tls16k 1048576" "quic1200 4194304" "mixedconn 4194304"; do set -- $w
-  timeout -k 10 300 python tools/ab.py $V --workload $1 --records $2 --rounds 6 --reps 2 > gpurun_out/w8cut_$1.log 2>&1; rc=$?
-  echo "== $1 rc=$rc"; grep -v amdgpu.ids gpurun_out/w8cut_$1.log | tail -4 | cut -c1-150; [ $rc -ne 0 ] && exit $rc
+R=$GRAFT_REPO_ROOT; cd /tmp && export TMPDIR=/tmp
+for L in $1 $2; do n=$(basename $L .so)
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/trace2_$n -o t -- python3 $R/tools/ab.py $R/$L --workload $3 --records $4 --rounds 3 --reps 2 > $R/gpurun_out/trace2_$n.log 2>&1
+  rc=$?; echo "== $n rc=$rc"; [ $rc -ne 0 ] && { tail -5 $R/gpurun_out/trace2_$n.log; exit $rc; }
+  f=$(ls $R/gpurun_out/trace2_$n/*kernel_stats.csv 2>/dev/null | head -1); [ -n "$f" ] && cut -d, -f1-6 $f | head -8
 done
 exit 0
   )
@@ -64,14 +62,14 @@ w8all)
   # round 4: every run of an unframed batch in the W8 kernel alone (lib_w8all) against the shipped pair (lib_base4)
   # and W8 cut runs in the reordered pair (lib_w8cut_rev): parity of the new variant, bulk A/B, small batches
   (
-PTLS_MI355X_LIB=$PWD/tools/variants/lib_w8all.so timeout -k 10 600 python -u -m pytest tests/test_gpu_w8.py tests/test_gpu_configs.py tests/test_gpu_parity.py tests/test_gpu_ct.py tests/test_gpu_lifecycle.py -m gpu -x -q --timeout 300 --timeout-method thread -k "not vtable" > gpurun_out/w8all_tests.log 2>&1; rc=$?
+PTLS_MI355X_LIB=$PWD/tools/variants/${W8ALL_LIB:-lib_w8all.so} timeout -k 10 600 python -u -m pytest tests/test_gpu_w8.py tests/test_gpu_configs.py tests/test_gpu_parity.py tests/test_gpu_ct.py tests/test_gpu_lifecycle.py tests/test_gpu_tls12.py tests/test_gpu_fuzz.py -m gpu -x -q --timeout 300 --timeout-method thread -k "not vtable" > gpurun_out/w8all_tests.log 2>&1; rc=$?
 echo "w8all suite rc=$rc"; tail -3 gpurun_out/w8all_tests.log; [ $rc -ne 0 ] && { grep -B5 -A30 "Error\|FAILED" gpurun_out/w8all_tests.log | head -80; exit $rc; }
-V="tools/variants/lib_base4.so tools/variants/lib_w8cut_rev.so tools/variants/lib_w8all.so"
+V=${W8ALL_AB:-"tools/variants/lib_base4.so tools/variants/lib_w8cut_rev.so tools/variants/lib_w8all.so"}
 for w in "mixed 4194304" "mixedrand 4194304" "mixedconn 4194304" "mixed1key 2097152" "tls16k 1048576" "quic1200 4194304"; do set -- $w
   timeout -k 10 300 python tools/ab.py $V --workload $1 --records $2 --rounds 6 --reps 2 > gpurun_out/w8all_$1.log 2>&1; rc=$?
   echo "== $1 rc=$rc"; grep -v amdgpu.ids gpurun_out/w8all_$1.log | tail -3 | cut -c1-150; [ $rc -ne 0 ] && exit $rc
 done
-timeout -k 10 300 python tools/small_batch.py tools/variants/lib_base4.so tools/variants/lib_w8all.so --rounds 3 > gpurun_out/w8all_small.log 2>&1; rc=$?
+timeout -k 10 300 python tools/small_batch.py tools/variants/lib_base4.so tools/variants/${W8ALL_LIB:-lib_w8all.so} --rounds 3 > gpurun_out/w8all_small.log 2>&1; rc=$?
 echo "== small batches rc=$rc"; grep -v amdgpu.ids gpurun_out/w8all_small.log | tail -30
 exit $rc
   )
