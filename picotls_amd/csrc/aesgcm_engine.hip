@@ -1131,11 +1131,10 @@ static bool spread_eligible(const ptls_mi355x_keyset_t *ks, size_t nrecs, int fr
     return frame == 0 && nrecs >= 2 && nrecs < (size_t)ks->ds->ncu && nrecs <= SPREAD_MAX_RECS && (ks->ct || use_chunked(ks->schedule));
 }
 
-// a batch that may launch the W8 pair (launch_chunked): chunked, at least one whole-record run's worth
+// a batch that may launch the W8 pair (launch_chunked): chunked, unframed or TLS 1.3-framed, W8_MIN_RECS records
 static bool w8_eligible(const ptls_mi355x_keyset_t *ks, size_t nrecs, int frame)
 {
-    (void)frame;
-    return W8_HORNER && nrecs >= WHOLE_MIN_RECS && (ks->ct || use_chunked(ks->schedule));
+    return W8_HORNER && frame != 2 && nrecs >= W8_MIN_RECS && (ks->ct || use_chunked(ks->schedule));
 }
 
 // orders a launch on `s` that uses the keyset's scratch (spread pieces, W8 flags) after the last launch that used it;
