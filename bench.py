@@ -553,18 +553,20 @@ def run_e2e(R, wl, nchunks: int = 16, reps: int = 3, schedule: str = "auto"):
     return out
 
 
-def lds_model(res, key_size: int):
+def lds_model(res, key_size: int, nrecs: int):
     """The bound the seal kernel actually meets: LDS table lookups. Per GHASH stream block an AES-128
-    block costs 133 ds_read_b32 (AES-256: 197) and its GHASH fold 32 ds_read_b128 (one 4-bit window each); at the MI355X
-    aggregate LDS rates (MI355X_MICROARCH.md: ~75 TB/s ds_read_b32, ~150 TB/s ds_read_b128 with every CU at 2.4 GHz)
-    that gives the chip's block rate ceiling; frac = achieved blocks/s over it (the clock under this load is lower)."""
+    block costs 133 ds_read_b32 (AES-256: 197) and its GHASH fold 16 ds_read_b128 (the W8 kernels' Horner step on the
+    8-bit H^8 table, batches of at least W8_MIN_RECS = 2048 records) or 32 (4-bit windows); at the MI355X aggregate LDS
+    rates (MI355X_MICROARCH.md: ~75 TB/s ds_read_b32, ~150 TB/s ds_read_b128 with every CU at 2.4 GHz) that gives the
+    chip's block rate ceiling; frac = achieved blocks/s over it (the clock under this load is lower)."""
     lookups = 133 if key_size == 16 else 197
-    sec_per_block = lookups * 4 / 75e12 + 32 * 16 / 150e12
+    ghash = 16 if nrecs >= 2048 else 32
+    sec_per_block = lookups * 4 / 75e12 + ghash * 16 / 150e12
     peak = 1.0 / sec_per_block
     achieved = res["stream_blocks"] / (res["seal_ms"] / 1e3)
     return {"bound": "lds", "unit": "stream blocks/s", "achieved": round(achieved, -6), "peak_at_2.4GHz": round(peak, -6),
             "frac": round(achieved / peak, 4),
-            "per_block": f"{lookups} ds_read_b32 (AES) + 32 ds_read_b128 (GHASH)"}
+            "per_block": f"{lookups} ds_read_b32 (AES) + {ghash} ds_read_b128 (GHASH)"}
 
 
 def traffic_from_profiles(workload: str, records: int, key: str = "seal_hbm_bytes_per_launch"):
@@ -627,16 +629,16 @@ def main():
         "open_GiBps": round(res["payload_bytes"] / open_s / 2**30, 3),
         "roofline": {"bound": "hbm", "kernel": f"{'gcm_batch_kernel' if args.schedule == 'lockstep' else 'gcm_chunked_kernel'}"
                                                f"<{10 if wl.key_size == 16 else 14},seal>",
-                     # (one seal launch is the W8 pair, EXT 0 + EXT 3, when a workgroup can hold whole-record runs:
+                     # (one seal launch of W8_MIN_RECS = 2048 records or more is the W8 pair, EXT 4 + EXT 3:
                      # avg_launch_ms covers both, and profiles/pmc_<workload>.json sums their bytes)
-                     "launch": "w8 pair" if args.schedule != "lockstep" and res["records"] >= 256 * 128 else "single",
+                     "launch": "w8 pair" if args.schedule != "lockstep" and res["records"] >= 2048 else "single",
                      "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic_from_profiles(wl.name, res["records"]),
                      "alg_bytes_per_launch": res["seal_alg_bytes"], "avg_launch_ms": round(res["seal_ms"], 4),
                      "open_achieved": round(res["open_alg_bytes"] / open_s / 1e9, 2),
                      "open_alg_bytes_per_launch": res["open_alg_bytes"],
                      "open_traffic": traffic_from_profiles(wl.name, res["records"], "open_hbm_bytes_per_launch")},
-        "lds_model": lds_model(res, wl.key_size),
+        "lds_model": lds_model(res, wl.key_size, res["records"]),
         "verified": {"roundtrip": res.get("verified_roundtrip"), "fusion_spot_check": None},
     }
     samples = {wl.name: res.get("sample")}
