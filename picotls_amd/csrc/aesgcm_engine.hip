@@ -28,6 +28,7 @@
 // 4c..4c+3 = AES state column c. GHASH elements use the same byte order (byte 0 holds x^0..x^7, MSB first).
 
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <mutex>
@@ -512,8 +513,9 @@ struct st_ptls_mi355x_keyset_t {
     hipStream_t spread_stream;
     bool spread_used;
     // W8 launch pairs (launch_chunked, W8_HORNER): one word per workgroup from the pair's first kernel to its second,
-    // allocated on first use; ordered across streams like the spread scratch (spread_stream / spread_used)
-    u32 *d_w8flags;
+    // one buffer per stream (allocated on the stream's first pair; a stream orders its own pairs), so that pairs on
+    // several streams run concurrently; at most W8_FLAG_STREAMS, the oldest taken over by a new stream in stream order
+    std::vector<std::pair<hipStream_t, u32 *>> w8flags;
 };
 
 static int mark_ready(ptls_mi355x_keyset_t *ks, hipStream_t s);
@@ -778,8 +780,9 @@ void ptls_mi355x_keyset_free(ptls_mi355x_keyset_t *ks)
         (void)hipFreeAsync(ks->d_group, ds->maint);
     if (ks->d_spread != nullptr)
         (void)hipFreeAsync(ks->d_spread, ds->maint);
-    if (ks->d_w8flags != nullptr)
-        (void)hipFreeAsync(ks->d_w8flags, ds->maint);
+    for (auto &f : ks->w8flags)
+        (void)hipFreeAsync(f.second, ds->maint);
+    ks->w8flags.clear();
     if (ks->slot) {
         // back to the pool once the clear has run (slot_get checks the event)
         hipEvent_t cleared = event_get(ds);
@@ -1137,7 +1140,7 @@ static bool w8_eligible(const ptls_mi355x_keyset_t *ks, size_t nrecs, int frame)
     return W8_HORNER && frame != 2 && nrecs >= W8_MIN_RECS && (ks->ct || use_chunked(ks->schedule));
 }
 
-// orders a launch on `s` that uses the keyset's scratch (spread pieces, W8 flags) after the last launch that used it;
+// orders a launch on `s` that uses the keyset's spread scratch after the last launch that used it;
 // the caller holds ks->mu from here through the launch and the use event recorded after it (launch_batch)
 static int scratch_order_locked(ptls_mi355x_keyset_t *ks, hipStream_t s)
 {
@@ -1154,17 +1157,39 @@ static int scratch_order_locked(ptls_mi355x_keyset_t *ks, hipStream_t s)
     return 0;
 }
 
-// the keyset's W8 flag words for a launch on `s` (allocated in stream order on first use; every word is written by
-// the pair's first kernel before its second reads it); nullptr on failure (the pair then runs without them)
+// the keyset's W8 flag words for a launch on `s`: the stream's own buffer (every word is written by the pair's first
+// kernel before its second reads it, and a stream runs its pairs in order), allocated in stream order on the stream's
+// first pair. A stream beyond W8_FLAG_STREAMS takes over the least recently used buffer after that buffer's last use
+// (the keyset's use event on its stream). nullptr on failure: the pair then runs without them (EXT 3 scans every run).
+// The caller holds ks->mu through the launch and its use event (launch_batch).
+#define W8_FLAG_STREAMS 8
 static u32 *w8_flags_locked(ptls_mi355x_keyset_t *ks, hipStream_t s)
 {
-    if (scratch_order_locked(ks, s) != 0)
-        return nullptr;
-    if (ks->d_w8flags == nullptr && hipMallocAsync((void **)&ks->d_w8flags, 4 * (size_t)ks->ds->ncu, s) != hipSuccess) {
-        (void)hipGetLastError();
-        ks->d_w8flags = nullptr;
+    auto &v = ks->w8flags;
+    for (size_t i = 0; i < v.size(); ++i) {
+        if (v[i].first == s) {
+            std::rotate(v.begin() + i, v.begin() + i + 1, v.end());  // most recently used last
+            return v.back().second;
+        }
     }
-    return ks->d_w8flags;
+    if (v.size() < W8_FLAG_STREAMS) {
+        u32 *f = nullptr;
+        if (hipMallocAsync((void **)&f, 4 * (size_t)ks->ds->ncu, s) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        v.emplace_back(s, f);
+        return f;
+    }
+    const hipStream_t prev = v.front().first;
+    for (auto &u : ks->uses)
+        if (u.first == prev && hipStreamWaitEvent(s, u.second, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+    v.front().first = s;
+    std::rotate(v.begin(), v.begin() + 1, v.end());
+    return v.back().second;
 }
 
 // the keyset's spread scratch for a launch on `s` (allocated and zeroed in stream order on first use); nullptr on

@@ -142,3 +142,34 @@ def _record_mask(recs, size):
     for r in recs:
         m[int(r["in_off"]):int(r["in_off"]) + int(r["len"])] = True
     return m
+
+
+def test_w8_pairs_on_many_streams_vs_fusion(ref):
+    """W8 pairs of one keyset on 12 streams at once (more than W8_FLAG_STREAMS = 8, so streams take over the least
+    recently used flag buffer): each stream has its own flag words, so the pairs run concurrently; every batch (long
+    whole runs, short whole runs and cut runs, so that both kernels of each pair skip runs) equals fusion, twice over."""
+    rng = np.random.default_rng(8105)
+    nstreams, n = 12, 2048
+    key = np.frombuffer(rng.bytes(16), np.uint8)
+    iv = np.frombuffer(rng.bytes(12), np.uint8)
+    ks = pa.Keyset(key, iv, 16)
+    jobs = []
+    for i in range(nstreams):
+        lens = np.concatenate([np.full(n // 4, 16384), np.full(n // 4, 1200), rng.integers(64, 16385, n // 2)])
+        b = RecordBatch.build(lens, np.full(n, 13), seqs=rng.integers(0, 2**62, n, dtype=np.uint64))
+        pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+        aad = np.frombuffer(rng.bytes(b.aad_bytes), np.uint8)
+        want = np.zeros(b.sealed_bytes, np.uint8)
+        ref.run_batch(True, key, iv, 16, b.seal, pt, aad, want, nthreads=8)
+        jobs.append((b, dev(b.seal), dev(pt), dev(aad), empty(b.sealed_bytes), want))
+    streams = [torch.cuda.Stream() for _ in range(nstreams)]
+    torch.cuda.synchronize()
+    for rnd in range(2):
+        for (b, d_recs, d_pt, d_aad, d_out, _), st in zip(jobs, streams if rnd == 0 else streams[::-1]):
+            with torch.cuda.stream(st):
+                d_out.fill_(0)
+            pa.seal_batch(ks, d_recs.data_ptr(), n, d_pt.data_ptr(), d_aad.data_ptr(), d_out.data_ptr(), st.cuda_stream)
+        torch.cuda.synchronize()
+        for i, (b, _, _, _, d_out, want) in enumerate(jobs):
+            assert np.array_equal(d_out[:b.sealed_bytes].cpu().numpy(), want), f"round {rnd}, stream {i}"
+    ks.free()
