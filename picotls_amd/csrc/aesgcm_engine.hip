@@ -195,6 +195,9 @@ static int set_kernel_attrs(void)
 #if W8_HORNER
     CHUNKED_ATTR_W8(0);
     CHUNKED_ATTR_W8(1);
+#if W8_TLS12
+    CHUNKED_ATTR_W8(2);
+#endif
 #endif
 #undef CHUNKED_ATTR_W8
     CHUNKED_ATTR(10, false, 0);
@@ -945,9 +948,9 @@ static void launch_chunked(bool ct, unsigned grid, hipStream_t s, const BatchArg
     // other's runs and EXT 3 returning at once in the workgroups where EXT 4 saw none (BatchArgs::w8_split, w8_flags).
     // A batch of fewer than WHOLE_MIN_RECS records per workgroup in contiguous ranges holds no whole-record run: EXT 4
     // alone. Not for a per-record launch (it publishes completion words, and its 1-16-step units suit the 4-bit path),
-    // a batch of fewer than W8_MIN_RECS records (the table build is not repaid), nor TLS 1.2 framing (its seal kernels
-    // would spill: 96 bytes per lane).
-    if constexpr (W8_HORNER && FRAME != 2) {
+    // nor a batch of fewer than W8_MIN_RECS records (the table build is not repaid). TLS 1.2 framing only with W8_TLS12
+    // (on: faster despite EXT 4's 96-byte-per-lane seal spill, common.h).
+    if constexpr (W8_HORNER && (FRAME != 2 || W8_TLS12)) {
         if (!a.one_inline && a.done_flag == nullptr && a.nrecs >= W8_MIN_RECS) {
             const bool whole_possible = a.chunk != 0 || a.bounds != nullptr || (a.nrecs + grid - 1) / grid >= WHOLE_MIN_RECS;
             BatchArgs b = a;
@@ -1134,10 +1137,10 @@ static bool spread_eligible(const ptls_mi355x_keyset_t *ks, size_t nrecs, int fr
     return frame == 0 && nrecs >= 2 && nrecs < (size_t)ks->ds->ncu && nrecs <= SPREAD_MAX_RECS && (ks->ct || use_chunked(ks->schedule));
 }
 
-// a batch that may launch the W8 pair (launch_chunked): chunked, unframed or TLS 1.3-framed, W8_MIN_RECS records
+// a batch that may launch the W8 pair (launch_chunked): chunked, W8_MIN_RECS records (TLS 1.2 framing with W8_TLS12)
 static bool w8_eligible(const ptls_mi355x_keyset_t *ks, size_t nrecs, int frame)
 {
-    return W8_HORNER && frame != 2 && nrecs >= W8_MIN_RECS && (ks->ct || use_chunked(ks->schedule));
+    return W8_HORNER && (frame != 2 || W8_TLS12) && nrecs >= W8_MIN_RECS && (ks->ct || use_chunked(ks->schedule));
 }
 
 // orders a launch on `s` that uses the keyset's spread scratch after the last launch that used it;

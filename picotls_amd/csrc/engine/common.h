@@ -153,6 +153,11 @@ __device__ __forceinline__ u32 lane_here()
 #ifndef W8_MIN_STEPS
 #define W8_MIN_STEPS 64
 #endif
+#ifndef W8_TLS12
+// TLS 1.2-framed batches in the W8 kernels too, although EXT 4's TLS 1.2 seal spills 96 B per lane: 131072 x 16 KiB
+// records 1036.9 -> 1172.1 GiB/s seal+open, 1M x 1200 B 907.2 -> 979.1 (tools/ab_tls12.py, profiles/r4/tls12_w8_ab.txt)
+#define W8_TLS12 1
+#endif
 #ifndef W8_MIN_RECS
 // batches of fewer records keep the 4-bit kernel: the 8-bit table's build is not repaid (256 x 16 KiB -5 %, 1000 x 1200 B
 // -4 %, 1000 x 16 KiB even, 4096 x 16 KiB +7 %; profiles/r4/w8all_ab.txt)

@@ -355,3 +355,100 @@ def test_tls13_many_key_large_framed_batch_balanced():
     got = np.concatenate([plain[int(o):int(o) + int(ln)] for o, ln in zip(orecs["out_off"], lens)])
     assert np.array_equal(got, data)
     ks.free()
+
+
+def _tls12_batch(rng, lens, nkeys, key_size):
+    """TLS 1.2 records back to back: explicit nonce || payload in, header || nonce || ciphertext || tag out."""
+    n = len(lens)
+    keys = rng.bytes(nkeys * key_size)
+    fixed = rng.bytes(nkeys * 4)
+    ivs = b"".join(fixed[4 * k:4 * k + 4] + bytes(8) for k in range(nkeys))
+    recs = np.zeros(n, dtype=pa.RECORD_DTYPE)
+    recs["len"] = lens
+    recs["in_off"] = np.concatenate([[0], np.cumsum(lens + 8)[:-1]])
+    recs["out_off"] = np.concatenate([[0], np.cumsum(lens + 29)[:-1]])
+    recs["seq"] = rng.integers(0, 2**62, n, dtype=np.uint64)
+    recs["flags"] = 23
+    recs["key_idx"] = np.arange(n) * nkeys // n
+    arena = np.frombuffer(rng.bytes(int((lens + 8).sum())), np.uint8).copy()
+    return keys, ivs, recs, arena
+
+
+def _tls12_expect(ref, keys, ivs, key_size, recs, arena, i):
+    k, ln, p = int(recs["key_idx"][i]), int(recs["len"][i]), int(recs["in_off"][i])
+    nonce = arena[p:p + 8].tobytes()
+    aad = int(recs["seq"][i]).to_bytes(8, "big") + bytes([23, 3, 3]) + ln.to_bytes(2, "big")
+    return (bytes([23, 3, 3]) + (ln + 24).to_bytes(2, "big") + nonce +
+            ref.seal(keys[k * key_size:(k + 1) * key_size], ivs[12 * k:12 * k + 12], int.from_bytes(nonce, "big"), aad,
+                     arena[p + 8:p + 8 + ln].tobytes()))
+
+
+@pytest.mark.parametrize("key_size,nkeys,n,long_runs", [(16, 3, 2600, False), (32, 1, 2100, False), (16, 1, 256 * 130, True)])
+def test_tls12_w8_kernels_vs_fusion(ref, key_size, nkeys, n, long_runs):
+    """TLS 1.2 framing in the W8 kernels (batches of at least W8_MIN_RECS = 2048 records): random lengths (EXT 4's cut
+    runs), and 33,280 records of 16 KiB, 130 per workgroup (EXT 3's whole runs of long records). Every record (the long
+    batch: 400 sampled and the ends) equals lib/fusion.c's seal with the record-layer nonce and AAD, nothing outside the
+    wire records is written, and every record opens back to its payload."""
+    rng = np.random.default_rng(1200 + n + key_size)
+    lens = np.full(n, 16384) if long_runs else rng.integers(0, 16385, n)
+    keys, ivs, recs, arena = _tls12_batch(rng, lens, nkeys, key_size)
+    ks = pa.Keyset(keys, ivs, key_size)
+    wire_len = int((lens + 29).sum())
+    out = _seal(ks, recs, arena, wire_len + 3)
+    check = list(rng.choice(n, 400, replace=False)) + [0, n - 1] if long_runs else range(n)
+    for i in check:
+        o = int(recs["out_off"][i])
+        want = _tls12_expect(ref, keys, ivs, key_size, recs, arena, i)
+        assert out[o:o + len(want)].tobytes() == want, i
+    assert (out[wire_len:] == 0xEE).all()
+    precs = recs.copy()
+    precs["in_off"] = recs["out_off"]
+    precs["out_off"] = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    plain, ok, res = _open(ks, precs, out[:wire_len].tobytes(), int(lens.sum()))
+    assert ok.all() and (res["status"] == pa.TLS_OK).all()
+    src = arena.reshape(n, 8 + 16384)[:, 8:].reshape(-1) if long_runs else np.concatenate(
+        [arena[int(recs["in_off"][i]) + 8:int(recs["in_off"][i]) + 8 + int(lens[i])] for i in range(n)])
+    assert np.array_equal(plain[:int(lens.sum())], src)
+    ks.free()
+
+
+def test_tls13_w8_tree_kernel_long_records_vs_fusion(ref):
+    """TLS 1.3 framing in the EXT 3 kernel: 33,280 records of 16 KiB (130 per workgroup: whole runs of long records) of
+    two connections; sampled records equal header || fusion's seal of payload || type under the header as AAD, and every
+    record opens back."""
+    rng = np.random.default_rng(1313)
+    n, nkeys, ln = 256 * 130, 2, 16384
+    keys, ivs = rng.bytes(16 * nkeys), rng.bytes(12 * nkeys)
+    data = np.frombuffer(rng.bytes(n * ln), np.uint8)
+    recs = np.zeros(n, dtype=pa.RECORD_DTYPE)
+    recs["len"] = ln
+    recs["in_off"] = np.arange(n, dtype=np.uint64) * ln
+    recs["out_off"] = np.arange(n, dtype=np.uint64) * (ln + 22)
+    recs["key_idx"] = np.arange(n) * nkeys // n
+    recs["seq"] = rng.integers(0, 2**40, n)
+    recs["flags"] = 23
+    ks = pa.Keyset(keys, ivs, 16)
+    s = torch.cuda.current_stream().cuda_stream
+    d_recs, d_in, d_out = dev(recs), dev(data), empty(n * (ln + 22), 0xEE)
+    pa.seal_tls_records(ks, d_recs.data_ptr(), n, d_in.data_ptr(), d_out.data_ptr(), s)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    hdr = bytes([23, 3, 3, (ln + 17) >> 8, (ln + 17) & 0xFF])
+    for i in list(rng.choice(n, 400, replace=False)) + [0, n - 1]:
+        k, o, p = int(recs["key_idx"][i]), int(recs["out_off"][i]), int(recs["in_off"][i])
+        want = hdr + ref.seal(keys[16 * k:16 * k + 16], ivs[12 * k:12 * k + 12], int(recs["seq"][i]), hdr,
+                              data[p:p + ln].tobytes() + b"\x17")
+        assert out[o:o + len(want)].tobytes() == want, i
+    orecs = np.zeros(n, dtype=pa.RECORD_DTYPE)
+    orecs["in_off"], orecs["len"], orecs["seq"], orecs["key_idx"] = recs["out_off"], ln + 1, recs["seq"], recs["key_idx"]
+    orecs["out_off"] = np.arange(n, dtype=np.uint64) * (ln + 1)
+    d_recs2, d_plain = dev(orecs), empty(n * (ln + 1) + 1)
+    d_ok, d_res = empty(n, 0x77), empty(8 * n, 0x77)
+    pa.open_tls_records(ks, d_recs2.data_ptr(), n, d_out.data_ptr(), d_plain.data_ptr(), d_ok.data_ptr(), d_res.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert d_ok.cpu().numpy().all()
+    res = d_res.cpu().numpy().view(pa.TLS_RESULT_DTYPE)
+    assert (res["status"] == pa.TLS_OK).all() and (res["plain_len"] == ln).all()
+    plain = d_plain.cpu().numpy()[:n * (ln + 1)].reshape(n, ln + 1)
+    assert np.array_equal(plain[:, :ln].reshape(-1), data)
+    ks.free()

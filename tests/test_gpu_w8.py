@@ -1,5 +1,5 @@
 """The W8 kernels (the Horner step on an 8-bit window-major H^8 table, ghash.h gmul8; round 4) bit-exact against
-lib/fusion.c. Every run of an unframed or TLS 1.3-framed chunked batch takes them: EXT 4 (segment ends by a serial lane
+lib/fusion.c. Every run of a chunked batch of at least W8_MIN_RECS records takes them (unframed or TLS framed): EXT 4 (segment ends by a serial lane
 Horner with one window-major H table, w8_lane_end) for cut runs and whole runs of short records, EXT 3 (the butterfly
 end, w8_tree_end) for whole runs of records of at least W8_MIN_STEPS steps, launched after EXT 4 and skipping its runs
 (the EXT 4 workgroups tell it which have none). Cases: one key and several, AES-128 and AES-256, the 64-step threshold
@@ -173,3 +173,18 @@ def test_w8_pairs_on_many_streams_vs_fusion(ref):
         for i, (b, _, _, _, d_out, want) in enumerate(jobs):
             assert np.array_equal(d_out[:b.sealed_bytes].cpu().numpy(), want), f"round {rnd}, stream {i}"
     ks.free()
+
+
+@pytest.mark.parametrize("key_size,nkeys", [(16, 1), (32, 3)])
+def test_w8_tree_kernel_long_whole_runs_vs_fusion(ref, key_size, nkeys):
+    """The EXT 3 kernel (butterfly segment ends) takes whole runs of records of at least W8_MIN_STEPS steps, which need
+    at least 128 records per workgroup: 33,280 records of 16 KiB (130 per workgroup at 256 CUs; one key in dealt
+    contiguous ranges, or three keys in work-balanced ranges), with 1200-byte records (EXT 4's whole runs) and cut runs
+    mixed in at the front so that both kernels of the pair work and skip each other's runs; every record and tag
+    against fusion, then opened with tampering."""
+    rng = np.random.default_rng(8200 + key_size + nkeys)
+    n = 256 * 130
+    lens = np.full(n, 16384)
+    lens[:600] = 1200
+    lens[600:900] = rng.integers(64, 16385, 300)
+    _check(ref, rng, lens, np.full(n, 13), key_size, nkeys, tamper=12)
