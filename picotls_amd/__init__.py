@@ -27,7 +27,8 @@ from .records import (CID_DTYPE, HP_DTYPE, QUICLB_MAX_LEN, QUICLB_MIN_LEN, RECOR
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 # PTLS_MI355X_LIB: another build of the same engine (an A/B variant under tools/variants/) for the GPU suite
-LIB_PATH = os.environ.get("PTLS_MI355X_LIB") or os.path.join(_PKG, "_lib", "libptls_mi355x.so")
+_DEFAULT_LIB = os.path.join(_PKG, "_lib", "libptls_mi355x.so")
+LIB_PATH = os.environ.get("PTLS_MI355X_LIB") or _DEFAULT_LIB
 PICOTLS_LIB_PATH = os.path.join(_PKG, "_lib", "libptls_mi355x_picotls.so")
 
 # every function of include/picotls/mi355x.h (tests check the .so exports exactly these)
@@ -81,6 +82,12 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     if not os.path.exists(path):
         raise EngineError(f"{path} is missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
                           "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    if path == _DEFAULT_LIB:  # the in-tree build must be of the sources beside it (build.py's digest stamp)
+        from . import build as _b
+
+        if os.path.exists(_b.ENGINE_SRCS[0]) and _b._stamp(path) != _b.engine_digest():
+            raise EngineError(f"{path} was not built from the current sources (its {path}.sha256 differs): rebuild with "
+                              "`python -c 'import __graft_entry__ as g; g.build()'`")
     lib = ctypes.CDLL(path)
     vp, sz, u64, ci = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int
     lib.ptls_mi355x_is_supported.restype = ci

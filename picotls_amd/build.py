@@ -5,6 +5,7 @@
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
@@ -28,23 +29,55 @@ ENGINE_PARTS = sorted(os.path.join(PKG, "csrc", "engine", f) for f in os.listdir
                       if f.endswith(".h"))  # included by aesgcm_engine.hip (one translation unit)
 
 
-def _stale(target: str, deps: list[str]) -> bool:
-    if not os.path.exists(target):
-        return True
-    t = os.path.getmtime(target)
-    return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
+def source_digest(files: list[str], extra: str = "") -> str:
+    """SHA-256 over the sources' paths and contents (and the compile settings): a built library carries the digest of
+    what it was built from (<lib>.sha256 beside it), so a rebuild is decided by content, not by file times, and
+    load_library refuses an in-tree library whose sources changed since (picotls_amd/__init__.py)."""
+    h = hashlib.sha256(extra.encode())
+    for f in sorted(files):
+        h.update(os.path.relpath(f, ROOT).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def engine_digest() -> str:
+    return source_digest(ENGINE_SRCS + ENGINE_PARTS + HEADERS, " ".join([ARCH, *ENGINE_FLAGS]))
+
+
+def picotls_digest() -> str:
+    return source_digest(PICOTLS_SRCS + HEADERS, engine_digest())
+
+
+def _stamp(lib: str) -> str | None:
+    try:
+        with open(lib + ".sha256") as fh:
+            return fh.read().strip()
+    except OSError:
+        return None
+
+
+def _stale(lib: str, digest: str) -> bool:
+    return not os.path.exists(lib) or _stamp(lib) != digest
+
+
+def _install(tmp: str, lib: str, digest: str) -> None:
+    os.replace(tmp, lib)
+    with open(lib + ".sha256", "w") as fh:
+        fh.write(digest + "\n")
 
 
 def build_engine(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(LIB_DIR, exist_ok=True)
-    if force or _stale(ENGINE_SO, ENGINE_SRCS + ENGINE_PARTS + HEADERS):
+    digest = engine_digest()
+    if force or _stale(ENGINE_SO, digest):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result",
                "-Wno-unused-value", *ENGINE_FLAGS, "-I", os.path.join(ROOT, "include"), *ENGINE_SRCS,
                "-o", ENGINE_SO + ".tmp"]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
-        os.replace(ENGINE_SO + ".tmp", ENGINE_SO)
+        _install(ENGINE_SO + ".tmp", ENGINE_SO, digest)
     return ENGINE_SO
 
 
@@ -52,7 +85,8 @@ def build_picotls_backend(force: bool = False, verbose: bool = False) -> str | N
     """The picotls vtable adapter needs picotls.h at build time (a picotls installation; here the reference tree)."""
     if not os.path.exists(os.path.join(PICOTLS_INCLUDE, "picotls.h")):
         return PICOTLS_SO if os.path.exists(PICOTLS_SO) else None
-    if force or _stale(PICOTLS_SO, PICOTLS_SRCS + HEADERS + [ENGINE_SO]):
+    digest = picotls_digest()
+    if force or _stale(PICOTLS_SO, digest):
         cc = shutil.which("gcc") or "cc"
         cmd = [cc, "-std=gnu99", "-O2", "-fPIC", "-shared", "-Wall", "-I", os.path.join(ROOT, "include"), "-I",
                PICOTLS_INCLUDE, *PICOTLS_SRCS, "-L", LIB_DIR, "-lptls_mi355x", "-Wl,-rpath,$ORIGIN",
@@ -60,7 +94,7 @@ def build_picotls_backend(force: bool = False, verbose: bool = False) -> str | N
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
-        os.replace(PICOTLS_SO + ".tmp", PICOTLS_SO)
+        _install(PICOTLS_SO + ".tmp", PICOTLS_SO, digest)
     return PICOTLS_SO
 
 

@@ -85,3 +85,22 @@ def test_no_cpu_fallback_when_library_missing(tmp_path):
             pa.load_library(str(tmp_path / "missing.so"))
     finally:
         pa._lib = saved
+
+
+def test_in_tree_library_is_built_from_the_current_sources(tmp_path):
+    """build.py stamps each library with the SHA-256 of its sources and compile settings (<lib>.sha256), so a rebuild
+    follows content rather than file times; the in-tree engine library carries the digest of the sources beside it
+    (load_library refuses it otherwise), and the digest moves with any source byte."""
+    from picotls_amd import build as b
+
+    if os.environ.get("PTLS_MI355X_LIB"):
+        pytest.skip("a variant library is loaded instead of the in-tree build")
+    assert b._stamp(b.ENGINE_SO) == b.engine_digest()
+    if os.path.exists(b.PICOTLS_SO + ".sha256"):
+        assert b._stamp(b.PICOTLS_SO) == b.picotls_digest()
+    f = tmp_path / "x.h"
+    f.write_text("int a;\n")
+    d0 = b.source_digest([str(f)])
+    f.write_text("int b;\n")
+    assert b.source_digest([str(f)]) != d0
+    assert b.source_digest([str(f)], "gfx950") != b.source_digest([str(f)], "gfx942")
