@@ -1040,6 +1040,9 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             unit_of(u, lo, first, unc, k_back);
             if (OPEN && okw <= 1)  // a whole record's tag check (its length lane)
                 args.ok[ok_at(pos + lo)] = (uint8_t)okw;
+#if ENGINE_PROFILE
+            PROF_STAMP(tc0);
+#endif
             if (unc > 1) {  // uniform over the group; a rejected descriptor is always one unit
                 u32 last = 0;
                 if (j == G - 1) {
@@ -1081,6 +1084,10 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                     }
                 }
             }
+#if ENGINE_PROFILE
+            if (lane_here() == 0)  // [11] wave cycles in the unit's combine tail, [12] unit rounds of the wave
+                PROF_ADD(11, stamp() - tc0), PROF_ADD(12, 1);
+#endif
         }
         // the run's units are all handed out: the first wave to get here scans the next run into the other buffer
         // while the rest finish theirs

@@ -59,6 +59,9 @@ def main():
     if p[10]:
         print("  prologue split (cycles/workgroup): AES tables (waves 1-15) %.0f | first run scan (wave 0) %.0f" %
               (p[8] / p[10], p[9] / p[10]))
+    if p[12]:
+        print(f"  unit tails (partial store, record combine, tag): {p[11] / p[12]:.0f} cycles per wave-round, "
+              f"{100 * p[11] / 16 / max(p[2], 1):.1f} % of the unit loop")
     waves = 16
     print(f"  wave idle at unit-loop barrier: {p[4] / runs / waves:.0f} cycles/run/wave "
           f"({100 * p[4] / waves / max(p[2], 1):.1f} % of the unit loop)")
