@@ -2,7 +2,8 @@
 # The one-off GPU measurement recipes of rounds 2-3 (interleaved A/Bs of engine variants, counter passes, latency
 # sweeps), kept in one file so that the profiles/ files they produced can name their source:
 #   bash tools/gpu_recipes.sh <name>    (run on the GPU box through gpurun, from the repository root)
-# Variant libraries (tools/variants/*.so) are built beforehand with tools/mkvariant.sh; the recurring drivers stay
+# Variant libraries (tools/variants/*.so) are built beforehand with tools/mkvariant.sh (and ./tools/variants taken out of
+# .gpurunignore for the calls that use them: it is listed there so that ordinary GPU calls do not carry them); the recurring drivers stay
 # separate: tools/gpu_tests.sh (GPU parity suite), tools/gpu_prof.sh (rocprofv3 passes), tools/gpu_mt.sh and
 # tools/gpu_lat_ab.sh (per-record rates and latency), tools/ab.sh / tools/ab.py (A/B of variants).
 set +e
