@@ -79,10 +79,11 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     }
 }
 
-// One workgroup: GHASH = sum_s part[s] M^s with M = (H^128)^(2^e), the record's tag: written after the ciphertext
-// (seal) or compared with the received one (open, ok[0]). Constant-time as it stands: every product is a gmul_tab in
-// which all threads read the same window row of the same table.
-static_assert(CHUNK_BLOCKS == 128, "span_combine_kernel takes M = H^(CHUNK_BLOCKS 2^e) from the keyset's H^128 .. H^1024");
+// One workgroup: GHASH = sum_s part[s] M^s with M = (H^CHUNK_BLOCKS)^(2^e), the record's tag: written after the
+// ciphertext (seal) or compared with the received one (open, ok[0]). Constant-time as it stands: every product is a
+// gmul_tab in which all threads read the same window row of the same table.
+static_assert((CHUNK_BLOCKS & (CHUNK_BLOCKS - 1)) == 0 && CHUNK_BLOCKS >= 8 && CHUNK_BLOCKS <= 1024,
+              "span_combine_kernel starts M = H^(CHUNK_BLOCKS 2^e) from a power H^(2^m), m <= 10, of the keyset");
 template <bool OPEN>
 __global__ __launch_bounds__(256) void span_combine_kernel(BatchArgs args, u32 nspans, u32 e, const u32x4 *part)
 {
@@ -93,12 +94,15 @@ __global__ __launch_bounds__(256) void span_combine_kernel(BatchArgs args, u32 n
     lds_u32x4 *s_pow = s_val + 256;                               // the level's multiplier
     const u32 t = threadIdx.x;
     s_val[t] = t < nspans ? part[t] : u32x4{0, 0, 0, 0};
+    // M = H^(2^m0), m0 = log2(CHUNK_BLOCKS) + e: the keyset holds H^(2^m) up to m = 10 (H^1024), the rest are squarings
+    constexpr u32 CL = __builtin_ctz(CHUNK_BLOCKS);
+    const u32 m0 = CL + e, mb = m0 < 10u ? m0 : 10u;
     if (t == 0) {
-        const u32 *h = args.keys->h[e <= 3 ? 12 + e : 15];  // H^(128 * 2^min(e, 3)): H^128 .. H^1024 (keyset)
+        const u32 *h = args.keys->h[key_pow2_idx(mb)];
         *s_pow = u32x4{h[0], h[1], h[2], h[3]};
     }
     __syncthreads();
-    for (u32 i = 3; i < e; ++i) {  // M = (H^128)^(2^e): the squarings left (a table of the element, then one product)
+    for (u32 i = mb; i < m0; ++i) {  // the squarings left (a table of the element, then one product)
         build_elem_table(lds, 0, *s_pow);
         __syncthreads();
         const u32x4 sq = gmul_tab(lds, *s_pow, 0);
