@@ -188,3 +188,52 @@ def test_w8_tree_kernel_long_whole_runs_vs_fusion(ref, key_size, nkeys):
     lens[:600] = 1200
     lens[600:900] = rng.integers(64, 16385, 300)
     _check(ref, rng, lens, np.full(n, 13), key_size, nkeys, tamper=12)
+
+
+def test_w8_pairs_from_many_threads_vs_fusion(ref):
+    """Ten threads, each on its own stream, seal their own batches through one shared keyset three times over: the
+    per-stream flag buffers are taken under the keyset's lock, and past W8_FLAG_STREAMS = 8 streams the least recently
+    used one is taken over after its stream's last use, while the launches overlap on the device. Every output equals
+    fusion's."""
+    import threading
+
+    rng = np.random.default_rng(8106)
+    nthreads, n = 10, 2048
+    key = np.frombuffer(rng.bytes(32), np.uint8)
+    iv = np.frombuffer(rng.bytes(12), np.uint8)
+    ks = pa.Keyset(key, iv, 32)
+    jobs = []
+    for t in range(nthreads):
+        lens = np.concatenate([np.full(n // 2, 1200), rng.integers(64, 16385, n // 2)])
+        b = RecordBatch.build(lens, np.full(n, 13), seqs=rng.integers(0, 2**62, n, dtype=np.uint64))
+        pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+        aad = np.frombuffer(rng.bytes(b.aad_bytes), np.uint8)
+        want = np.zeros(b.sealed_bytes, np.uint8)
+        ref.run_batch(True, key, iv, 32, b.seal, pt, aad, want, nthreads=8)
+        jobs.append((b, dev(b.seal), dev(pt), dev(aad), [empty(b.sealed_bytes) for _ in range(3)], want))
+    torch.cuda.synchronize()
+    errors = []
+
+    def worker(t):
+        try:
+            b, d_recs, d_pt, d_aad, outs, _ = jobs[t]
+            st = torch.cuda.Stream()
+            for k in range(3):
+                with torch.cuda.stream(st):
+                    outs[k].fill_(0)
+                pa.seal_batch(ks, d_recs.data_ptr(), n, d_pt.data_ptr(), d_aad.data_ptr(), outs[k].data_ptr(), st.cuda_stream)
+            st.synchronize()
+        except Exception as e:  # reported below
+            errors.append(f"thread {t}: {e!r}")
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(nthreads)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    torch.cuda.synchronize()
+    assert errors == []
+    for t, (b, _, _, _, outs, want) in enumerate(jobs):
+        for k, o in enumerate(outs):
+            assert np.array_equal(o[:b.sealed_bytes].cpu().numpy(), want), f"thread {t}, launch {k}"
+    ks.free()
