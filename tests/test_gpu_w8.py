@@ -237,3 +237,16 @@ def test_w8_pairs_from_many_threads_vs_fusion(ref):
         for k, o in enumerate(outs):
             assert np.array_equal(o[:b.sealed_bytes].cpu().numpy(), want), f"thread {t}, launch {k}"
     ks.free()
+
+
+def test_w8_records_beyond_the_run_unit_cap_vs_fusion(ref):
+    """A W8 pair cuts its runs at W8_RUN_UNITS = 512 units (run_unit_cap), so in its kernels records from 1 MiB take
+    units of a multiple length (unit_mul > 1: partials combined with the unit power applied that many times) where the
+    4-bit kernel starts at 2 MiB. Records of 1 MiB - 40 B to 5 MiB + 7 B among 2,100 short ones, sealed and opened
+    (two tampered) against fusion."""
+    rng = np.random.default_rng(8107)
+    lens = rng.integers(0, 2000, 2100)
+    big = [(1 << 20) - 40, (1 << 20) + 1, 3 << 19, 3 << 20, (5 << 20) + 7]
+    for k, ln in enumerate(big):
+        lens[300 * k + 7] = ln
+    _check(ref, rng, lens, rng.integers(0, 40, len(lens)), 32, 1, tamper=2)
