@@ -452,3 +452,51 @@ def test_tls13_w8_tree_kernel_long_records_vs_fusion(ref):
     plain = d_plain.cpu().numpy()[:n * (ln + 1)].reshape(n, ln + 1)
     assert np.array_equal(plain[:, :ln].reshape(-1), data)
     ks.free()
+
+
+def test_tls13_w8_cut_runs_random_lengths_vs_fusion(ref):
+    """TLS 1.3 framing in the EXT 4 kernel's cut runs: 2,500 records of 0-16,383 payload bytes over three connections,
+    AES-256; every record equals header || fusion's seal of payload || type under the header as AAD, and every record
+    opens back with its content type."""
+    rng = np.random.default_rng(1314)
+    n, nkeys = 2500, 3
+    lens = rng.integers(0, 16384, n)
+    keys, ivs = rng.bytes(32 * nkeys), rng.bytes(12 * nkeys)
+    data = np.frombuffer(rng.bytes(int(lens.sum())), np.uint8)
+    recs = np.zeros(n, dtype=pa.RECORD_DTYPE)
+    recs["len"] = lens
+    recs["in_off"] = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    recs["out_off"] = np.concatenate([[0], np.cumsum(lens + 22)[:-1]])
+    recs["key_idx"] = np.arange(n) * nkeys // n
+    recs["seq"] = rng.integers(0, 2**40, n)
+    recs["flags"] = rng.choice([21, 22, 23], n)
+    wire_len = int((lens + 22).sum())
+    ks = pa.Keyset(keys, ivs, 32)
+    s = torch.cuda.current_stream().cuda_stream
+    d_recs, d_in, d_out = dev(recs), dev(data), empty(wire_len + 3, 0xEE)
+    pa.seal_tls_records(ks, d_recs.data_ptr(), n, d_in.data_ptr(), d_out.data_ptr(), s)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    for i in range(n):
+        k, o, ln, p = int(recs["key_idx"][i]), int(recs["out_off"][i]), int(lens[i]), int(recs["in_off"][i])
+        hdr = bytes([23, 3, 3, (ln + 17) >> 8, (ln + 17) & 0xFF])
+        want = hdr + ref.seal(keys[32 * k:32 * k + 32], ivs[12 * k:12 * k + 12], int(recs["seq"][i]), hdr,
+                              data[p:p + ln].tobytes() + bytes([int(recs["flags"][i])]))
+        assert out[o:o + len(want)].tobytes() == want, i
+    assert (out[wire_len:] == 0xEE).all()
+    orecs = np.zeros(n, dtype=pa.RECORD_DTYPE)
+    orecs["in_off"], orecs["len"], orecs["seq"], orecs["key_idx"] = recs["out_off"], lens + 1, recs["seq"], recs["key_idx"]
+    orecs["out_off"] = np.concatenate([[0], np.cumsum(lens + 1)[:-1]])
+    d_recs2, d_plain = dev(orecs), empty(int((lens + 1).sum()) + 1)
+    d_ok, d_res = empty(n, 0x77), empty(8 * n, 0x77)
+    pa.open_tls_records(ks, d_recs2.data_ptr(), n, d_out.data_ptr(), d_plain.data_ptr(), d_ok.data_ptr(), d_res.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert d_ok.cpu().numpy().all()
+    res = d_res.cpu().numpy().view(pa.TLS_RESULT_DTYPE)
+    assert (res["status"] == pa.TLS_OK).all() and (res["plain_len"] == lens).all()
+    assert (res["content_type"] == recs["flags"]).all()
+    plain = d_plain.cpu().numpy()
+    for i in range(0, n, 7):
+        o, ln, p = int(orecs["out_off"][i]), int(lens[i]), int(recs["in_off"][i])
+        assert np.array_equal(plain[o:o + ln], data[p:p + ln]), i
+    ks.free()
