@@ -133,7 +133,7 @@ def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool
     b = wl.descriptors(begin, end)
     keys, ivs = wl.keys()
     ks = pa.Keyset(keys, ivs, wl.key_size)
-    ks.set_schedule(schedule)
+    ks.set_schedule(schedule, allow_variable_time=True)
     dev = R.device
     d_seal = torch.from_numpy(b.seal.view(np.uint8).copy()).to(dev)
     d_open = torch.from_numpy(b.open.view(np.uint8).copy()).to(dev)
@@ -158,16 +158,19 @@ def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool
         open_()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(steps)]
+    clk = torch.zeros(8, dtype=torch.int64, device=dev)  # two (s_memtime, s_memrealtime, XCD) samples of XCD 0
     torch.cuda.synchronize(dev)
     R.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    pa.debug_clock_sample(clk.data_ptr(), sp)
     for e0, e1, e2 in ev:
         e0.record(stream)
         seal()
         e1.record(stream)
         open_()
         e2.record(stream)
+    pa.debug_clock_sample(clk.data_ptr() + 32, sp)
     torch.cuda.synchronize(dev)
     R.barrier()
     t1 = time.perf_counter()
@@ -176,7 +179,7 @@ def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool
     open_ms = float(np.mean([bb.elapsed_time(c) for _, bb, c in ev]))
 
     res = {"records": b.n, "payload_bytes": b.payload_bytes, "wall_s": wall, "seal_ms": seal_ms, "open_ms": open_ms,
-           "shard": [begin, end]}
+           "shard": [begin, end], "sclk_mhz": shader_clock_mhz(clk.cpu().numpy())}
     lens = b.seal["len"]
     res["seal_alg_bytes"] = algorithmic_bytes(lens, b.seal["aad_len"], True)
     res["open_alg_bytes"] = algorithmic_bytes(lens, b.seal["aad_len"], False)
@@ -190,11 +193,24 @@ def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool
         same = bool(torch.equal(d_back, d_pt))
         res["verified_roundtrip"] = R.sum(float(ok_all and same)) == R.world  # every rank's shard round-trips
         # records for the bit-exact fusion check, which runs in the cpu_baseline leg (rank 0)
-        res["sample"] = collect_sample(wl, b, keys, ivs, d_pt, d_aad, d_sealed) if R.rank == 0 else None
+        res["sample"] = collect_sample(wl, b, keys, ivs, d_pt, d_aad, d_sealed, d_back, d_ok) if R.rank == 0 else None
     del d_pt, d_sealed, d_back, d_ok, d_seal, d_open, d_aad
     ks.free()
     torch.cuda.empty_cache()
     return res
+
+
+def shader_clock_mhz(c) -> float | None:
+    """XCD 0's average shader clock over a timed leg from two clock probes (ptls_mi355x_debug_clock_sample: s_memtime
+    counts shader-clock cycles, s_memrealtime ticks at the device's wall-clock rate), or None when the two samples came
+    from different XCDs or the rate is unknown."""
+    import picotls_amd as pa
+
+    khz = pa.debug_wallclock_khz()
+    dt, drt = int(c[4]) - int(c[0]), int(c[5]) - int(c[1])
+    if khz <= 0 or drt <= 0 or dt <= 0 or int(c[2]) != int(c[6]):
+        return None
+    return round(dt / (drt / (khz * 1e3)) / 1e6, 1)
 
 
 def zero_slot_padding(arena, recs, dev):
@@ -212,13 +228,14 @@ def zero_slot_padding(arena, recs, dev):
         arena[sel] = 0
 
 
-def collect_sample(wl, b, keys, ivs, d_pt, d_aad, d_sealed, nsample: int = 64):
-    """Host copies of nsample records (inputs and the GPU's sealed output), repacked as a small batch, for the
-    bit-exact comparison with lib/fusion.c in the cpu_baseline leg."""
+def collect_sample(wl, b, keys, ivs, d_pt, d_aad, d_sealed, d_back, d_ok, nsample: int = 64):
+    """Host copies of nsample records (inputs, the GPU's sealed output, and what the timed open of the full-size batch
+    wrote for them: plaintext and ok byte), repacked as a small batch, for the bit-exact comparison with lib/fusion.c
+    in the cpu_baseline leg."""
     rng = np.random.default_rng(99)
     idx = np.unique(np.concatenate([[0, b.n - 1], rng.integers(0, b.n, nsample)]))
     sub = b.seal[idx].copy()
-    pt_parts, aad_parts, gpu_parts, new_in, new_aad = [], [], [], [], []
+    pt_parts, aad_parts, gpu_parts, back_parts, new_in, new_aad = [], [], [], [], [], []
     off = aoff = 0
     for r in sub:
         ln, al = int(r["len"]), int(r["aad_len"])
@@ -226,6 +243,7 @@ def collect_sample(wl, b, keys, ivs, d_pt, d_aad, d_sealed, nsample: int = 64):
         pt_parts.append(np.zeros(16, np.uint8))  # room for the tag (sealed in place)
         aad_parts.append(d_aad[int(r["aad_off"]):int(r["aad_off"]) + al].cpu().numpy())
         gpu_parts.append(d_sealed[int(r["out_off"]):int(r["out_off"]) + ln + 16].cpu().numpy())
+        back_parts.append(d_back[int(r["in_off"]):int(r["in_off"]) + ln].cpu().numpy())  # (the open writes at the seal's in_off)
         new_in.append(off)
         new_aad.append(aoff)
         off += ln + 16
@@ -236,16 +254,40 @@ def collect_sample(wl, b, keys, ivs, d_pt, d_aad, d_sealed, nsample: int = 64):
     recs["aad_off"] = new_aad
     return {"key_size": wl.key_size, "keys": keys, "ivs": ivs, "recs": recs,
             "pt": np.concatenate(pt_parts + [np.zeros(1, np.uint8)]),
-            "aad": np.concatenate(aad_parts + [np.zeros(1, np.uint8)]), "gpu": np.concatenate(gpu_parts)}
+            "aad": np.concatenate(aad_parts + [np.zeros(1, np.uint8)]), "gpu": np.concatenate(gpu_parts),
+            "gpu_back": np.concatenate(back_parts + [np.zeros(1, np.uint8)]), "gpu_ok": d_ok[torch_index(idx)].cpu().numpy()}
 
 
-def check_sample(ref, sample) -> bool:
-    """lib/fusion.c (ptls_aead_encrypt per record) on the sampled inputs, compared with the GPU's sealed records."""
+def torch_index(idx):
+    import torch
+
+    return torch.from_numpy(np.asarray(idx, np.int64))
+
+
+def check_sample(ref, sample) -> tuple[bool, bool]:
+    """lib/fusion.c (ptls_aead_encrypt per record) on the sampled inputs, compared with the GPU's sealed records; and
+    fusion opening the GPU's sealed records (ptls_aead_decrypt), compared with the plaintext and ok bytes the GPU's
+    full-size open wrote for them."""
     out = np.zeros(len(sample["pt"]), np.uint8)
     ref.run_batch(True, sample["keys"], sample["ivs"], sample["key_size"], sample["recs"], sample["pt"], sample["aad"], out,
                   nthreads=1)
     fus = np.concatenate([out[int(r["out_off"]):int(r["out_off"]) + int(r["len"]) + 16] for r in sample["recs"]])
-    return bool(np.array_equal(fus, sample["gpu"]))
+    seal_ok = bool(np.array_equal(fus, sample["gpu"]))
+    # fusion opens the GPU's ciphertext || tag (repacked at the same offsets) into its own plaintext arena
+    gpu_sealed = np.zeros(len(sample["pt"]), np.uint8)
+    back = np.zeros(len(sample["pt"]), np.uint8)
+    pos = 0
+    for r in sample["recs"]:
+        ln = int(r["len"])
+        gpu_sealed[int(r["in_off"]):int(r["in_off"]) + ln + 16] = sample["gpu"][pos:pos + ln + 16]
+        pos += ln + 16
+    ok = np.zeros(len(sample["recs"]), np.uint8)
+    ref.run_batch(False, sample["keys"], sample["ivs"], sample["key_size"], sample["recs"], gpu_sealed, sample["aad"], back,
+                  ok=ok, nthreads=1)
+    ref_back = np.concatenate([back[int(r["in_off"]):int(r["in_off"]) + int(r["len"])] for r in sample["recs"]] +
+                              [np.zeros(1, np.uint8)])
+    open_ok = bool(np.array_equal(ok, sample["gpu_ok"]) and np.array_equal(ref_back, sample["gpu_back"]) and ok.all())
+    return seal_ok, open_ok
 
 
 def run_ptlsbench(R, steps: int, warmup: int, rec_len: int = 16384):
@@ -319,6 +361,20 @@ def _cpu_share():
     return cpus[:max(1, min(share, len(cpus)))]
 
 
+def cpu_topology(cpus) -> dict:
+    """Physical cores behind the logical CPUs used (sysfs core_id / physical_package_id): how many distinct cores, and
+    how many of the CPUs are SMT siblings of another CPU in the set."""
+    cores = {}
+    for c in cpus:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            key = (open(base + "physical_package_id").read().strip(), open(base + "core_id").read().strip())
+        except OSError:
+            return {"physical_cores": None, "smt_siblings_in_set": None, "logical_cpus": len(cpus)}
+        cores.setdefault(key, []).append(c)
+    return {"physical_cores": len(cores), "smt_siblings_in_set": len(cpus) - len(cores), "logical_cpus": len(cpus)}
+
+
 def _fusion_leg(ref, wl, cpus, seconds: float, nontemporal: bool = False, sample_bytes: int = 256 << 20,
                 max_reps: int = 200):
     """fusion sealing then opening a bounded sample of the workload with len(cpus) pinned threads (contiguous shards,
@@ -370,7 +426,9 @@ def cpu_baseline(wl, seconds: float, samples: dict, ptlsbench_gpu):
         return {"value": None, "unit": "GiB/s", "cores": 0, "kind": "reference", "sample": f"unavailable: {e}"}, {}
     from picotls_amd.workloads import WORKLOADS
 
-    checks = {name: check_sample(ref, smp) for name, smp in samples.items() if smp is not None}
+    both = {name: check_sample(ref, smp) for name, smp in samples.items() if smp is not None}
+    checks = {name: v[0] for name, v in both.items()}
+    checks.update({name + ":open": v[1] for name, v in both.items()})
     cpus = _cpu_share()
     legs = {}
     primary = _fusion_leg(ref, wl, cpus, seconds)
@@ -407,10 +465,14 @@ def cpu_baseline(wl, seconds: float, samples: dict, ptlsbench_gpu):
     except OSError:
         pass
     one = legs[wl.name]["fusion_1_thread"]["value"]
+    topo = cpu_topology(cpus)
     out = {"value": primary["value"], "unit": "GiB/s", "cores": len(cpus), "kind": "reference",
+           "physical_cores": topo["physical_cores"], "smt_siblings_in_set": topo["smt_siblings_in_set"],
+           "cpus": cpus,
            "sample": primary["sample"] + f", {len(cpus)} pinned threads, CLOCK_MONOTONIC, median of {primary['reps']} reps "
                                          f"(p25 {primary['p25']}, p75 {primary['p75']}, min {primary['min']}, max "
-                                         f"{primary['max']}); CPU: {model}",
+                                         f"{primary['max']}); CPU: {model}; {topo['physical_cores']} physical cores "
+                                         f"({topo['smt_siblings_in_set']} of the threads on SMT siblings)",
            "p25": primary["p25"], "p75": primary["p75"], "iqr_rel": primary["iqr_rel"],
            "seal_GiBps": primary["seal_GiBps"], "open_GiBps": primary["open_GiBps"],
            "single_thread_GiBps": one,
@@ -432,7 +494,7 @@ def run_e2e(R, wl, nchunks: int = 16, reps: int = 3, schedule: str = "auto"):
     b = wl.descriptors(0, wl.nrecs)
     keys, ivs = wl.keys()
     ks = pa.Keyset(keys, ivs, wl.key_size)
-    ks.set_schedule(schedule)
+    ks.set_schedule(schedule, allow_variable_time=True)
     dev = R.device
     from picotls_amd.workloads import payload_np
 
@@ -553,6 +615,18 @@ def run_e2e(R, wl, nchunks: int = 16, reps: int = 3, schedule: str = "auto"):
     return out
 
 
+def per_rank(R, res) -> dict:
+    """Every rank's seal / open launch time and wall time of the timed steps (rank order), so that a straggler of a
+    multi-GPU run shows; value uses the max of wall_s."""
+    rows = R.gather([res["seal_ms"], res["open_ms"], res["wall_s"], res.get("sclk_mhz") or 0.0])
+    wall = [r[2] for r in rows]
+    slow = int(np.argmax(wall))
+    return {"seal_ms": [round(r[0], 4) for r in rows], "open_ms": [round(r[1], 4) for r in rows],
+            "wall_s": [round(r[2], 5) for r in rows], "sclk_mhz": [round(r[3], 1) if r[3] else None for r in rows],
+            "max_wall_s": round(max(wall), 5), "min_wall_s": round(min(wall), 5), "slowest_rank": slow,
+            "max_over_min": round(max(wall) / min(wall), 4) if min(wall) > 0 else None}
+
+
 def lds_model(res, key_size: int, nrecs: int):
     """The bound the seal kernel actually meets: LDS table lookups. Per GHASH stream block an AES-128
     block costs 133 ds_read_b32 (AES-256: 197) and its GHASH fold 16 ds_read_b128 (the W8 kernels' Horner step on the
@@ -639,8 +713,12 @@ def main():
                      "open_alg_bytes_per_launch": res["open_alg_bytes"],
                      "open_traffic": traffic_from_profiles(wl.name, res["records"], "open_hbm_bytes_per_launch")},
         "lds_model": lds_model(res, wl.key_size, res["records"]),
-        "verified": {"roundtrip": res.get("verified_roundtrip"), "fusion_spot_check": None},
+        "verified": {"roundtrip": res.get("verified_roundtrip"), "fusion_spot_check": None, "fusion_open_spot_check": None},
+        # XCD 0's average shader clock over the timed steps (rank 0), so that box-to-box spread can be attributed
+        "sclk_mhz": res.get("sclk_mhz"),
     }
+    if R.world > 1:
+        out["per_rank"] = per_rank(R, res)
     samples = {wl.name: res.get("sample")}
     extra = {}
     ptlsbench_gpu = None
@@ -676,8 +754,11 @@ def main():
                        "open_GiBps": round(r2["payload_bytes"] / (r2["open_ms"] / 1e3) / 2**30, 3),
                        "seal_achieved_GBps": round(r2["seal_alg_bytes"] / (r2["seal_ms"] / 1e3) / 1e9, 2),
                        "seal_hbm_frac": round(r2["seal_alg_bytes"] / (r2["seal_ms"] / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
-                       "seal_avg_launch_ms": round(r2["seal_ms"], 4),
-                       "verified": {"roundtrip": r2.get("verified_roundtrip"), "fusion_spot_check": None}}
+                       "seal_avg_launch_ms": round(r2["seal_ms"], 4), "sclk_mhz": r2.get("sclk_mhz"),
+                       "verified": {"roundtrip": r2.get("verified_roundtrip"), "fusion_spot_check": None,
+                                    "fusion_open_spot_check": None}}
+        if R.world > 1:
+            extra[name]["per_rank"] = per_rank(R, r2)
     if extra:
         out["extra"] = extra
     if args.e2e or (args.e2e is None and R.world == 1 and not args.records):  # (N = 1 at full size: 12 GiB pinned)
@@ -691,8 +772,11 @@ def main():
                                    "vs_single_thread_x_cores": round(out["value"] / cb["single_thread_x_cores_GiBps"], 2)
                                    if cb.get("single_thread_x_cores_GiBps") else None}
         out["verified"]["fusion_spot_check"] = checks.get(wl.name)
+        out["verified"]["fusion_open_spot_check"] = checks.get(wl.name + ":open")
         for name, e in extra.items():
             e["verified"]["fusion_spot_check"] = checks.get(name)
+            if name != "ptlsbench":
+                e["verified"]["fusion_open_spot_check"] = checks.get(name + ":open")
     elif R.rank == 0:
         out["cpu_baseline"] = None
     if R.rank == 0:

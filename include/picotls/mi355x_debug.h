@@ -1,0 +1,47 @@
+/*
+ * picotls/mi355x_debug.h -- test and measurement hooks of libptls_mi355x.so. Not part of the picotls drop-in boundary
+ * (include/picotls/mi355x.h is); no reference counterpart. Used by tests/ and bench.py only.
+ */
+#ifndef picotls_mi355x_debug_h
+#define picotls_mi355x_debug_h
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/**
+ * Counters since the last reset, into out[16]:
+ *   out[0..4]  launches of the chunked batch kernel per instantiation: 0 plain (4-bit GHASH tables), 1 spread (small
+ *              batch with long records), 2 seal with header-protection masks, 3 W8 butterfly end (long whole records
+ *              of a W8 pair), 4 W8 serial end (every other run of a W8 pair)
+ *   out[5]     launches of the lockstep kernel, out[6] of the span kernels (a lone long record), out[7] 0
+ *   out[8..15] runs processed on the device by each chunked instantiation (same order; a run skipped because the
+ *              pair's other kernel takes it is not counted)
+ * Waits for the whole device (reading the device counters). reset != 0 zeroes them after reading. Returns 0 or -1.
+ */
+int ptls_mi355x_debug_counters(uint64_t *out, int reset);
+
+/**
+ * Leaves a HIP error (hipErrorInvalidValue from hipHostGetDevicePointer on pageable memory) as the calling thread's last
+ * error without clearing it, the state a handled failure used to leave behind. Returns the error code
+ * left (0 if the call unexpectedly succeeded). The engine's calls on this thread must not be affected by it.
+ */
+int ptls_mi355x_debug_inject_error(void);
+
+/**
+ * Launches one wave on `stream` (a hipStream_t; workgroup 0 runs on XCD 0) that writes three 64-bit words to the
+ * device-accessible `out`: the shader-clock counter (s_memtime), the real-time counter (s_memrealtime, rate
+ * ptls_mi355x_debug_wallclock_khz) and the XCD it ran on. Two samples around a timed region give XCD 0's average
+ * shader clock over it. Returns 0 or -1.
+ */
+int ptls_mi355x_debug_clock_sample(void *out, void *stream);
+/* the real-time counter's rate in kHz (hipDeviceAttributeWallClockRate of the current device), 0 if unknown */
+int ptls_mi355x_debug_wallclock_khz(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

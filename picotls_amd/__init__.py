@@ -65,6 +65,13 @@ ABI_FUNCTIONS = (
     "ptls_mi355x_release_staging",
     "ptls_mi355x_last_error",
 )
+# include/picotls/mi355x_debug.h: test and measurement hooks (not the picotls boundary)
+DEBUG_FUNCTIONS = (
+    "ptls_mi355x_debug_counters",
+    "ptls_mi355x_debug_inject_error",
+    "ptls_mi355x_debug_clock_sample",
+    "ptls_mi355x_debug_wallclock_khz",
+)
 
 SIZE_MAX = ctypes.c_size_t(-1).value
 _lib = None
@@ -127,6 +134,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.ptls_mi355x_quiclb_batch.argtypes = [vp, vp, sz, vp, vp, vp]
     lib.ptls_mi355x_quiclb_transform.argtypes = [vp, sz, vp, vp, sz, ci]
     lib.ptls_mi355x_last_error.restype = ctypes.c_char_p
+    lib.ptls_mi355x_debug_counters.argtypes = [vp, ci]
+    lib.ptls_mi355x_debug_inject_error.restype = ci
+    lib.ptls_mi355x_debug_clock_sample.argtypes = [vp, vp]
+    lib.ptls_mi355x_debug_wallclock_khz.restype = ci
     _lib = lib
     return lib
 
@@ -213,18 +224,24 @@ class Keyset:
 
     SCHEDULES = {"auto": 0, "lockstep": 1, "chunked": 2}
 
-    def set_schedule(self, schedule: str) -> None:
+    def set_schedule(self, schedule: str, allow_variable_time: bool = False) -> None:
         """Batch schedule (ptls_mi355x_keyset_set_schedule): "auto", "lockstep" or "chunked".
 
-        The lockstep schedule (the round-1 kernel, kept for comparison) is not offered to constant-time keysets, which
-        every keyset is by default since round 4: asking for it here also turns the keyset's constant-time setting off,
-        so that the lockstep kernel is the one that runs."""
+        The lockstep schedule (the round-1 kernel, kept for comparison) has data-dependent LDS bank conflicts, so the
+        engine never runs it for a constant-time keyset (every keyset is one by default since round 4): the C call
+        records the schedule and such a keyset keeps the chunked kernels. Here asking for "lockstep" on a constant-time
+        keyset raises, unless allow_variable_time=True, which (after the schedule is set) turns the keyset's
+        constant-time setting off so that the lockstep kernel is the one that runs."""
         if schedule not in self.SCHEDULES:
             raise ValueError(f"unknown schedule {schedule!r}")
-        if schedule == "lockstep":
-            self.set_constant_time(False)
+        lockstep_ct = schedule == "lockstep" and self.constant_time
+        if lockstep_ct and not allow_variable_time:
+            raise EngineError("set_schedule('lockstep') on a constant-time keyset: the lockstep kernel is not constant-time; "
+                              "pass allow_variable_time=True to turn the keyset's constant-time setting off")
         if load_library().ptls_mi355x_keyset_set_schedule(self.handle, self.SCHEDULES[schedule]) != 0:
             raise _err("set_schedule")
+        if lockstep_ct:
+            self.set_constant_time(False)
 
 
 def seal_batch(ks: Keyset, recs_ptr: int, nrecs: int, in_ptr: int, aad_ptr: int, out_ptr: int, stream: int = 0) -> None:
@@ -434,6 +451,36 @@ def staging_bytes() -> int:
 def release_staging() -> None:
     """Frees the idle staging buffers (ptls_mi355x_release_staging)."""
     load_library().ptls_mi355x_release_staging()
+
+
+# ------------------------------------------------------------------------------------------------ debug hooks
+
+
+COUNTER_NAMES = ("chunked", "spread", "seal_hp", "w8_tree", "w8_serial", "lockstep", "span", "_")
+
+
+def debug_counters(reset: bool = False) -> dict:
+    """ptls_mi355x_debug_counters: {"launches": {kind: n}, "runs": {kind: n}} (chunked kinds: EXT 0..4). Waits for the
+    device."""
+    out = (ctypes.c_uint64 * 16)()
+    if load_library().ptls_mi355x_debug_counters(ctypes.cast(out, ctypes.c_void_p), 1 if reset else 0) != 0:
+        raise _err("ptls_mi355x_debug_counters")
+    return {"launches": dict(zip(COUNTER_NAMES, out[:8])), "runs": dict(zip(COUNTER_NAMES[:5], out[8:13]))}
+
+
+def debug_inject_error() -> int:
+    """Leaves a HIP error as this thread's last error (ptls_mi355x_debug_inject_error); returns its code."""
+    return int(load_library().ptls_mi355x_debug_inject_error())
+
+
+def debug_clock_sample(dev_ptr: int, stream: int = 0) -> None:
+    """Writes (s_memtime, s_memrealtime, XCC id) of XCD 0 to 3 x u64 at dev_ptr, in stream order."""
+    if load_library().ptls_mi355x_debug_clock_sample(dev_ptr, stream or None) != 0:
+        raise _err("ptls_mi355x_debug_clock_sample")
+
+
+def debug_wallclock_khz() -> int:
+    return int(load_library().ptls_mi355x_debug_wallclock_khz())
 
 
 def aead_new_direct(algo: AeadAlgorithm, is_enc: bool, key: bytes, iv: bytes) -> AeadContext:

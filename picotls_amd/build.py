@@ -24,7 +24,7 @@ PICOTLS_INCLUDE = os.environ.get("PICOTLS_INCLUDE", "/root/reference/include")
 ENGINE_FLAGS = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
 ENGINE_SRCS = [os.path.join(PKG, "csrc", "aesgcm_engine.hip")]
 PICOTLS_SRCS = [os.path.join(PKG, "csrc", "ptls_mi355x.c")]
-HEADERS = [os.path.join(ROOT, "include", "picotls", "mi355x.h"), os.path.join(ROOT, "include", "picotls", "mi355x_picotls.h")]
+HEADERS = [os.path.join(ROOT, "include", "picotls", h) for h in ("mi355x.h", "mi355x_picotls.h", "mi355x_debug.h")]
 ENGINE_PARTS = sorted(os.path.join(PKG, "csrc", "engine", f) for f in os.listdir(os.path.join(PKG, "csrc", "engine"))
                       if f.endswith(".h"))  # included by aesgcm_engine.hip (one translation unit)
 

@@ -42,6 +42,7 @@
 #include <sched.h>
 
 #include "picotls/mi355x.h"
+#include "picotls/mi355x_debug.h"
 
 // Device code, in dependency order (one translation unit: the kernels are templates instantiated by the host side)
 #include "engine/common.h"
@@ -68,7 +69,18 @@ static int fail(const char *fmt, const char *detail)
 // Kernel launches are checked with hipGetLastError, which also returns the error of any earlier call of this thread
 // whose failure was handled (a failed hipHostGetDevicePointer, for one: tools/mb/lasterr.hip showed that error reported
 // after a good launch). LAUNCH_CLEAR() before a launch makes the check after it about that launch only.
+// (-DLAUNCH_CLEAR_NOOP=1: a tools/ variant without it, which the regression test of tests/c/test_vtable.c `lasterr`
+// must fail on; never the shipped build)
+#if LAUNCH_CLEAR_NOOP
+#define LAUNCH_CLEAR() ((void)0)
+#else
 #define LAUNCH_CLEAR() ((void)hipGetLastError())
+#endif
+
+// Test and measurement counters (include/picotls/mi355x_debug.h): chunked-kernel launches per EXT instantiation (0..4),
+// lockstep launches (5), span launches (6) -- host side, counted where the launch is made
+static std::atomic<uint64_t> g_launches[8];
+#define COUNT_LAUNCH(i) g_launches[(i)].fetch_add(1, std::memory_order_relaxed)
 
 #define HIP_TRY(expr)                                                                                                         \
     do {                                                                                                                      \
@@ -385,6 +397,23 @@ static void stager_destroy(Stager *s)
     delete s;
 }
 
+// frees the idle staging buffers of one device (hipHostFree waits for that device)
+static void release_idle_stagers(DeviceState *ds)
+{
+    std::vector<Stager *> idle;
+    {
+        std::lock_guard<std::mutex> lk(ds->mu);
+        for (int c = 0; c < STAGE_CLASSES; ++c) {
+            for (Stager *s = ds->stagers[c]; s != nullptr; s = s->next)
+                idle.push_back(s);
+            ds->stagers[c] = nullptr;
+        }
+        ds->stage_idle = 0;
+    }
+    for (Stager *s : idle)
+        stager_destroy(s);
+}
+
 static Stager *stager_get(DeviceState *ds, size_t bytes)
 {
     if (bytes > ds->stage_limit) {
@@ -442,9 +471,10 @@ static Stager *stager_get(DeviceState *ds, size_t bytes)
     // kernel on this buffer can read lines of the previous call's input.
     const unsigned hflags = ds->stage_coherent ? hipHostMallocCoherent : hipHostMallocDefault;
     if (hipHostMalloc((void **)&s->h, s->cap, hflags) != hipSuccess) {
-        // (round 4) the pinned memory of idle buffers of other sizes is what this one may need: free them, try again
+        // (round 4) the pinned memory of idle buffers of other sizes is what this one may need: free this device's
+        // (not every device's -- hipHostFree synchronises the device it frees for), try again
         (void)hipGetLastError();
-        ptls_mi355x_release_staging();
+        release_idle_stagers(ds);
         if (hipHostMalloc((void **)&s->h, s->cap, hflags) != hipSuccess) {
             (void)hipGetLastError();
             delete s;
@@ -818,6 +848,57 @@ int ptls_mi355x_debug_profile(unsigned long long *out, int reset)
 }
 #endif
 
+// ---- test and measurement hooks (include/picotls/mi355x_debug.h)
+
+int ptls_mi355x_debug_counters(uint64_t *out, int reset)
+{
+    if (out == NULL)
+        return fail("%s", "debug_counters: invalid arguments");
+    for (int i = 0; i < 8; ++i)
+        out[i] = reset ? g_launches[i].exchange(0) : g_launches[i].load();
+    HIP_TRY(hipDeviceSynchronize());  // (test-only: the device counters of every launch made so far)
+    static unsigned long long rows[EXT_RUN_ROWS][8];
+    HIP_TRY(hipMemcpyFromSymbol(rows, HIP_SYMBOL(g_ext_runs), sizeof(rows)));
+    for (int i = 0; i < 8; ++i) {
+        out[8 + i] = 0;
+        for (int r = 0; r < EXT_RUN_ROWS; ++r)
+            out[8 + i] += rows[r][i];
+    }
+    if (reset) {
+        memset(rows, 0, sizeof(rows));
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_ext_runs), rows, sizeof(rows)));
+    }
+    return 0;
+}
+
+int ptls_mi355x_debug_inject_error(void)
+{
+    // a handled-looking failure of the kind the per-record path meets (hipHostGetDevicePointer on memory HIP did not
+    // allocate), deliberately NOT cleared: the thread's last error is left set, as a handled failure used to leave it
+    static uint8_t pageable[64];
+    void *p = nullptr;
+    const hipError_t e = hipHostGetDevicePointer(&p, pageable, 0);
+    return (int)(e != hipSuccess ? hipPeekAtLastError() : hipSuccess);
+}
+
+int ptls_mi355x_debug_clock_sample(void *out, void *stream)
+{
+    if (out == NULL)
+        return fail("%s", "debug_clock_sample: invalid arguments");
+    LAUNCH_CLEAR();
+    clock_probe_kernel<<<1, 64, 0, (hipStream_t)stream>>>((unsigned long long *)out);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int ptls_mi355x_debug_wallclock_khz(void)
+{
+    int dev = 0, khz = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess)
+        return 0;
+    return khz;
+}
+
 int ptls_mi355x_keyset_set_schedule(ptls_mi355x_keyset_t *ks, int schedule)
 {
     if (ks == NULL || schedule < PTLS_MI355X_SCHEDULE_AUTO || schedule > PTLS_MI355X_SCHEDULE_CHUNKED)
@@ -859,19 +940,8 @@ void ptls_mi355x_release_staging(void)
         DeviceState *ds = g_devs[d].load(std::memory_order_acquire);
         if (ds == nullptr)
             continue;
-        std::vector<Stager *> idle;
-        {
-            std::lock_guard<std::mutex> lk(ds->mu);
-            for (int c = 0; c < STAGE_CLASSES; ++c) {
-                for (Stager *s = ds->stagers[c]; s != nullptr; s = s->next)
-                    idle.push_back(s);
-                ds->stagers[c] = nullptr;
-            }
-            ds->stage_idle = 0;
-        }
         DeviceScope scope(d);
-        for (Stager *s : idle)
-            stager_destroy(s);
+        release_idle_stagers(ds);
     }
 }
 
@@ -914,6 +984,7 @@ static bool use_chunked(int schedule) { return schedule != PTLS_MI355X_SCHEDULE_
 template <int NR, bool OPEN, int FRAME, int EXT = 0>
 static void launch_chunked_x(bool ct, unsigned grid, hipStream_t s, const BatchArgs &a)
 {
+    COUNT_LAUNCH(EXT);
 #if SEG_COOP
     (void)ct;
     gcm_chunked_kernel<NR, OPEN, FRAME, true, EXT><<<grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
@@ -1063,7 +1134,7 @@ static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int sche
         CHUNKED_BY_KEY(2);
     else if (ct || use_chunked(schedule))
         CHUNKED_BY_KEY(0);
-    else if (nr == 10) {
+    else if ((COUNT_LAUNCH(5), nr == 10)) {
         if (open)
             gcm_batch_kernel<10, true><<<(unsigned)grid, ENGINE_WG, LDS_ALLOC, s>>>(a);
         else
@@ -1086,6 +1157,7 @@ static int launch_gcm(const KeyEntry *keys, u32 nkeys, int nr, int ncu, int sche
 template <int NR, bool OPEN>
 static void launch_span_kernel(bool ct, u32 nspans, hipStream_t s, const BatchArgs &a, u32 span, u32 units, void *part)
 {
+    COUNT_LAUNCH(6);
 #if SEG_COOP  // (one instantiation for both settings, as launch_chunked_x)
     (void)ct;
     gcm_span_kernel<NR, OPEN, true><<<nspans, ENGINE_WG, SPAN_LDS, s>>>(a, span, units, (u32x4 *)part);
@@ -1306,9 +1378,11 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
         ret = launch_gcm(ks->d_keys, (u32)ks->nkeys, ks->nr, ks->ds->ncu, ks->schedule, ks->ct, open, recs, nrecs, in, aad, out, ok,
                          s, frame, CHUNK_LOG2, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, hpl, spread, 0, w8flags);
     }
-    if (ret != 0)
-        return -1;
-    return lk.owns_lock() ? note_use_locked(ks, s) : note_use(ks, s);
+    // (a failed launch may have queued part of its work, e.g. EXT 4 of a W8 pair before its EXT 3 failed: the use is
+    // recorded either way, so that a later takeover of this stream's flag buffer or a scratch regrow waits for it;
+    // ADVICE round 4)
+    const int noted = lk.owns_lock() ? note_use_locked(ks, s) : note_use(ks, s);
+    return ret != 0 ? -1 : noted;
 }
 
 static unsigned aux_grid(size_t n, int ncu)

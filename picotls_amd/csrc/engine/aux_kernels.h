@@ -368,4 +368,20 @@ __global__ __launch_bounds__(256) void tls12_check_kernel(const ptls_mi355x_reco
     }
 }
 
+// Measurement (ptls_mi355x_debug_clock_sample): one wave of one workgroup -- workgroup 0 of a launch is dispatched to
+// XCD 0 -- reads the shader-clock counter (s_memtime) and the constant-rate real-time counter (s_memrealtime) and the
+// XCD it ran on. Two samples around a timed region give that XCD's average shader clock over it.
+__global__ __launch_bounds__(64) void clock_probe_kernel(unsigned long long *out)
+{
+    if (threadIdx.x != 0)
+        return;
+    unsigned long long t, rt;
+    u32 xcc;
+    asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_getreg_b32 %2, hwreg(HW_REG_XCC_ID)\n\ts_waitcnt lgkmcnt(0)"
+                 : "=s"(t), "=s"(rt), "=s"(xcc)::"memory");
+    out[0] = t;
+    out[1] = rt;
+    out[2] = xcc;
+}
+
 #endif  // PTLS_MI355X_ENGINE_AUX_KERNELS_H

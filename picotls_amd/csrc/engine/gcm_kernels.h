@@ -165,6 +165,15 @@ __device__ __forceinline__ unsigned long long stamp()
 #define PROF_ADD(i, x)
 #endif
 
+// Runs processed per chunked instantiation (EXT 0..4), one row per workgroup (blockIdx.x mod EXT_RUN_ROWS), summed on the
+// host by ptls_mi355x_debug_counters: the evidence that a batch ran in the kernel a test means to exercise (one
+// uncontended atomic per run and workgroup)
+#ifndef COMBINE_SCATTER
+#define COMBINE_SCATTER 1  // round 5: a record's unit combine as a scattered chain of group products (ghash.h)
+#endif
+#define EXT_RUN_ROWS 256
+__device__ unsigned long long g_ext_runs[EXT_RUN_ROWS][8];
+
 #ifndef RUN_FILL_UNITS
 #define RUN_FILL_UNITS (ENGINE_WG / ENGINE_G / 2)  // a cut run takes the longest units that still give this many
 #endif
@@ -906,6 +915,8 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             rb ^= 1;
             continue;
         }
+        if (threadIdx.x == 0)  // (this instantiation processes the run: ptls_mi355x_debug_counters)
+            atomicAdd(&g_ext_runs[blockIdx.x % EXT_RUN_ROWS][EXT], 1ull);
         typedef __attribute__((address_space(3))) const KeyEntry lds_key_t;
         lds_key_t *key = (lds_key_t *)(rs + RUN_KEY_OFF);  // staged by the scanner
         // the EXT 3 kernel's runs (all W8: the others were skipped above) take the 8-bit Horner table (ghash.h)
@@ -1063,6 +1074,18 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                     u32x4 g;
                     if (CT && CT_COMB_TREE_ON && mul == 1) {
                         g = ct_combine_tree(lds, s_part + first, unc, j);
+                    } else if constexpr (SEG_COOP && COMBINE_SCATTER) {
+                        // (round 5) a scattered chain (ghash.h): each lane carries its dword of the running sum
+                        const GroupWs k = group_ws(tsel_chunk, lane);
+                        const u32 q = j >> 1;
+                        const u32x4 z = {0, 0, 0, 0};
+                        u32 gs = ((const lds_u32 *)(s_part + first))[q];
+                        for (u32 i = 1; i < unc; ++i) {
+                            for (u32 t = 0; t < mul; ++t)  // (mul > 1: huge records only)
+                                gs = gmul_group_ws(lds, gs, k, z, lane);
+                            gs ^= ((const lds_u32 *)(s_part + first + i))[q];
+                        }
+                        g = group_gather(gs, lane);
                     } else {
                         g = s_part[first];
                         for (u32 i = 1; i < unc; ++i) {

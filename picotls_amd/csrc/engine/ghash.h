@@ -252,17 +252,119 @@ __device__ __forceinline__ u32x4 gmul_group_w_add(const lds_u8 *, u32x4 a, u32 t
     return r;
 }
 
+// ------------------------------------------------------------------------------------------------ GHASH (scattered chains)
+//
+// A chain of group products (a Horner over the group's ranks, a record's unit combine) needs, for each link, lane y's
+// halfword y of the previous product, not the whole product in every lane. gmul_group_w all-reduces each product over
+// the 8 lanes (dpp_xor8 of 4 dwords: 12 DPP operations) and each lane then picks its dword (3 selects). Here a link
+// reduce-scatters instead (group_scatter: 10 operations; lane y keeps dword y >> 1 of the sum, complete) and extracts
+// its nibbles with a bit-field extract and an OR into the opaque per-lane window bases (2 operations a lookup instead
+// of 4): ~30 VALU operations a link instead of ~46 (the EXT 4 kernel's segment end: 413 VALU instructions in the code
+// object before, round 5). The lookups and tables are gmul_group_w's: conflict-free by construction.
+struct GroupWs {
+    u32 Wi[4];  // the lane's window base for lookup i (wtab_lane_base ^ i << 4)
+    u32 sh[4];  // the bit offset of the lane's nibble for lookup i in its dword: 16 (y & 1) + (4 f ^ 4 (i ^ 1))
+};
+__device__ __forceinline__ GroupWs group_ws(u32 tsel, u32 lane)
+{
+    GroupWs k;
+    const u32 W = wtab_lane_base(tsel, lane), h16 = 16u * (lane & 1), f4 = 4u * ((lane >> 2) & 3);
+#pragma unroll
+    for (u32 i = 0; i < 4; ++i) {
+        k.Wi[i] = W ^ (i << 4);
+        k.sh[i] = h16 + (f4 ^ (4u * (i ^ 1u)));
+        asm volatile("" : "+v"(k.Wi[i]), "+v"(k.sh[i]));  // (computed once, not re-derived at every lookup)
+    }
+    return k;
+}
+
+// Reduce-scatter of t over the 8 lanes of a group: returns dword (y >> 1) of the XOR of the group's t, complete (both
+// halves), in lane y = lane & 7. Three butterfly stages: lane 7 - y (row_half_mirror) exchanges the dword pair the
+// other needs, lane y ^ 2 (quad_perm [2,3,0,1]) the dword, lane y ^ 1 (quad_perm [1,0,3,2]) the sum of the last two.
+__device__ __forceinline__ u32 group_scatter(u32x4 t, u32 lane)
+{
+    const bool b = (lane & 4) != 0, c = (lane & 2) != 0;
+    const u32 k0 = b ? t[2] : t[0], k1 = b ? t[3] : t[1], s0 = b ? t[0] : t[2], s1 = b ? t[1] : t[3];
+    const u32 m0 = k0 ^ (u32)__builtin_amdgcn_update_dpp(0, (int)s0, 0x141, 0xF, 0xF, false);
+    const u32 m1 = k1 ^ (u32)__builtin_amdgcn_update_dpp(0, (int)s1, 0x141, 0xF, 0xF, false);
+    const u32 kk = c ? m1 : m0, ss = c ? m0 : m1;
+    const u32 m = kk ^ (u32)__builtin_amdgcn_update_dpp(0, (int)ss, 0x4E, 0xF, 0xF, false);
+    return m ^ (u32)__builtin_amdgcn_update_dpp(0, (int)m, 0xB1, 0xF, 0xF, false);
+}
+
+// The whole value in every lane of the group from its scattered form (lanes 2q, 2q + 1 hold dword q): each quad's
+// lanes 0 and 2 broadcast (quad_perm [0,0,0,0], [2,2,2,2]), the other quad's copies come over row_half_mirror
+__device__ __forceinline__ u32x4 group_gather(u32 g, u32 lane)
+{
+    const u32 a = (u32)__builtin_amdgcn_update_dpp(0, (int)g, 0x00, 0xF, 0xF, false);
+    const u32 b = (u32)__builtin_amdgcn_update_dpp(0, (int)g, 0xAA, 0xF, 0xF, false);
+    const u32 am = (u32)__builtin_amdgcn_update_dpp(0, (int)a, 0x141, 0xF, 0xF, false);
+    const u32 bm = (u32)__builtin_amdgcn_update_dpp(0, (int)b, 0x141, 0xF, 0xF, false);
+    const bool hi = (lane & 4) != 0;
+    return u32x4{hi ? am : a, hi ? bm : b, hi ? a : am, hi ? b : bm};
+}
+
+// the lane's dword (y >> 1) of a value every lane of the group holds
+__device__ __forceinline__ u32 group_dword(u32x4 v, u32 lane)
+{
+    const u32 q = (lane & 7) >> 1;
+    return q == 0 ? v[0] : q == 1 ? v[1] : q == 2 ? v[2] : v[3];
+}
+
+// the 4 table entries of the lane's windows of a (ga: the lane's dword of a), folded with x (this lane's share of a
+// term added to the product: zero in all lanes but one)
+__device__ __forceinline__ u32x4 group_ws_terms(u32 ga, const GroupWs &k, u32x4 x)
+{
+    u32x4 e[4];
+#pragma unroll
+    for (u32 i = 0; i < 4; ++i)
+        e[i] = lds_load128((((ga >> k.sh[i]) & 15u) << 8) | k.Wi[i]);
+    u32x4 t;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        t[c] = xor3(xor3(e[0][c], e[1][c], e[2][c]), e[3][c], x[c]);
+    return t;
+}
+
+// a link of a scattered chain: the lane's dword of a * T + x
+__device__ __forceinline__ u32 gmul_group_ws(const lds_u8 *, u32 ga, const GroupWs &k, u32x4 x, u32 lane)
+{
+    return group_scatter(group_ws_terms(ga, k, x), lane);
+}
+
+// the last link: a * T whole in every lane (all-reduce)
+__device__ __forceinline__ u32x4 gmul_group_ws_full(const lds_u8 *, u32 ga, const GroupWs &k)
+{
+    u32x4 t = group_ws_terms(ga, k, u32x4{0, 0, 0, 0});
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        t[c] = dpp_xor8(t[c]);
+    return t;
+}
+
+#ifndef W8_END_SCATTER
+#define W8_END_SCATTER 1  // round 5: the segment end's chain as a scattered chain (gmul_group_ws)
+#endif
+
 // The W8 segment end (gcm_segment, W8 runs): lane j of a group holds a_j, its partial with its last stream position
 // unmultiplied, owing H^(8 - rank_j). Returns sum_j a_j H^(8 - rank_j) in every lane of the group, as the Horner
 // ((v_0 H + v_1) H + ... + v_7) H over the ranks (v_r: the value of the lane of rank r) by eight group multiplies with
 // the window-major H table at W8_TAB_H; the lane of rank r folds its value into its share of the r-th product, so the
 // values never move between lanes. The W8 map has room for that one table only (the 8-bit H^8 table takes slots
 // 0..7), where coop_last_powers needs seven: the lookups are the same 32 per lane, conflict-free, the price is a
-// chain of eight dependent products.
+// chain of eight dependent products, run scattered (above) since round 5.
 __device__ __forceinline__ u32x4 w8_lane_end(const lds_u8 *lds, u32x4 v, u32 lane, u32 rank)
 {
     static_assert(ENGINE_G == 8, "a chain over 8 lanes");
     const u32x4 z = {0, 0, 0, 0};
+#if W8_END_SCATTER
+    const GroupWs k = group_ws(W8_TAB_H, lane);
+    u32 g = group_scatter(rank == 0 ? v : z, lane);
+#pragma unroll
+    for (u32 r = 1; r < 8; ++r)
+        g = gmul_group_ws(lds, g, k, rank == r ? v : z, lane);
+    return gmul_group_ws_full(lds, g, k);
+#else
     u32x4 g;
 #pragma unroll
     for (int c = 0; c < 4; ++c)
@@ -271,6 +373,7 @@ __device__ __forceinline__ u32x4 w8_lane_end(const lds_u8 *lds, u32x4 v, u32 lan
     for (u32 r = 1; r < 8; ++r)
         g = gmul_group_w_add(lds, g, W8_TAB_H, lane, rank == r ? v : z);
     return gmul_group_w(lds, g, W8_TAB_H, lane);
+#endif
 }
 
 // The W8 segment end of a long whole record (at least W8_MIN_STEPS steps, the EXT 3 kernel): the same sum by a butterfly over the

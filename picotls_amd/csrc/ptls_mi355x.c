@@ -15,8 +15,9 @@
  * Constant time. fusion's AES and GHASH are AES-NI / PCLMUL (lib/fusion.c:157-186, :323-335): their timing does not depend on
  * keys or data. The AEAD objects here therefore put their keysets in the engine's constant-time mode (every LDS access
  * with a data-independent bank pattern, include/picotls/mi355x.h ptls_mi355x_keyset_set_constant_time) unless the
- * environment sets PTLS_MI355X_CONSTANT_TIME=0. A per-record call is bound by its launch and PCIe round trip, so the
- * mode costs it little; batch keysets keep the engine's own default.
+ * environment sets PTLS_MI355X_CONSTANT_TIME=0. Since round 4 that is also the engine's own default for every keyset
+ * (ptls_mi355x_keyset_new creates them constant-time, batch keysets included), and both settings run the same kernels
+ * at the same rate; the explicit call here keeps the objects constant-time whatever that default is.
  *
  * Failure behaviour. picotls' encrypt callbacks cannot report errors (fusion asserts on OOM, lib/fusion.c:1143), so
  * every engine failure fails closed in every build: a failed seal overwrites the whole output (inlen + 16 bytes) with

@@ -12,8 +12,11 @@
 #include "picotls/fusion.h"
 #include "picotls/openssl.h"
 #include "picotls/mi355x_picotls.h"
+#include "picotls/mi355x_debug.h"
 
 static int nfail, ntest;
+/* `test_vtable lasterr`: a HIP error is left on the calling thread right before each engine call (inject_now) */
+static int g_inject;
 #define OK(cond, ...)                                                                                                       \
     do {                                                                                                                    \
         ++ntest;                                                                                                            \
@@ -191,6 +194,12 @@ static void quiclb_test(void)
     }
 }
 
+static void inject_now(void)
+{
+    if (g_inject)
+        OK(ptls_mi355x_debug_inject_error() != 0, "a HIP error is left on the thread before the engine call");
+}
+
 /* picotls' own TLS 1.2 record layer (ptls_build_tls12_export_params -> ptls_import -> ptls_send / ptls_receive,
  * lib/picotls.c:779-799, :6019-6060) over the MI355X non-temporal objects vs fusion's (lib/fusion.c:2159-2184) */
 static ptls_t *tls12_import(ptls_cipher_suite_t *suite, int is_server, const uint8_t *ms, const uint8_t *randoms,
@@ -218,6 +227,7 @@ static void tls12_send(ptls_aead_algorithm_t *aead, ptls_hash_algorithm_t *hash,
     ptls_context_t ctx;
     ptls_cipher_suite_t suite = {hash == &ptls_openssl_sha384 ? 0xc030 : 0xc02f, aead, hash, "tls12"}, *suites[2];
     ptls_t *tls = tls12_import(&suite, 1, ms, randoms, &ctx, suites);
+    inject_now();
     OK(tls != NULL && ptls_send(tls, out, data, len) == 0, "tls12 send");
     if (tls != NULL)
         ptls_free(tls);
@@ -233,6 +243,7 @@ static int tls12_receive(ptls_aead_algorithm_t *aead, ptls_hash_algorithm_t *has
     size_t off = 0;
     while (ret == 0 && off < len) {
         size_t consumed = len - off;
+        inject_now();
         ret = ptls_receive(tls, out, wire + off, &consumed);
         off += consumed;
     }
@@ -362,6 +373,43 @@ static int stress_main(int rounds)
     printf("# stress: %d rounds, %d with a TLS 1.2 failure, %d per-record failures\n", rounds, bad_rounds, bad_records);
     printf("1..%d\n# %d failed\n", ntest, nfail + bad_records);
     return nfail == 0 && bad_records == 0 ? 0 : 1;
+}
+
+/* run as `test_vtable lasterr` in a fresh process: the round-3 TLS 1.2 failure pattern
+ * with a handled HIP error deterministically present. Before every engine call -- picotls' TLS 1.2 ptls_send of 16384 +
+ * 16384 + 7232 bytes and each ptls_receive of fusion's records (the first uses of the 16 KiB and 32 KiB staging size
+ * classes of this process), then per-record seals and opens of those lengths -- the thread is left with the error a
+ * handled hipHostGetDevicePointer failure leaves (ptls_mi355x_debug_inject_error). Every wire byte and plaintext must
+ * equal fusion's. The shipped engine clears the thread's error before each launch (LAUNCH_CLEAR); a build with it
+ * compiled out (-DLAUNCH_CLEAR_NOOP=1, tools/gpu_recipes.sh lasterr5) fails exactly the round-3 checks. */
+static int lasterr_main(void)
+{
+    g_inject = 1;
+    tls12_test(&ptls_mi355x_non_temporal_aes128gcm, &ptls_non_temporal_aes128gcm, &ptls_openssl_sha256,
+               "lasterr: tls12 aes128gcm wire == fusion");
+    tls12_test(&ptls_mi355x_non_temporal_aes256gcm, &ptls_non_temporal_aes256gcm, &ptls_openssl_sha384,
+               "lasterr: tls12 aes256gcm wire == fusion");
+    static uint8_t text[16384], aad[13], a[16400], b[16400], dec[16384];
+    uint8_t key[16], iv[12];
+    rnd(key, sizeof(key)), rnd(iv, sizeof(iv));
+    ptls_aead_context_t *e = ptls_aead_new_direct(&ptls_mi355x_aes128gcm, 1, key, iv), *f = ptls_aead_new_direct(&ptls_fusion_aes128gcm, 1, key, iv),
+                        *d = ptls_aead_new_direct(&ptls_mi355x_aes128gcm, 0, key, iv);
+    static const size_t lens[4] = {16384, 16384, 7232, 100};
+    for (int k = 0; k < 4; ++k) {
+        size_t len = lens[k];
+        rnd(text, len), rnd(aad, sizeof(aad));
+        inject_now();
+        ptls_aead_encrypt(e, a, text, len, (uint64_t)k, aad, sizeof(aad));
+        ptls_aead_encrypt(f, b, text, len, (uint64_t)k, aad, sizeof(aad));
+        OK(memcmp(a, b, len + 16) == 0, "lasterr: per-record seal of %zu bytes equals fusion (last error: %s)", len,
+           ptls_mi355x_last_error());
+        inject_now();
+        OK(ptls_aead_decrypt(d, dec, b, len + 16, (uint64_t)k, aad, sizeof(aad)) == len && memcmp(dec, text, len) == 0,
+           "lasterr: per-record open of fusion's %zu-byte record", len);
+    }
+    ptls_aead_free(e), ptls_aead_free(f), ptls_aead_free(d);
+    printf("1..%d\n# %d failed\n", ntest, nfail);
+    return nfail == 0 ? 0 : 1;
 }
 
 /* Distinct contexts are independent and need no locking (SURVEY 8(b) Threading, lib/picotls.c:6553-6568): threads that
@@ -507,6 +555,8 @@ int main(int argc, char **argv)
         return failclosed_main();
     if (argc > 2 && strcmp(argv[1], "stress") == 0)
         return stress_main(atoi(argv[2]));
+    if (argc > 1 && strcmp(argv[1], "lasterr") == 0)
+        return lasterr_main();
     OK(strcmp(ptls_mi355x_aes128gcm.name, ptls_fusion_aes128gcm.name) == 0 && ptls_mi355x_aes128gcm.key_size == 16 &&
            ptls_mi355x_aes128gcm.iv_size == 12 && ptls_mi355x_aes128gcm.tag_size == 16 &&
            ptls_mi355x_aes128gcm.confidentiality_limit == ptls_fusion_aes128gcm.confidentiality_limit &&

@@ -33,6 +33,15 @@ def test_engine_library_loads_and_exports_header():
     assert not missing, missing
 
 
+def test_engine_library_exports_debug_hooks():
+    """include/picotls/mi355x_debug.h (test and measurement hooks, outside the picotls boundary) is exported too."""
+    decl = declared("mi355x_debug.h")
+    assert decl == set(pa.DEBUG_FUNCTIONS)
+    assert not decl & set(pa.ABI_FUNCTIONS)
+    missing = decl - exported(pa.LIB_PATH)
+    assert not missing, missing
+
+
 def test_picotls_backend_exports_algorithms():
     if not os.path.exists(pa.PICOTLS_LIB_PATH):
         pytest.skip("picotls headers were not available at build time")

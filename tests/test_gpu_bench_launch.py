@@ -64,6 +64,12 @@ def test_bench_eight_ranks_shard_the_configs4_index_space_once():
     assert all(shards[i][1] == shards[i + 1][0] for i in range(7))  # contiguous: every index exactly once
     assert all(z - a in (total // 8, total - 7 * (total // 8)) for a, z in shards)
     assert sh["value"] > 0 and out["value"] > 0
+    # every rank's seal / open / wall times, and the slowest rank named
+    for leg in (out, sh):
+        pr = leg["per_rank"]
+        assert len(pr["seal_ms"]) == len(pr["open_ms"]) == len(pr["wall_s"]) == 8
+        assert all(t > 0 for t in pr["seal_ms"] + pr["open_ms"] + pr["wall_s"])
+        assert pr["wall_s"][pr["slowest_rank"]] == pr["max_wall_s"] and pr["min_wall_s"] <= pr["max_wall_s"]
 
 
 def test_bench_single_gpu_line_has_shard1200_by_default():
@@ -72,6 +78,9 @@ def test_bench_single_gpu_line_has_shard1200_by_default():
     assert out["n_gpus"] == 1
     sh = out["extra"]["shard1200"]
     assert sh["scaling"] == "strong" and sh["n_gpus"] == 1 and sh["verified"]["roundtrip"] is True
+    # XCD 0's shader clock over each timed leg: a plausible MI355X clock
+    for leg in (out, sh):
+        assert leg["sclk_mhz"] is not None and 500 < leg["sclk_mhz"] < 3000, leg["sclk_mhz"]
 
 
 def test_bench_nccl_process_group_on_one_gpu():

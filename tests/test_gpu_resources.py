@@ -95,6 +95,24 @@ def test_picotls_contexts_are_constant_time_by_default(ref):
     ctx.free()
 
 
+def test_lockstep_schedule_never_silently_drops_constant_time():
+    """asking a constant-time keyset for the lockstep schedule raises (the keyset stays constant-time),
+    unless the caller says it accepts variable-time LDS access; then the schedule is set first and the setting turned
+    off after. The C call itself records the schedule and a constant-time keyset keeps the chunked kernels."""
+    rng = np.random.default_rng(33)
+    ks = pa.Keyset(rng.bytes(16), rng.bytes(12), 16)
+    ks.set_constant_time(True)
+    with pytest.raises(pa.EngineError):
+        ks.set_schedule("lockstep")
+    assert ks.constant_time
+    ks.set_schedule("chunked")
+    assert ks.constant_time
+    ks.set_schedule("lockstep", allow_variable_time=True)
+    assert not ks.constant_time
+    ks.set_schedule("lockstep")  # (no longer constant-time: nothing to protect)
+    ks.free()
+
+
 def test_encrypt_s_rejects_sample_past_the_record():
     rng = np.random.default_rng(33)
     ctx = pa.aead_new_direct(pa.aes128gcm, True, rng.bytes(16), rng.bytes(12))

@@ -144,26 +144,41 @@ def _record_mask(recs, size):
     return m
 
 
+def _pair_batch_lens(rng, n):
+    """Lengths of a batch whose every workgroup (256 CUs, contiguous ranges of 130 records) holds whole runs: mostly
+    8200-byte records (65 steps: EXT 3's long whole runs), 1200-byte ones in the first ten ranges (EXT 4's short whole
+    runs) and random lengths in the next ten (EXT 4's cut runs), so both kernels of a pair work and skip each other's
+    runs and EXT 4 writes the flag words that EXT 3 reads (at 2,048 records no flag word was ever
+    written on the device)."""
+    lens = np.full(n, 8200)
+    lens[:1300] = 1200
+    lens[1300:2600] = rng.integers(64, 16385, 1300)
+    return lens
+
+
 def test_w8_pairs_on_many_streams_vs_fusion(ref):
-    """W8 pairs of one keyset on 12 streams at once (more than W8_FLAG_STREAMS = 8, so streams take over the least
+    """W8 pairs of one keyset on 9 streams at once (more than W8_FLAG_STREAMS = 8, so a stream takes over the least
     recently used flag buffer): each stream has its own flag words, so the pairs run concurrently; every batch (long
-    whole runs, short whole runs and cut runs, so that both kernels of each pair skip runs) equals fusion, twice over."""
+    whole runs, short whole runs and cut runs, so that both kernels of each pair skip runs) equals fusion, twice over,
+    and the counters show both kernels processing runs."""
     rng = np.random.default_rng(8105)
-    nstreams, n = 12, 2048
+    nstreams, n = 9, 256 * 130
     key = np.frombuffer(rng.bytes(16), np.uint8)
     iv = np.frombuffer(rng.bytes(12), np.uint8)
     ks = pa.Keyset(key, iv, 16)
     jobs = []
     for i in range(nstreams):
-        lens = np.concatenate([np.full(n // 4, 16384), np.full(n // 4, 1200), rng.integers(64, 16385, n // 2)])
+        lens = _pair_batch_lens(rng, n)
         b = RecordBatch.build(lens, np.full(n, 13), seqs=rng.integers(0, 2**62, n, dtype=np.uint64))
         pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
         aad = np.frombuffer(rng.bytes(b.aad_bytes), np.uint8)
         want = np.zeros(b.sealed_bytes, np.uint8)
         ref.run_batch(True, key, iv, 16, b.seal, pt, aad, want, nthreads=8)
         jobs.append((b, dev(b.seal), dev(pt), dev(aad), empty(b.sealed_bytes), want))
+        del pt
     streams = [torch.cuda.Stream() for _ in range(nstreams)]
     torch.cuda.synchronize()
+    pa.debug_counters(reset=True)
     for rnd in range(2):
         for (b, d_recs, d_pt, d_aad, d_out, _), st in zip(jobs, streams if rnd == 0 else streams[::-1]):
             with torch.cuda.stream(st):
@@ -172,6 +187,10 @@ def test_w8_pairs_on_many_streams_vs_fusion(ref):
         torch.cuda.synchronize()
         for i, (b, _, _, _, d_out, want) in enumerate(jobs):
             assert np.array_equal(d_out[:b.sealed_bytes].cpu().numpy(), want), f"round {rnd}, stream {i}"
+    c = pa.debug_counters(reset=True)
+    assert c["launches"]["w8_serial"] == 2 * nstreams and c["launches"]["w8_tree"] == 2 * nstreams, c
+    # (at 256 CUs: ~236 EXT 3 runs and ~30 EXT 4 runs per batch)
+    assert c["runs"]["w8_tree"] >= 2 * nstreams * 100 and c["runs"]["w8_serial"] >= 2 * nstreams * 10, c
     ks.free()
 
 
@@ -191,27 +210,29 @@ def test_w8_tree_kernel_long_whole_runs_vs_fusion(ref, key_size, nkeys):
 
 
 def test_w8_pairs_from_many_threads_vs_fusion(ref):
-    """Ten threads, each on its own stream, seal their own batches through one shared keyset three times over: the
-    per-stream flag buffers are taken under the keyset's lock, and past W8_FLAG_STREAMS = 8 streams the least recently
-    used one is taken over after its stream's last use, while the launches overlap on the device. Every output equals
-    fusion's."""
+    """Nine threads, each on its own stream, seal their own batches (whole-run sized, _pair_batch_lens) through one
+    shared keyset three times over: the per-stream flag buffers are taken under the keyset's lock, and past
+    W8_FLAG_STREAMS = 8 streams the least recently used one is taken over after its stream's last use, while the
+    launches overlap on the device. Every output equals fusion's; the counters show both kernels processing runs."""
     import threading
 
     rng = np.random.default_rng(8106)
-    nthreads, n = 10, 2048
+    nthreads, n = 9, 256 * 130
     key = np.frombuffer(rng.bytes(32), np.uint8)
     iv = np.frombuffer(rng.bytes(12), np.uint8)
     ks = pa.Keyset(key, iv, 32)
     jobs = []
     for t in range(nthreads):
-        lens = np.concatenate([np.full(n // 2, 1200), rng.integers(64, 16385, n // 2)])
+        lens = _pair_batch_lens(rng, n)
         b = RecordBatch.build(lens, np.full(n, 13), seqs=rng.integers(0, 2**62, n, dtype=np.uint64))
         pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
         aad = np.frombuffer(rng.bytes(b.aad_bytes), np.uint8)
         want = np.zeros(b.sealed_bytes, np.uint8)
         ref.run_batch(True, key, iv, 32, b.seal, pt, aad, want, nthreads=8)
         jobs.append((b, dev(b.seal), dev(pt), dev(aad), [empty(b.sealed_bytes) for _ in range(3)], want))
+        del pt
     torch.cuda.synchronize()
+    pa.debug_counters(reset=True)
     errors = []
 
     def worker(t):
@@ -236,6 +257,9 @@ def test_w8_pairs_from_many_threads_vs_fusion(ref):
     for t, (b, _, _, _, outs, want) in enumerate(jobs):
         for k, o in enumerate(outs):
             assert np.array_equal(o[:b.sealed_bytes].cpu().numpy(), want), f"thread {t}, launch {k}"
+    c = pa.debug_counters(reset=True)
+    assert c["launches"]["w8_tree"] == 3 * nthreads and c["runs"]["w8_tree"] >= 3 * nthreads * 100, c
+    assert c["runs"]["w8_serial"] >= 3 * nthreads * 10, c
     ks.free()
 
 

@@ -81,3 +81,89 @@ def test_8bit_lookup_is_the_product():
             n = byts[w]
             acc ^= e4(2 * w, n >> 4) ^ e4(2 * w + 1, n & 15)
         assert acc == gmul(a, h8)
+
+
+# ---- lane-level models of the scattered chains (ghash.h group_scatter / group_gather / group_ws, round 5)
+
+def _dpp(vals, src_of):  # update_dpp within each 8-lane group: lane y reads lane src_of(y)
+    return [vals[src_of(y)] for y in range(8)]
+
+
+def _scatter(t):  # t[y] = the 4 dwords of lane y
+    b = [(y & 4) != 0 for y in range(8)]
+    c = [(y & 2) != 0 for y in range(8)]
+    k0 = [t[y][2] if b[y] else t[y][0] for y in range(8)]
+    k1 = [t[y][3] if b[y] else t[y][1] for y in range(8)]
+    s0 = [t[y][0] if b[y] else t[y][2] for y in range(8)]
+    s1 = [t[y][1] if b[y] else t[y][3] for y in range(8)]
+    mirror = lambda y: 7 - y  # row_half_mirror inside 8 lanes
+    m0 = [k ^ s for k, s in zip(k0, _dpp(s0, mirror))]
+    m1 = [k ^ s for k, s in zip(k1, _dpp(s1, mirror))]
+    kk = [m1[y] if c[y] else m0[y] for y in range(8)]
+    ss = [m0[y] if c[y] else m1[y] for y in range(8)]
+    m = [k ^ s for k, s in zip(kk, _dpp(ss, lambda y: y ^ 2))]  # quad_perm [2,3,0,1]
+    return [a ^ s for a, s in zip(m, _dpp(m, lambda y: y ^ 1))]  # quad_perm [1,0,3,2]
+
+
+def _gather(g):
+    a = _dpp(g, lambda y: y & 4)  # quad_perm [0,0,0,0]
+    b = _dpp(g, lambda y: (y & 4) | 2)  # quad_perm [2,2,2,2]
+    am, bm = _dpp(a, lambda y: 7 - y), _dpp(b, lambda y: 7 - y)
+    return [[am[y], bm[y], a[y], b[y]] if y & 4 else [a[y], b[y], am[y], bm[y]] for y in range(8)]
+
+
+def test_group_scatter_gives_each_lane_its_dword_of_the_sum():
+    rng = np.random.default_rng(11)
+    for _ in range(200):
+        t = [[int(x) for x in rng.integers(0, 2**32, 4, dtype=np.uint64)] for _ in range(8)]
+        total = [0, 0, 0, 0]
+        for y in range(8):
+            for c in range(4):
+                total[c] ^= t[y][c]
+        g = _scatter(t)
+        assert all(g[y] == total[y >> 1] for y in range(8))
+        assert all(row == total for row in _gather(g))
+
+
+def test_group_ws_nibble_offsets_equal_gmul_group_w():
+    # gmul_group_w: shift sh ^ 4 (i ^ 1), sh = 4 f + 16 (y & 1); group_ws: 16 (y & 1) + (4 f ^ 4 (i ^ 1)); the same
+    # nibble of the lane's dword y >> 1, i.e. window 4 y + (i ^ f) of its halfword (ghash.h, window-major comment)
+    for lane in range(64):
+        y, f = lane & 7, (lane >> 2) & 3
+        for i in range(4):
+            old = (4 * f + 16 * (y & 1)) ^ (4 * (i ^ 1))
+            new = 16 * (lane & 1) + ((4 * f) ^ (4 * (i ^ 1)))
+            assert old == new
+            u = i ^ f  # window 4y + u sits at bit 4 (u ^ 1) of the halfword
+            assert new == 16 * (y & 1) + 4 * (u ^ 1)
+
+
+def test_scattered_serial_chain_equals_the_powers():
+    # the chain run on scattered values is the plain chain: a link's terms XOR-reduced once over the group equal the
+    # all-reduced product (linearity), so sum_r v_r H^(8 - r) comes out for any rank rotation
+    rng = np.random.default_rng(12)
+    h = int.from_bytes(rng.bytes(16), "big")
+    for _ in range(10):
+        v = [int.from_bytes(rng.bytes(16), "big") for _ in range(8)]
+        rot = int(rng.integers(0, 8))
+        rank = [(j - rot) % 8 for j in range(8)]
+        want = 0
+        for j in range(8):
+            want ^= gmul(v[j], gpow(h, 8 - rank[j]))
+        # scattered: each link's product split into 8 lane terms (any split whose XOR is the product), plus the value
+        # of the lane of rank r on that lane; the reduce-scatter gives each lane its dword of the sum
+        to_w = lambda x: [(x >> (96 - 32 * c)) & 0xFFFFFFFF for c in range(4)]
+        from_w = lambda w: (w[0] << 96) | (w[1] << 64) | (w[2] << 32) | w[3]
+        cur = 0
+        for r in range(8):
+            prod = gmul(cur, h) if r else 0
+            parts = [int.from_bytes(rng.bytes(16), "big") for _ in range(7)]
+            last = prod
+            for p in parts:
+                last ^= p
+            terms = parts + [last]
+            t = [to_w(terms[y] ^ (v[y] if rank[y] == r else 0)) for y in range(8)]
+            g = _scatter(t)
+            cur = from_w([g[2 * q] for q in range(4)])
+            assert all(g[y] == to_w(cur)[y >> 1] for y in range(8))
+        assert gmul(cur, h) == want

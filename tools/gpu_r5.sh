@@ -1,0 +1,45 @@
+#!/bin/bash
+# Round-5 GPU recipes (run on the GPU box through gpurun, from the repository root):  bash tools/gpu_r5.sh <name>
+# Variant engines for these recipes live under tools/gv/<name>/libptls_mi355x.so (built with tools/mkvariant.sh-style
+# hipcc lines; tools/gv is not in .gpurunignore, unlike tools/variants).
+set +e
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+recipe=$1; shift
+case "$recipe" in
+check)
+  # the round's new and changed GPU tests: exact-shape headline parity (EXT 3 counted), W8 pairs on streams and threads
+  # at whole-run sizes, the handled-error regression test, the lockstep / constant-time rule, the bench launch tests
+  timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_headline.py \
+      tests/test_gpu_w8.py tests/test_gpu_resources.py tests/test_gpu_bench_launch.py \
+      "tests/test_gpu_parity.py::test_picotls_vtable_tls12_with_handled_errors_left_on_the_thread" \
+      > gpurun_out/r5_check.log 2>&1; rc=$?
+  echo "pytest rc=$rc"; grep -E "PASSED|FAILED|ERROR" gpurun_out/r5_check.log | tail -40; tail -3 gpurun_out/r5_check.log
+  exit $rc
+  ;;
+lasterr5)
+  # the regression test against an engine with LAUNCH_CLEAR() compiled out (must fail the
+  # TLS 1.2 checks) and against the shipped engine (must pass); the C binary is the same
+  {
+  echo "== engine built with -DLAUNCH_CLEAR_NOOP=1 (tools/gv/noop)"
+  LD_LIBRARY_PATH=$PWD/tools/gv/noop timeout -k 10 120 tests/c/_bin/test_vtable lasterr; echo "exit status $?"
+  echo "== shipped engine (picotls_amd/_lib)"
+  timeout -k 10 120 tests/c/_bin/test_vtable lasterr; echo "exit status $?"
+  } > gpurun_out/lasterr_regression.txt 2>&1
+  cat gpurun_out/lasterr_regression.txt | tail -40
+  grep -q "== shipped" gpurun_out/lasterr_regression.txt && tail -1 gpurun_out/lasterr_regression.txt | grep -q "exit status 0"
+  ;;
+ab)
+  # interleaved A/B (tools/ab.py, one process per workload) of tools/gv/<name> engines at the full BASELINE sizes:
+  #   bash tools/gpu_r5.sh ab "base scat" [tag] [workloads...]
+  names=$1; tag=${2:-ab}; shift 2 2>/dev/null
+  wls=${*:-"quic1200:4194304 tls16k:1048576 mixed:4194304"}
+  libs=""; for n in $names; do libs="$libs tools/gv/$n/libptls_mi355x.so"; done
+  for wn in $wls; do w=${wn%%:*}; r=${wn##*:}
+    timeout -k 10 400 python tools/ab.py $libs --workload $w --records $r --rounds 5 --reps 2 > gpurun_out/${tag}_$w.log 2>&1
+    rc=$?; echo "== $w rc=$rc"; grep -v amdgpu.ids gpurun_out/${tag}_$w.log | tail -6; [ $rc -ne 0 ] && exit $rc
+  done
+  exit 0
+  ;;
+*)
+  echo "unknown recipe $recipe"; exit 2 ;;
+esac
