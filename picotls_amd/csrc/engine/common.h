@@ -163,6 +163,14 @@ __device__ __forceinline__ u32 lane_here()
 // -4 %, 1000 x 16 KiB even, 4096 x 16 KiB +7 %; profiles/r4/w8all_ab.txt)
 #define W8_MIN_RECS 2048
 #endif
+#ifndef W8_SWAP
+// (round 5) the W8 kernels' LDS map puts the 8-bit H^8 table at [0, 64K) and the AES T-tables at [64K, 128K): the
+// table's address bytes are then two (window, value), formed by one v_perm from registers that stay fixed through the
+// loop, and the AES addresses take their 64 KiB slot from laneoff's byte 2 in the same v_perm (aes_tt.h TE_ADDR)
+#define W8_SWAP 1
+#endif
+#define W8_H8_BASE (W8_SWAP ? 0u : (u32)LDS_AES_BYTES)   // the W8 kernels' 8-bit H^8 table
+#define W8_AES_BASE (W8_SWAP ? (u32)LDS_AES_BYTES : 0u)  // ... and their AES T-tables
 #define W8_RUN_UNITS 512  // units per run of a launch pair (both kernels: their runs must be the same)
 #define W8_TAB_H (LDS_AES_BYTES + 8 * GHASH_TABLE_BYTES)
 #define W8_TAB_COMB (CLDS_PART + 16 * W8_RUN_UNITS)

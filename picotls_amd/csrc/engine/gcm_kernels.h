@@ -841,7 +841,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             PROF_ADD(9, stamp() - tk), PROF_ADD(10, 1);
 #endif
     } else {
-        build_aes_tables(lds, 64, early ? EARLY_GHASH_WAVE * 64 : 0);
+        build_aes_tables(lds, 64, early ? EARLY_GHASH_WAVE * 64 : 0, W8K ? W8_AES_BASE : 0u);
 #if ENGINE_PROFILE
         if (threadIdx.x == 64)
             PROF_ADD(8, stamp() - tk);
@@ -1009,7 +1009,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             u32x4 acc;
             u32 okw;
             {
-                const u32 lane = lane_here(), j = lane % G, slot = lane / G, laneoff = (lane & 31) * 4;
+                const u32 lane = lane_here(), j = lane % G, slot = lane / G, laneoff = (lane & 31) * 4 | (W8K ? W8_AES_BASE : 0u);
                 const u32 u = ub + slot;
                 const bool valid = u < total_units;
                 u32 lo, first, unc, k_back;

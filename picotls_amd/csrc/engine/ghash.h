@@ -105,18 +105,56 @@ __device__ __forceinline__ u32x4 gmul_group_w(const lds_u8 *, u32x4 a, u32 tsel,
 // (tools/mb/ghash8.hip: +20.8 % on the engine's step). W8Lane holds the lane's address base B (l in the window bits of
 // bytes 0 and 1, byte 2 of the table base) and byte selector; the lookups' address words B ^ (2k, 2k + 1 window bits)
 // are formed at each multiply (B made opaque there: kept live through the loop, the eight words spilled the kernel).
+//
+// W8_SWAP (round 5): the table sits at LDS address 0, so an address is two bytes: byte 0 the window (operand byte
+// (i ^ l), times 16), byte 1 the operand's byte value, bytes 2-3 zero (v_perm's constant selector). The window bytes of
+// lookups 4c..4c+3 are one register, L_c = L_0 ^ 0x40404040 c (bits 6-7 of ((4c + t) ^ l) << 4 are c ^ (l >> 2)), so
+// the 16 addresses cost 16 v_perm and 3 XORs per multiply instead of 16 v_perm and 8 XORs; and the operand's dword swap
+// by bit 2 of l and byte permutation by bits 0-1 merge into one two-source v_perm per dword (4 selects and 4 v_perm
+// instead of 8 and 4): 9 VALU operations fewer per Horner step.
 struct W8Lane {
-    u32 base;
-    u32 psel;
+    u32 base;  // W8_SWAP: L_0, the window bytes of lookups 0..3; else B
+    u32 psel;  // byte c <- byte c ^ (l & 3) (W8_SWAP: from the pair's other dword when bit 2 of l is set)
 };
 __device__ __forceinline__ W8Lane w8_lane(u32 lane)
 {
     const u32 l = lane & 15, lb = l & 3;
+    if constexpr (W8_SWAP) {
+        u32 L0 = 0;
+#pragma unroll
+        for (u32 t = 0; t < 4; ++t)
+            L0 |= ((t ^ l) << 4) << (8 * t);
+        return W8Lane{L0, (lb * 0x01010101u ^ 0x03020100u) + ((l & 4) ? 0x04040404u : 0u)};
+    }
     return W8Lane{(l << 4) | (l << 12) | ((u32)(LDS_AES_BYTES >> 16) << 16), lb * 0x01010101u ^ 0x03020100u};
 }
 __device__ __forceinline__ u32x4 gmul8(const lds_u8 *, u32x4 t, u32 lane, W8Lane w)
 {
     asm volatile("" : "+v"(w.base));
+    if constexpr (W8_SWAP) {
+        static_assert(!W8_SWAP || W8_H8_BASE == 0, "the table's address bytes 2-3 are zero");
+        u32 L[4];
+#pragma unroll
+        for (u32 c = 0; c < 4; ++c)
+            L[c] = w.base ^ (c * 0x40404040u);
+        // p[k] byte c = t byte ((4k + c) ^ l): the dword pair by bit 3 of l (selects), then dword k ^ (bit 2 of l) and
+        // the bytes by bits 0-1 in one v_perm of the pair (psel picks from the other dword when bit 2 is set)
+        const bool s2 = (lane & 8) != 0;
+        const u32 a0 = s2 ? t[2] : t[0], a1 = s2 ? t[3] : t[1], a2 = s2 ? t[0] : t[2], a3 = s2 ? t[1] : t[3];
+        const u32 p[4] = {__builtin_amdgcn_perm(a1, a0, w.psel), __builtin_amdgcn_perm(a0, a1, w.psel),
+                          __builtin_amdgcn_perm(a3, a2, w.psel), __builtin_amdgcn_perm(a2, a3, w.psel)};
+        u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+        for (u32 i = 0; i < 16; i += 2) {
+            const u32 c = i >> 2, b = i & 3;
+            const u32x4 e0 = lds_load128(__builtin_amdgcn_perm(p[c], L[c], 0x0c0c0000u | ((4u + b) << 8) | b));
+            const u32x4 e1 = lds_load128(__builtin_amdgcn_perm(p[c], L[c], 0x0c0c0000u | ((5u + b) << 8) | (b + 1)));
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                acc[k] = xor3(acc[k], e0[k], e1[k]);
+        }
+        return acc;
+    }
     u32 wreg[8];
 #pragma unroll
     for (u32 k = 0; k < 8; ++k)

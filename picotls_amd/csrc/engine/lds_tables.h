@@ -37,13 +37,13 @@ constexpr AesTtabImage make_aes_ttab()
 __device__ const AesTtabImage g_aes_ttab = make_aes_ttab();
 
 // Threads [skip, end) build it (end 0: blockDim.x; both multiples of 64; the chunked kernel's other waves scan the first
-// run and build the GHASH tables meanwhile)
-__device__ void build_aes_tables(lds_u8 *lds, u32 skip = 0, u32 end = 0)
+// run and build the GHASH tables meanwhile), at LDS offset base (0, or 64 KiB in the W8 kernels: W8_SWAP)
+__device__ void build_aes_tables(lds_u8 *lds, u32 skip = 0, u32 end = 0, u32 base = 0)
 {
     const u32 tid = threadIdx.x - skip, nthr = (end != 0 ? end : blockDim.x) - skip;
 #if AES_TTAB_COPY
     const u32x4 *src = (const u32x4 *)g_aes_ttab.v;
-    lds_u32x4 *dst = (lds_u32x4 *)lds;
+    lds_u32x4 *dst = (lds_u32x4 *)(lds + base);
     // every thread's loads are in flight before its first LDS write (AES_TTAB_BATCH of them: one round trip for 512
     // threads or more)
     for (u32 base = 0; base < 256 * 64 / 4; base += AES_TTAB_BATCH * nthr) {
@@ -61,7 +61,7 @@ __device__ void build_aes_tables(lds_u8 *lds, u32 skip = 0, u32 end = 0)
         }
     }
 #else
-    lds_u32 *t = (lds_u32 *)lds;
+    lds_u32 *t = (lds_u32 *)(lds + base);
     // entry n = idx >> 6 is wave-uniform (blockDim.x is a multiple of 64): scalar S-box loads, 16 in flight per batch,
     // so a launch pays one memory latency here instead of one per loop trip (the per-record path is a launch of one)
     for (u32 base = 0; base < 256 * 64; base += 16 * nthr) {
@@ -152,7 +152,7 @@ __device__ void build_ghash_tables(lds_u8 *lds, KeyPtr key, u32 ntables = ENGINE
     }
 }
 
-// W8 runs (ghash.h): the 8-bit window-major H^8 table at LDS_AES_BYTES from H^8's 4-bit nibble-major table at `scratch`
+// W8 runs (ghash.h): the 8-bit window-major H^8 table at W8_H8_BASE from H^8's 4-bit nibble-major table at `scratch`
 // (entry (w, n) = e4(2w, n >> 4) ^ e4(2w + 1, n & 15): byte w of the operand is 4-bit windows 2w and 2w + 1)
 // Lane w of a 16-lane phase takes value n = k ^ (w << 4) ^ w (k = i >> 4): its two reads land in bank groups
 // (n >> 4) and (n & 15), both distinct across w, and its store in group w (round 4: the plain order n = k read one bank
@@ -163,7 +163,7 @@ __device__ __forceinline__ void build_h8_byte_table(lds_u8 *lds, u32 scratch)
         const u32 w = i & 15, n = (i >> 4) ^ (w << 4) ^ w;
         const u32x4 e = u32x4(*(const lds_u32x4 *)(lds + scratch + (2 * w) * 256 + (n >> 4) * 16)) ^
                         u32x4(*(const lds_u32x4 *)(lds + scratch + (2 * w + 1) * 256 + (n & 15) * 16));
-        *(lds_u32x4 *)(lds + LDS_AES_BYTES + n * 256 + w * 16) = e;
+        *(lds_u32x4 *)(lds + W8_H8_BASE + n * 256 + w * 16) = e;
     }
 }
 
