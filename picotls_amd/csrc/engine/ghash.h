@@ -119,13 +119,8 @@ struct W8Lane {
 __device__ __forceinline__ W8Lane w8_lane(u32 lane)
 {
     const u32 l = lane & 15, lb = l & 3;
-    if constexpr (W8_SWAP) {
-        u32 L0 = 0;
-#pragma unroll
-        for (u32 t = 0; t < 4; ++t)
-            L0 |= ((t ^ l) << 4) << (8 * t);
-        return W8Lane{L0, (lb * 0x01010101u ^ 0x03020100u) + ((l & 4) ? 0x04040404u : 0u)};
-    }
+    if constexpr (W8_SWAP)  // byte t of L_0: (t ^ l) << 4 (l < 16: no carries between bytes)
+        return W8Lane{((l * 0x01010101u) ^ 0x03020100u) << 4, (lb * 0x01010101u ^ 0x03020100u) | ((l & 4) * 0x01010101u)};
     return W8Lane{(l << 4) | (l << 12) | ((u32)(LDS_AES_BYTES >> 16) << 16), lb * 0x01010101u ^ 0x03020100u};
 }
 __device__ __forceinline__ u32x4 gmul8(const lds_u8 *, u32x4 t, u32 lane, W8Lane w)
@@ -355,8 +350,8 @@ __device__ __forceinline__ u32x4 group_ws_terms(u32 ga, const GroupWs &k, u32x4 
 {
     u32x4 e[4];
 #pragma unroll
-    for (u32 i = 0; i < 4; ++i)
-        e[i] = lds_load128((((ga >> k.sh[i]) & 15u) << 8) | k.Wi[i]);
+    for (u32 i = 0; i < 4; ++i)  // (v_bfe_u32 + v_lshl_or_b32)
+        e[i] = lds_load128((__builtin_amdgcn_ubfe(ga, k.sh[i], 4u) << 8) | k.Wi[i]);
     u32x4 t;
 #pragma unroll
     for (int c = 0; c < 4; ++c)
