@@ -291,8 +291,8 @@ __device__ __forceinline__ u32x4 gmul_group_w_add(const lds_u8 *, u32x4 a, u32 t
 // halfword y of the previous product, not the whole product in every lane. gmul_group_w all-reduces each product over
 // the 8 lanes (dpp_xor8 of 4 dwords: 12 DPP operations) and each lane then picks its dword (3 selects). Here a link
 // reduce-scatters instead (group_scatter: 10 operations; lane y keeps dword y >> 1 of the sum, complete) and extracts
-// its nibbles with a bit-field extract and an OR into the opaque per-lane window bases (2 operations a lookup instead
-// of 4): ~30 VALU operations a link instead of ~46 (the EXT 4 kernel's segment end: 413 VALU instructions in the code
+// its nibbles with a bit-field extract and a shift-add onto the opaque per-lane window bases (2 operations a lookup
+// instead of 4): ~30 VALU operations a link instead of ~46 (the EXT 4 kernel's segment end: 413 VALU instructions in the code
 // object before, round 5). The lookups and tables are gmul_group_w's: conflict-free by construction.
 struct GroupWs {
     u32 Wi[4];  // the lane's window base for lookup i (wtab_lane_base ^ i << 4)
@@ -350,8 +350,8 @@ __device__ __forceinline__ u32x4 group_ws_terms(u32 ga, const GroupWs &k, u32x4 
 {
     u32x4 e[4];
 #pragma unroll
-    for (u32 i = 0; i < 4; ++i)  // (v_bfe_u32 + v_lshl_or_b32)
-        e[i] = lds_load128((__builtin_amdgcn_ubfe(ga, k.sh[i], 4u) << 8) | k.Wi[i]);
+    for (u32 i = 0; i < 4; ++i)  // (v_bfe_u32 + v_lshl_add_u32: a table base need only be a multiple of 256)
+        e[i] = lds_load128((__builtin_amdgcn_ubfe(ga, k.sh[i], 4u) << 8) + k.Wi[i]);
     u32x4 t;
 #pragma unroll
     for (int c = 0; c < 4; ++c)

@@ -384,7 +384,7 @@ static int stress_main(int rounds)
  * compiled out (-DLAUNCH_CLEAR_NOOP=1, tools/gpu_recipes.sh lasterr5) fails exactly the round-3 checks. */
 static int lasterr_main(void)
 {
-    g_inject = 1;
+    g_inject = getenv("PTLS_TEST_NO_INJECT") == NULL; /* (PTLS_TEST_NO_INJECT: the same calls without the injected error) */
     tls12_test(&ptls_mi355x_non_temporal_aes128gcm, &ptls_non_temporal_aes128gcm, &ptls_openssl_sha256,
                "lasterr: tls12 aes128gcm wire == fusion");
     tls12_test(&ptls_mi355x_non_temporal_aes256gcm, &ptls_non_temporal_aes256gcm, &ptls_openssl_sha384,

@@ -28,6 +28,23 @@ lasterr5)
   cat gpurun_out/lasterr_regression.txt | tail -40
   grep -q "== shipped" gpurun_out/lasterr_regression.txt && tail -1 gpurun_out/lasterr_regression.txt | grep -q "exit status 0"
   ;;
+firstcall)
+  # the TLS 1.2 first-call tag difference of lasterr5 (round 5): fresh processes with and without the injected error,
+  # the shipped engine and the base variant, then the whole vtable suite
+  for v in shipped base; do for inj in 1 0; do
+    if [ $v = base ]; then LIB="LD_LIBRARY_PATH=$PWD/tools/gv/base"; else LIB=""; fi
+    if [ $inj = 0 ]; then NI="PTLS_TEST_NO_INJECT=1"; else NI=""; fi
+    for rep in 1 2; do
+      env $LIB $NI timeout -k 10 120 tests/c/_bin/test_vtable lasterr > gpurun_out/fc_${v}_inj${inj}_$rep.txt 2>&1; rc=$?
+      echo "== $v inject=$inj rep=$rep exit=$rc: $(grep -c '^not ok' gpurun_out/fc_${v}_inj${inj}_$rep.txt) failed checks"
+      grep -A2 "^not ok" gpurun_out/fc_${v}_inj${inj}_$rep.txt | head -8
+      [ $rc -gt 1 ] && exit $rc
+    done
+  done; done
+  timeout -k 10 300 tests/c/_bin/test_vtable > gpurun_out/fc_full.txt 2>&1; rc=$?
+  echo "== full suite exit=$rc"; grep "^not ok" gpurun_out/fc_full.txt | head; tail -2 gpurun_out/fc_full.txt
+  exit 0
+  ;;
 ab)
   # interleaved A/B (tools/ab.py, one process per workload) of tools/gv/<name> engines at the full BASELINE sizes:
   #   bash tools/gpu_r5.sh ab "base scat" [tag] [workloads...]
