@@ -154,6 +154,8 @@ struct DeviceState {
     size_t stage_limit = 0;       // PTLS_MI355X_MAX_STAGE_BYTES: the largest staging buffer one call may use
     bool ct_default = true;       // new keysets are constant-time (PTLS_MI355X_CONSTANT_TIME=0: not, for an A/B)
     bool fault_order = false;     // PTLS_MI355X_FAULT_ORDER=1 (tests only): keyset teardown cannot order itself on the device
+    bool diag = false;            // PTLS_MI355X_DIAG=1 (diagnosis only): per-record calls re-read their results after a stream
+                                  // synchronisation and report bytes that changed after the completion words were seen
     std::mutex mu;                // the pools below
     Stager *stagers[STAGE_CLASSES] = {};
     size_t stage_idle = 0;        // pinned bytes of the idle stagers above
@@ -283,6 +285,8 @@ static DeviceState *device_state(int dev)
     if (pool != nullptr)
         ds->stage_pool_cap = (size_t)strtoull(pool, nullptr, 0);
     ds->fault_order = fo != nullptr && strcmp(fo, "1") == 0;
+    const char *dg = getenv("PTLS_MI355X_DIAG");
+    ds->diag = dg != nullptr && strcmp(dg, "1") == 0;
     ds->stage_limit = limit != nullptr ? (size_t)strtoull(limit, nullptr, 0) : (size_t)4096 << (STAGE_CLASSES - 1);
     int least = 0;
     if (hipDeviceGetStreamPriorityRange(&least, &ds->priority) != hipSuccess)
@@ -1853,6 +1857,25 @@ static void run_calls(DeviceState *ds, OneCall *const *c, size_t n)
                     if (hp)
                         memcpy(x.mask, h + off_mask + 16 * i, 16);
                     out_at += a16(outbytes);
+                }
+                if (ds->diag && flag && call.mapped()) {
+                    // (diagnosis: did any result byte change after the completion words were seen?)
+                    (void)hipStreamSynchronize(s);
+                    size_t at = up;
+                    for (size_t i = 0; i < n; ++i) {
+                        const OneCall &x = *c[i];
+                        const size_t outbytes = x.len + (open ? 0 : 16);
+                        size_t diff = 0, first = SIZE_MAX;
+                        for (size_t b = 0; b < outbytes; ++b)
+                            if (h[at + b] != ((const uint8_t *)x.output)[b])
+                                diff++, first = first == SIZE_MAX ? b : first;
+                        const bool okchg = open && h[off_ok + i] != (uint8_t)*x.verified;
+                        if (diff != 0 || okchg)
+                            fprintf(stderr, "ptls_mi355x diag: %s of %zu bytes: %zu result bytes (first at %zu)%s changed after the "
+                                            "completion words were seen\n", open ? "open" : "seal", x.len, diff,
+                                    first == SIZE_MAX ? (size_t)0 : first, okchg ? " and the ok byte" : "");
+                        at += a16(outbytes);
+                    }
                 }
             }
         }

@@ -273,6 +273,23 @@ static void tls12_describe_diff(const char *what, const uint8_t *a, size_t alen,
             printf("# %s: record %zu (wire offset %zu, %zu bytes) first differs at record offset %zu (%s); %zu of %zu ciphertext "
                    "bytes and %zu of 16 tag bytes differ\n",
                    what, rec, off, rlen, first, field, nct, rlen - 29, ntag);
+            printf("#   tag here ");
+            for (size_t i = rlen - 16; i < rlen; ++i)
+                printf("%02x", a[off + i]);
+            printf(", fusion's ");
+            for (size_t i = rlen - 16; i < rlen; ++i)
+                printf("%02x", b[off + i]);
+            printf("\n");
+            /* the other records of the stream */
+            size_t o2 = off + rlen, r2 = rec + 1, bad2 = 0;
+            while (o2 + 5 <= alen && o2 + 5 <= blen) {
+                size_t l2 = 5 + ((size_t)a[o2 + 3] << 8 | a[o2 + 4]);
+                if (o2 + l2 > alen || o2 + l2 > blen)
+                    break;
+                bad2 += memcmp(a + o2, b + o2, l2) != 0;
+                o2 += l2, ++r2;
+            }
+            printf("#   later records of the stream: %zu of %zu differ\n", bad2, r2 - rec - 1);
             return;
         }
         off += rlen, ++rec;

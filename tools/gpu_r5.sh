@@ -45,6 +45,21 @@ firstcall)
   echo "== full suite exit=$rc"; grep "^not ok" gpurun_out/fc_full.txt | head; tail -2 gpurun_out/fc_full.txt
   exit 0
   ;;
+firstcall2)
+  # (round 5) fresh processes whose first engine calls are picotls' TLS 1.2 exchanges (test_vtable lasterr): how often the
+  # first record's tag differs, what the wrong tag holds, and (PTLS_MI355X_DIAG=1) whether result bytes changed after the
+  # completion words were seen
+  nf=0
+  for i in $(seq 1 ${1:-16}); do for d in 1 0; do
+    PTLS_MI355X_DIAG=$d timeout -k 10 60 tests/c/_bin/test_vtable lasterr > gpurun_out/fc2_${i}_d$d.txt 2>&1; rc=$?
+    [ $rc -gt 1 ] && { echo "process $i diag=$d exit $rc"; tail -5 gpurun_out/fc2_${i}_d$d.txt; exit $rc; }
+    if [ $rc -ne 0 ] || grep -q "ptls_mi355x diag" gpurun_out/fc2_${i}_d$d.txt; then
+      nf=$((nf+1)); echo "== process $i diag=$d exit $rc"; grep -E "^not ok|^#|diag" gpurun_out/fc2_${i}_d$d.txt | head -12
+    fi
+  done; done
+  echo "processes with a difference: $nf of $((2 * ${1:-16}))"
+  exit 0
+  ;;
 ab)
   # interleaved A/B (tools/ab.py, one process per workload) of tools/gv/<name> engines at the full BASELINE sizes:
   #   bash tools/gpu_r5.sh ab "base scat" [tag] [workloads...]
