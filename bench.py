@@ -179,7 +179,8 @@ def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool
     open_ms = float(np.mean([bb.elapsed_time(c) for _, bb, c in ev]))
 
     res = {"records": b.n, "payload_bytes": b.payload_bytes, "wall_s": wall, "seal_ms": seal_ms, "open_ms": open_ms,
-           "shard": [begin, end], "sclk_mhz": shader_clock_mhz(clk.cpu().numpy())}
+           "shard": [begin, end], "clock": shader_clock(clk.cpu().numpy(), wall)}
+    res["sclk_mhz"] = res["clock"]["sclk_mhz"]
     lens = b.seal["len"]
     res["seal_alg_bytes"] = algorithmic_bytes(lens, b.seal["aad_len"], True)
     res["open_alg_bytes"] = algorithmic_bytes(lens, b.seal["aad_len"], False)
@@ -200,17 +201,18 @@ def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool
     return res
 
 
-def shader_clock_mhz(c) -> float | None:
-    """XCD 0's average shader clock over a timed leg from two clock probes (ptls_mi355x_debug_clock_sample: s_memtime
-    counts shader-clock cycles, s_memrealtime ticks at the device's wall-clock rate), or None when the two samples came
-    from different XCDs or the rate is unknown."""
+def shader_clock(c, wall_s: float) -> dict:
+    """XCD 0's average shader clock over a timed leg from two clock probes enqueued at its start and end
+    (ptls_mi355x_debug_clock_sample: s_memtime counts shader-clock cycles): cycles / the host's wall time of the leg
+    (the probes bracket it in stream order; launch latency is microseconds of a leg of ~0.1-1 s). Also the raw counts and
+    the real-time counter's rate implied by the same interval, beside the rate the runtime reports."""
     import picotls_amd as pa
 
-    khz = pa.debug_wallclock_khz()
     dt, drt = int(c[4]) - int(c[0]), int(c[5]) - int(c[1])
-    if khz <= 0 or drt <= 0 or dt <= 0 or int(c[2]) != int(c[6]):
-        return None
-    return round(dt / (drt / (khz * 1e3)) / 1e6, 1)
+    same_xcd = int(c[2]) == int(c[6])
+    return {"sclk_mhz": round(dt / wall_s / 1e6, 1) if dt > 0 and wall_s > 0 and same_xcd else None, "cycles": dt,
+            "rtc_ticks": drt, "rtc_khz_measured": round(drt / wall_s / 1e3, 1) if wall_s > 0 else None,
+            "rtc_khz_reported": pa.debug_wallclock_khz(), "xcd": int(c[2]), "same_xcd": same_xcd}
 
 
 def zero_slot_padding(arena, recs, dev):
@@ -715,7 +717,7 @@ def main():
         "lds_model": lds_model(res, wl.key_size, res["records"]),
         "verified": {"roundtrip": res.get("verified_roundtrip"), "fusion_spot_check": None, "fusion_open_spot_check": None},
         # XCD 0's average shader clock over the timed steps (rank 0), so that box-to-box spread can be attributed
-        "sclk_mhz": res.get("sclk_mhz"),
+        "sclk_mhz": res.get("sclk_mhz"), "clock_probe": res.get("clock"),
     }
     if R.world > 1:
         out["per_rank"] = per_rank(R, res)
