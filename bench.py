@@ -163,14 +163,14 @@ def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool
     R.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    pa.debug_clock_sample(clk.data_ptr(), sp)
-    for e0, e1, e2 in ev:
+    for k, (e0, e1, e2) in enumerate(ev):
         e0.record(stream)
         seal()
         e1.record(stream)
         open_()
         e2.record(stream)
-    pa.debug_clock_sample(clk.data_ptr() + 32, sp)
+        if k == 0 or k == len(ev) - 1:  # (~20 us each, in a leg of ~0.1-1 s)
+            pa.debug_clock_sample(clk.data_ptr() + (32 if k else 0), sp)
     torch.cuda.synchronize(dev)
     R.barrier()
     t1 = time.perf_counter()
@@ -179,7 +179,7 @@ def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool
     open_ms = float(np.mean([bb.elapsed_time(c) for _, bb, c in ev]))
 
     res = {"records": b.n, "payload_bytes": b.payload_bytes, "wall_s": wall, "seal_ms": seal_ms, "open_ms": open_ms,
-           "shard": [begin, end], "clock": shader_clock(clk.cpu().numpy(), wall)}
+           "shard": [begin, end], "clock": shader_clock(clk.cpu().numpy())}
     res["sclk_mhz"] = res["clock"]["sclk_mhz"]
     lens = b.seal["len"]
     res["seal_alg_bytes"] = algorithmic_bytes(lens, b.seal["aad_len"], True)
@@ -201,18 +201,17 @@ def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool
     return res
 
 
-def shader_clock(c, wall_s: float) -> dict:
-    """XCD 0's average shader clock over a timed leg from two clock probes enqueued at its start and end
-    (ptls_mi355x_debug_clock_sample: s_memtime counts shader-clock cycles): cycles / the host's wall time of the leg
-    (the probes bracket it in stream order; launch latency is microseconds of a leg of ~0.1-1 s). Also the raw counts and
-    the real-time counter's rate implied by the same interval, beside the rate the runtime reports."""
+def shader_clock(c) -> dict:
+    """The shader clock right after a timed leg's first and last kernels (ptls_mi355x_debug_clock_sample: s_memtime
+    cycles over a ~20 us spin of one wave, against the real-time counter at the rate the runtime reports), so that
+    box-to-box spread in the line can be attributed; sclk_mhz is the mean of the two samples."""
     import picotls_amd as pa
 
-    dt, drt = int(c[4]) - int(c[0]), int(c[5]) - int(c[1])
-    same_xcd = int(c[2]) == int(c[6])
-    return {"sclk_mhz": round(dt / wall_s / 1e6, 1) if dt > 0 and wall_s > 0 and same_xcd else None, "cycles": dt,
-            "rtc_ticks": drt, "rtc_khz_measured": round(drt / wall_s / 1e3, 1) if wall_s > 0 else None,
-            "rtc_khz_reported": pa.debug_wallclock_khz(), "xcd": int(c[2]), "same_xcd": same_xcd}
+    khz = pa.debug_wallclock_khz()
+    mhz = [round(int(c[i]) / (int(c[i + 1]) / (khz * 1e3)) / 1e6, 1) if khz > 0 and int(c[i + 1]) > 0 else None for i in (0, 4)]
+    ok = [m for m in mhz if m is not None]
+    return {"sclk_mhz": round(sum(ok) / len(ok), 1) if ok else None, "after_first_step_mhz": mhz[0],
+            "after_last_step_mhz": mhz[1], "xcd": [int(c[2]), int(c[6])], "rtc_khz": khz}
 
 
 def zero_slot_padding(arena, recs, dev):

@@ -31,10 +31,10 @@ int ptls_mi355x_debug_counters(uint64_t *out, int reset);
 int ptls_mi355x_debug_inject_error(void);
 
 /**
- * Launches one wave on `stream` (a hipStream_t; workgroup 0 runs on XCD 0) that writes three 64-bit words to the
- * device-accessible `out`: the shader-clock counter (s_memtime), the real-time counter (s_memrealtime, rate
- * ptls_mi355x_debug_wallclock_khz) and the XCD it ran on. Two samples around a timed region give XCD 0's average
- * shader clock over it. Returns 0 or -1.
+ * Launches one wave on `stream` (a hipStream_t) that measures the shader clock of the CU it runs on over ~20 us: writes
+ * three 64-bit words to the device-accessible `out`: shader-clock cycles (s_memtime) and real-time counter ticks
+ * (s_memrealtime, rate ptls_mi355x_debug_wallclock_khz) elapsed over the same spin, and the XCD it ran on. Launched right
+ * after a timed leg's last kernel, on its stream, it reads the clock the chip held under that load. Returns 0 or -1.
  */
 int ptls_mi355x_debug_clock_sample(void *out, void *stream);
 /* the real-time counter's rate in kHz (hipDeviceAttributeWallClockRate of the current device), 0 if unknown */

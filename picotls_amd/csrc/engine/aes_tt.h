@@ -8,7 +8,11 @@
 // LDS byte address of Te0[byte r of w] in this lane's bank: byte0 = bank*4 (from laneoff), byte1 = byte r of w, byte2 =
 // laneoff's byte 2: the table's 64 KiB slot (0 in most kernels; 1 in the W8 kernels, whose 8-bit GHASH table takes
 // [0, 64K), W8_SWAP), at no cost -- the same single v_perm
+#if CT_PROBE_CONST  // (diagnosis build only, tools/gpu_r5.sh ct6: every lookup of entry 0; outputs are garbage)
+#define TE_ADDR(w, r, laneoff) __builtin_amdgcn_perm(0u, (laneoff), 0x0c020000u | ((4u + (r)) << 8))
+#else
 #define TE_ADDR(w, r, laneoff) __builtin_amdgcn_perm((w), (laneoff), 0x0c020000u | ((4u + (r)) << 8))
+#endif
 
 // LDS is addressed absolutely: the kernels declare no static __shared__ data, so their dynamic region starts at LDS
 // address 0 (checked at kernel entry by check_lds_base) and a v_perm result is directly a ds_read address; going

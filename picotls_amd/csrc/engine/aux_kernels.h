@@ -368,19 +368,24 @@ __global__ __launch_bounds__(256) void tls12_check_kernel(const ptls_mi355x_reco
     }
 }
 
-// Measurement (ptls_mi355x_debug_clock_sample): one wave of one workgroup -- workgroup 0 of a launch is dispatched to
-// XCD 0 -- reads the shader-clock counter (s_memtime) and the constant-rate real-time counter (s_memrealtime) and the
-// XCD it ran on. Two samples around a timed region give that XCD's average shader clock over it.
+// Measurement (ptls_mi355x_debug_clock_sample): one wave reads the shader-clock counter (s_memtime) and the constant-rate
+// real-time counter (s_memrealtime) twice, SPIN_TICKS real-time ticks apart (20 us at 100 MHz), on the same CU, and
+// writes both differences and the XCD: the shader clock of that XCD right then (s_memtime counters of different CUs or
+// launches are not comparable: round 5 measured nonsense across launches). A bounded spin: at most 2^22 reads.
+#define CLOCK_SPIN_TICKS 2000u
 __global__ __launch_bounds__(64) void clock_probe_kernel(unsigned long long *out)
 {
     if (threadIdx.x != 0)
         return;
-    unsigned long long t, rt;
+    unsigned long long t0, r0, t1, r1;
     u32 xcc;
     asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_getreg_b32 %2, hwreg(HW_REG_XCC_ID)\n\ts_waitcnt lgkmcnt(0)"
-                 : "=s"(t), "=s"(rt), "=s"(xcc)::"memory");
-    out[0] = t;
-    out[1] = rt;
+                 : "=s"(t0), "=s"(r0), "=s"(xcc)::"memory");
+    t1 = t0, r1 = r0;
+    for (u32 k = 0; k < (1u << 22) && r1 - r0 < CLOCK_SPIN_TICKS; ++k)
+        asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1), "=s"(r1)::"memory");
+    out[0] = t1 - t0;
+    out[1] = r1 - r0;
     out[2] = xcc;
 }
 

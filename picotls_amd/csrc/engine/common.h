@@ -66,6 +66,14 @@ __device__ __forceinline__ u32 lane_here()
     return x;
 }
 
+// CT_PROBE_CONST=1 (a diagnosis build only, never shipped): every LDS lookup whose address comes from data (AES T-table
+// bytes, GHASH operand bytes and nibbles) takes a constant operand instead, so the kernels' remaining LDS accesses are
+// exactly those whose addresses come from lengths, indices and the work queue; its bank-conflict count against the
+// product build's bounds what the data-dependent sites contribute (tools/gpu_r5.sh ct6)
+#ifndef CT_PROBE_CONST
+#define CT_PROBE_CONST 0
+#endif
+
 #ifndef ENGINE_FAST_STEP
 #define ENGINE_FAST_STEP 1         // wave-uniform fast path for steps where every lane holds a full text block
 #endif

@@ -136,8 +136,10 @@ __device__ __forceinline__ u32x4 gmul8(const lds_u8 *, u32x4 t, u32 lane, W8Lane
         // the bytes by bits 0-1 in one v_perm of the pair (psel picks from the other dword when bit 2 is set)
         const bool s2 = (lane & 8) != 0;
         const u32 a0 = s2 ? t[2] : t[0], a1 = s2 ? t[3] : t[1], a2 = s2 ? t[0] : t[2], a3 = s2 ? t[1] : t[3];
-        const u32 p[4] = {__builtin_amdgcn_perm(a1, a0, w.psel), __builtin_amdgcn_perm(a0, a1, w.psel),
-                          __builtin_amdgcn_perm(a3, a2, w.psel), __builtin_amdgcn_perm(a2, a3, w.psel)};
+        u32 p[4] = {__builtin_amdgcn_perm(a1, a0, w.psel), __builtin_amdgcn_perm(a0, a1, w.psel),
+                    __builtin_amdgcn_perm(a3, a2, w.psel), __builtin_amdgcn_perm(a2, a3, w.psel)};
+        if (CT_PROBE_CONST)
+            p[0] = p[1] = p[2] = p[3] = 0;
         u32x4 acc = {0, 0, 0, 0};
 #pragma unroll
         for (u32 i = 0; i < 16; i += 2) {
@@ -351,7 +353,7 @@ __device__ __forceinline__ u32x4 group_ws_terms(u32 ga, const GroupWs &k, u32x4 
     u32x4 e[4];
 #pragma unroll
     for (u32 i = 0; i < 4; ++i)  // (v_bfe_u32 + v_lshl_add_u32: a table base need only be a multiple of 256)
-        e[i] = lds_load128((__builtin_amdgcn_ubfe(ga, k.sh[i], 4u) << 8) + k.Wi[i]);
+        e[i] = lds_load128((CT_PROBE_CONST ? 0u : __builtin_amdgcn_ubfe(ga, k.sh[i], 4u) << 8) + k.Wi[i]);
     u32x4 t;
 #pragma unroll
     for (int c = 0; c < 4; ++c)

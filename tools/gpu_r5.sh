@@ -60,6 +60,26 @@ firstcall2)
   echo "processes with a difference: $nf of $((2 * ${1:-16}))"
   exit 0
   ;;
+ct6)
+  # (round 5) LDS bank conflicts of the many-key mixed kernel per dispatch (rocprofv3 --pmc
+  # SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS, one process per case, 2 seals + 2 opens): the product build over 4 keys x 3
+  # payloads and a length-permuted batch; the CT_PROBE_CONST diagnosis build (tools/gv/ctconst: every data-derived LDS
+  # address replaced by a constant) on the same batch
+  (
+R=$GRAFT_REPO_ROOT; cd /tmp && export TMPDIR=/tmp
+run() {  # name, extra args
+  timeout -k 10 240 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS --output-format csv -d $R/gpurun_out/ct6/$1 -o p -- python3 $R/tools/ct_probe.py --workload mixed --records 4194304 --reps 2 ${@:2} > $R/gpurun_out/ct6_$1.log 2>&1
+  rc=$?; echo "$1 rc=$rc"; [ $rc -ne 0 ] && { tail -5 $R/gpurun_out/ct6_$1.log; exit $rc; }
+}
+for k in 1 2 3 4; do for pl in zero random ones; do run k${k}_$pl --key-seed $k --payload $pl; done; done
+run k1_random_permuted --key-seed 1 --payload random --permute 7
+run ctconst_k1_random --key-seed 1 --payload random --lib $R/tools/gv/ctconst/libptls_mi355x.so --no-check
+run ctconst_k2_zero --key-seed 2 --payload zero --lib $R/tools/gv/ctconst/libptls_mi355x.so --no-check
+cd $R
+python3 tools/ct_summary.py gpurun_out/ct6 > gpurun_out/ct6_mixed.txt; cat gpurun_out/ct6_mixed.txt
+exit 0
+  )
+  ;;
 ab)
   # interleaved A/B (tools/ab.py, one process per workload) of tools/gv/<name> engines at the full BASELINE sizes:
   #   bash tools/gpu_r5.sh ab "base scat" [tag] [workloads...]
