@@ -456,7 +456,7 @@ def release_staging() -> None:
 # ------------------------------------------------------------------------------------------------ debug hooks
 
 
-COUNTER_NAMES = ("chunked", "spread", "seal_hp", "w8_tree", "w8_serial", "lockstep", "span", "_")
+COUNTER_NAMES = ("chunked", "spread", "seal_hp", "w8_tree", "w8_serial", "lockstep", "span", "w8_g4")
 
 
 def debug_counters(reset: bool = False) -> dict:
@@ -465,7 +465,9 @@ def debug_counters(reset: bool = False) -> dict:
     out = (ctypes.c_uint64 * 16)()
     if load_library().ptls_mi355x_debug_counters(ctypes.cast(out, ctypes.c_void_p), 1 if reset else 0) != 0:
         raise _err("ptls_mi355x_debug_counters")
-    return {"launches": dict(zip(COUNTER_NAMES, out[:8])), "runs": dict(zip(COUNTER_NAMES[:5], out[8:13]))}
+    runs = dict(zip(COUNTER_NAMES[:5], out[8:13]))
+    runs["w8_g4"] = out[15]  # (of the w8_serial runs: whole runs in 4-lane groups)
+    return {"launches": dict(zip(COUNTER_NAMES[:7], out[:7])), "runs": runs}
 
 
 def debug_inject_error() -> int:

@@ -177,6 +177,16 @@ __device__ __forceinline__ u32 lane_here()
 // loop, and the AES addresses take their 64 KiB slot from laneoff's byte 2 in the same v_perm (aes_tt.h TE_ADDR)
 #define W8_SWAP 1
 #endif
+// (round 5) the W8 kernels' unframed steps outside the steady range as one pass with the non-text inputs loaded ahead of
+// the AES (segment.h); 0 keeps the per-case setup_step / finish_step
+// (round 5) whole runs of the W8 serial kernel (EXT 4: uniform records under W8_MIN_STEPS steps) in 4-lane groups
+// (ghash.h, gcm_chunked_kernel); 0 keeps 8-lane groups
+#ifndef W8_G4
+#define W8_G4 1
+#endif
+#ifndef W8_LEAN_STEP
+#define W8_LEAN_STEP 1
+#endif
 #define W8_H8_BASE (W8_SWAP ? 0u : (u32)LDS_AES_BYTES)   // the W8 kernels' 8-bit H^8 table
 #define W8_AES_BASE (W8_SWAP ? (u32)LDS_AES_BYTES : 0u)  // ... and their AES T-tables
 #define W8_RUN_UNITS 512  // units per run of a launch pair (both kernels: their runs must be the same)
@@ -238,31 +248,69 @@ __device__ __forceinline__ u32 wave_max(u32 v)
     return (u32)__builtin_amdgcn_readlane((int)dpp_scan(v, 0u, [](u32 a, u32 b) { return max(a, b); }), 63);
 }
 
-// maximum over the wave of a value that is uniform within each 8-lane group
+// maximum / signed maximum / signed minimum over the wave of a value that is uniform within each 8-lane group: the two
+// groups of a 16-lane row meet through one DPP row rotation by 8, then four reads (one per row) instead of eight
+__device__ __forceinline__ u32 row_ror8(u32 v)
+{
+    return (u32)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
+}
 __device__ __forceinline__ u32 wave_max_per8(u32 v)
 {
-    u32 m = (u32)__builtin_amdgcn_readlane((int)v, 0);
-#pragma unroll
-    for (int g = 1; g < 8; ++g)
-        m = max(m, (u32)__builtin_amdgcn_readlane((int)v, 8 * g));
-    return m;
+    const u32 r = max(v, row_ror8(v));
+    return max(max((u32)__builtin_amdgcn_readlane((int)r, 0), (u32)__builtin_amdgcn_readlane((int)r, 16)),
+               max((u32)__builtin_amdgcn_readlane((int)r, 32), (u32)__builtin_amdgcn_readlane((int)r, 48)));
 }
-// signed maximum / minimum over the wave of a value that is uniform within each 8-lane group
 __device__ __forceinline__ int wave_smax_per8(int v)
 {
-    int m = __builtin_amdgcn_readlane(v, 0);
-#pragma unroll
-    for (int g = 1; g < 8; ++g)
-        m = max(m, __builtin_amdgcn_readlane(v, 8 * g));
-    return m;
+    const int r = max(v, (int)row_ror8((u32)v));
+    return max(max(__builtin_amdgcn_readlane(r, 0), __builtin_amdgcn_readlane(r, 16)),
+               max(__builtin_amdgcn_readlane(r, 32), __builtin_amdgcn_readlane(r, 48)));
 }
 __device__ __forceinline__ int wave_smin_per8(int v)
 {
-    int m = __builtin_amdgcn_readlane(v, 0);
-#pragma unroll
-    for (int g = 1; g < 8; ++g)
-        m = min(m, __builtin_amdgcn_readlane(v, 8 * g));
-    return m;
+    const int r = min(v, (int)row_ror8((u32)v));
+    return min(min(__builtin_amdgcn_readlane(r, 0), __builtin_amdgcn_readlane(r, 16)),
+               min(__builtin_amdgcn_readlane(r, 32), __builtin_amdgcn_readlane(r, 48)));
+}
+// the same over groups of G lanes (G = 8 above; G = 4: the 4-lane groups of a row meet through rotations by 4 and 8)
+template <int G>
+__device__ __forceinline__ u32 row_group_reduce_rot(u32 v, bool is_max, bool is_signed)
+{
+    auto op = [&](u32 a, u32 b) -> u32 {
+        if (is_signed)
+            return (u32)(is_max ? max((int)a, (int)b) : min((int)a, (int)b));
+        return is_max ? max(a, b) : min(a, b);
+    };
+    if constexpr (G == 4)
+        v = op(v, (u32)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x124, 0xf, 0xf, false));  // row_ror:4
+    return op(v, row_ror8(v));
+}
+template <int G>
+__device__ __forceinline__ u32 wave_max_perg(u32 v)
+{
+    if constexpr (G == 8)
+        return wave_max_per8(v);
+    const u32 r = row_group_reduce_rot<G>(v, true, false);
+    return max(max((u32)__builtin_amdgcn_readlane((int)r, 0), (u32)__builtin_amdgcn_readlane((int)r, 16)),
+               max((u32)__builtin_amdgcn_readlane((int)r, 32), (u32)__builtin_amdgcn_readlane((int)r, 48)));
+}
+template <int G>
+__device__ __forceinline__ int wave_smax_perg(int v)
+{
+    if constexpr (G == 8)
+        return wave_smax_per8(v);
+    const int r = (int)row_group_reduce_rot<G>((u32)v, true, true);
+    return max(max(__builtin_amdgcn_readlane(r, 0), __builtin_amdgcn_readlane(r, 16)),
+               max(__builtin_amdgcn_readlane(r, 32), __builtin_amdgcn_readlane(r, 48)));
+}
+template <int G>
+__device__ __forceinline__ int wave_smin_perg(int v)
+{
+    if constexpr (G == 8)
+        return wave_smin_per8(v);
+    const int r = (int)row_group_reduce_rot<G>((u32)v, false, true);
+    return min(min(__builtin_amdgcn_readlane(r, 0), __builtin_amdgcn_readlane(r, 16)),
+               min(__builtin_amdgcn_readlane(r, 32), __builtin_amdgcn_readlane(r, 48)));
 }
 
 typedef __attribute__((address_space(3))) uint8_t lds_u8;

@@ -732,12 +732,12 @@ __device__ __noinline__ u32x4 ct_combine_tree(const lds_u8 *lds, const lds_u32x4
 // (a cut run: usrc = the key element of its unit combine power) that power window-major at W8_TAB_COMB; then the 8-bit
 // table. Out of line: inlined into the run loop it cost the kernel's other runs registers (-4 % on 1200-byte records).
 // tree (the EXT 3 kernel: long whole records): H and H^2 nibble-major at W8_TAB_H and W8_TAB_COMB instead (w8_tree_end).
-__device__ __noinline__ void w8_build_tables(lds_u8 *lds, const lds_u8 *keyp, u32 usrc, bool tree)
+__device__ __noinline__ void w8_build_tables(lds_u8 *lds, const lds_u8 *keyp, u32 usrc, bool tree, u32 hpow)
 {
     typedef __attribute__((address_space(3))) const KeyEntry lds_key_t;
     lds_key_t *key = (lds_key_t *)keyp;
     auto el = [&](u32 i) { return u32x4{key->h[i][0], key->h[i][1], key->h[i][2], key->h[i][3]}; };
-    build_elem_table(lds, CLDS_PART, el(7), 0, false);
+    build_elem_table(lds, CLDS_PART, el(hpow), 0, false);  // (the Horner power: H^8, or H^4 for 4-lane groups)
     build_elem_table(lds, W8_TAB_H, el(0), 64, !tree);
     if (tree)
         build_elem_table(lds, W8_TAB_COMB, el(1), 128, false);
@@ -921,11 +921,14 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         lds_key_t *key = (lds_key_t *)(rs + RUN_KEY_OFF);  // staged by the scanner
         // the EXT 3 kernel's runs (all W8: the others were skipped above) take the 8-bit Horner table (ghash.h)
         constexpr bool w8run = W8K;
-        const u32 w8mode = !w8run ? 0u : W8TREE ? 2u : 1u;  // W8 segment ends: the serial chain (1) or the tree (2)
+        // W8 segment ends: the serial chain (1), the tree (2), or a whole run of the serial kernel in 4-lane groups (3:
+        // Horner with H^4)
+        const bool g4run = W8K && !W8TREE && W8_G4 && whole;
+        const u32 w8mode = !w8run ? 0u : W8TREE ? 2u : g4run ? 3u : 1u;
         if (w8run && (key_idx != loaded_key || loaded_w8 != w8mode)) {
-            // the 8-bit H^8 table over slots 0..7, H in slot 8, and a cut run's combine power (or the tree's H^2) at
-            // W8_TAB_COMB
-            w8_build_tables(lds, (const lds_u8 *)key, whole ? 0xffffffffu : usrc, w8mode == 2);
+            // the 8-bit H^8 (H^4) table over slots 0..7, H in slot 8, and a cut run's combine power (or the tree's H^2)
+            // at W8_TAB_COMB
+            w8_build_tables(lds, (const lds_u8 *)key, whole ? 0xffffffffu : usrc, w8mode == 2, w8mode == 3 ? 3u : 7u);
             loaded_key = key_idx;
             loaded_usrc = whole ? 0xffffffffu : usrc;
             loaded_w8 = w8mode;
@@ -988,6 +991,50 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 k_back = f - (first - lo);
             }
         };
+        bool g4done = false;
+        if constexpr (W8K && !W8TREE && W8_G4) {
+            if (g4run) {
+                // (round 5) a whole run of the serial W8 kernel: 16 records a wave in 4-lane groups (ghash.h), each a
+                // record's whole stream in 64-byte aligned steps; no partials, no combine
+                constexpr u32 G4 = 4, RPW4 = 64 / G4;
+                if (threadIdx.x == 0)  // (ptls_mi355x_debug_counters: runs in 4-lane groups)
+                    atomicAdd(&g_ext_runs[blockIdx.x % EXT_RUN_ROWS][7], 1ull);
+                for (;;) {
+                    u32 ub = 0;
+                    if (lane_here() == 0)
+                        ub = atomicAdd((u32 *)&rs[RC_NEXT], RPW4);
+                    ub = __builtin_amdgcn_readfirstlane(ub);
+                    if (ub >= total_units)
+                        break;
+                    u32x4 acc;
+                    u32 okw;
+                    {
+                        const u32 lane = lane_here(), j = lane % G4, u = ub + lane / G4;
+                        const u32 laneoff = (lane & 31) * 4 | W8_AES_BASE;
+                        const bool valid = u < total_units;
+                        ptls_mi355x_record_t r = {};
+                        if (valid)
+                            r = recs[pos + u];
+                        const bool live = valid && record_ok<FRAME>(args, r);
+                        if (valid && !live) {  // rejected descriptor: nothing is written
+                            r.len = 0, r.aad_len = 0, r.flags = 0;
+                            if (OPEN && j == 0)
+                                args.ok[ok_at(pos + u)] = 0;
+                        }
+                        const u32 ekslot = CLDS_PART + 16u * (threadIdx.x / G4);
+                        gcm_segment<NR, OPEN, 1, FRAME, CT, true, (int)G4>(args, lds, rk, iv0, iv1, iv2, r, live, 0u,
+                                                                         live ? 1u : 0u, j, laneoff, tsel_horner, acc,
+                                                                         true, okw, true, ekslot, false);
+                    }
+                    asm volatile("" ::: "memory");
+                    const u32 u = ub + lane_here() / G4;
+                    if (OPEN && okw <= 1 && u < total_units)  // a record's tag check (its length lane)
+                        args.ok[ok_at(pos + u)] = (uint8_t)okw;
+                }
+                g4done = true;
+            }
+        }
+        if (!g4done)
         for (;;) {
             u32 ub = 0;
             if (lane_here() == 0)

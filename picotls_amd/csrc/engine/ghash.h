@@ -119,8 +119,10 @@ struct W8Lane {
 __device__ __forceinline__ W8Lane w8_lane(u32 lane)
 {
     const u32 l = lane & 15, lb = l & 3;
+    // (x * 0x01010101 for a byte x as a v_perm broadcast of byte 0: v_mul_lo_u32 issues at a quarter of the rate)
+    auto bcast = [](u32 x) { return __builtin_amdgcn_perm(0u, x, 0u); };
     if constexpr (W8_SWAP)  // byte t of L_0: (t ^ l) << 4 (l < 16: no carries between bytes)
-        return W8Lane{((l * 0x01010101u) ^ 0x03020100u) << 4, (lb * 0x01010101u ^ 0x03020100u) | ((l & 4) * 0x01010101u)};
+        return W8Lane{(bcast(l) ^ 0x03020100u) << 4, (bcast(lb) ^ 0x03020100u) | bcast(l & 4)};
     return W8Lane{(l << 4) | (l << 12) | ((u32)(LDS_AES_BYTES >> 16) << 16), lb * 0x01010101u ^ 0x03020100u};
 }
 __device__ __forceinline__ u32x4 gmul8(const lds_u8 *, u32x4 t, u32 lane, W8Lane w)
@@ -409,6 +411,82 @@ __device__ __forceinline__ u32x4 w8_lane_end(const lds_u8 *lds, u32x4 v, u32 lan
         g = gmul_group_w_add(lds, g, W8_TAB_H, lane, rank == r ? v : z);
     return gmul_group_w(lds, g, W8_TAB_H, lane);
 #endif
+}
+
+// ------------------------------------------------------------------------------------------------ GHASH (4-lane groups)
+//
+// (round 5) Whole runs of short records in the W8 serial kernel (EXT 4) give each record a group of 4 lanes
+// (gcm_segment<..., 4>): a wave then carries 16 records instead of 8, so every per-record instruction (the descriptor and
+// segment setup, the first and last steps, the segment end) serves twice as many records, and the segment end is a chain
+// of 4 group products instead of 8. The Horner step multiplies by H^4 (the 8-bit table built from H^4). Lane y = lane & 3
+// of a group holds dword y of a scattered value and looks up the 8 windows 8y..8y+7 of the window-major table (layout
+// above: window w at bit 16 ((w >> 2) & 1) + 4 ((w & 3) ^ 1) of dword w >> 3, i.e. window 8y + t at bit 4 (t ^ 1) of
+// dword y), window 8y + (i ^ f) at its i-th lookup with f = (lane >> 1) & 7. The 16 lanes of a ds_read_b128 phase, 4 (g)
+// groups x 4 (y) lanes, have distinct (y & 1, f = 2g + (y >> 1)), so they read the bank groups 8 (y & 1) + (i ^ f)
+// once each: conflict-free for any data, as gmul_group_w.
+struct Group4Ws {
+    u32 Wi[8];  // the lane's address base for lookup i (the window's column and bank group)
+    u32 sh[8];  // the bit offset of the lane's nibble for lookup i in its dword: 4 ((i ^ f) ^ 1)
+};
+__device__ __forceinline__ Group4Ws group4_ws(u32 tsel, u32 lane)
+{
+    Group4Ws k;
+    const u32 y = lane & 3, f = (lane >> 1) & 7;
+    const u32 B = tsel + (y >> 1) * 4096u + (y & 1) * 128u + f * 16u;  // (tsel a multiple of 256: bits 4-6 are f)
+#pragma unroll
+    for (u32 i = 0; i < 8; ++i) {
+        k.Wi[i] = B ^ (i << 4);
+        k.sh[i] = 4u * ((i ^ f) ^ 1u);
+        asm volatile("" : "+v"(k.Wi[i]), "+v"(k.sh[i]));  // (computed once per segment end)
+    }
+    return k;
+}
+// the 8 table entries of the lane's windows of a (ga: the lane's dword of a), folded with x
+__device__ __forceinline__ u32x4 group4_ws_terms(u32 ga, const Group4Ws &k, u32x4 x)
+{
+    u32x4 t = x;
+#pragma unroll
+    for (u32 i = 0; i < 8; i += 2) {
+        const u32x4 e0 = lds_load128((__builtin_amdgcn_ubfe(ga, k.sh[i], 4u) << 8) + k.Wi[i]);
+        const u32x4 e1 = lds_load128((__builtin_amdgcn_ubfe(ga, k.sh[i + 1], 4u) << 8) + k.Wi[i + 1]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            t[c] = xor3(t[c], e0[c], e1[c]);
+    }
+    return t;
+}
+// Reduce-scatter of t over the 4 lanes of a group (a quad): dword y of the XOR in lane y. Lane y ^ 2 (quad_perm
+// [2,3,0,1]) takes the dword pair this lane does not keep, then lane y ^ 1 (quad_perm [1,0,3,2]) the other dword.
+__device__ __forceinline__ u32 group4_scatter(u32x4 t, u32 lane)
+{
+    const bool b = (lane & 2) != 0, c = (lane & 1) != 0;
+    const u32 k0 = b ? t[2] : t[0], k1 = b ? t[3] : t[1], s0 = b ? t[0] : t[2], s1 = b ? t[1] : t[3];
+    const u32 m0 = k0 ^ (u32)__builtin_amdgcn_update_dpp(0, (int)s0, 0x4E, 0xF, 0xF, false);
+    const u32 m1 = k1 ^ (u32)__builtin_amdgcn_update_dpp(0, (int)s1, 0x4E, 0xF, 0xF, false);
+    const u32 kk = c ? m1 : m0, ss = c ? m0 : m1;
+    return kk ^ (u32)__builtin_amdgcn_update_dpp(0, (int)ss, 0xB1, 0xF, 0xF, false);
+}
+// XOR over the 4 lanes of a group, the whole value in every lane
+__device__ __forceinline__ u32x4 group4_allreduce(u32x4 t)
+{
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        t[c] ^= (u32)__builtin_amdgcn_update_dpp(0, (int)t[c], 0x4E, 0xF, 0xF, false);
+        t[c] ^= (u32)__builtin_amdgcn_update_dpp(0, (int)t[c], 0xB1, 0xF, 0xF, false);
+    }
+    return t;
+}
+// The W8 segment end of a 4-lane group: sum_j a_j H^(4 - rank_j) = ((v_0 H + v_1) H + v_2) H + v_3) H over the ranks, a
+// scattered chain of four group products with the window-major H table (32 lookups per product, 8 per lane)
+__device__ __forceinline__ u32x4 w8_lane_end4(const lds_u8 *, u32x4 v, u32 lane, u32 rank)
+{
+    const u32x4 z = {0, 0, 0, 0};
+    const Group4Ws k = group4_ws(W8_TAB_H, lane);
+    u32 g = group4_scatter(rank == 0 ? v : z, lane);
+#pragma unroll
+    for (u32 r = 1; r < 4; ++r)
+        g = group4_scatter(group4_ws_terms(g, k, rank == r ? v : z), lane);
+    return group4_allreduce(group4_ws_terms(g, k, z));
 }
 
 // The W8 segment end of a long whole record (at least W8_MIN_STEPS steps, the EXT 3 kernel): the same sum by a butterfly over the

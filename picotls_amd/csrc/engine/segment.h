@@ -33,13 +33,17 @@
 // (ekslot) until the tree is done, and is added on the length lane only (lane jl: the lane the tag or the unit partial
 // is taken from). The round-2 form (CT_TREE 0) ran four multiplies, H^8, H^4, H^2, H^1 kept on the bits of e, in every
 // step in which some lane of the wave was at its last position (two or more steps per segment).
-template <int NR, bool OPEN, int NB, int FRAME = 0, bool CT = false, bool W8 = false>
+template <int NR, bool OPEN, int NB, int FRAME = 0, bool CT = false, bool W8 = false, int GG = ENGINE_G>
 __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 *lds, const u32 (&rk)[NR + 1][4], u32 iv0,
                                             u32 iv1, u32 iv2, const ptls_mi355x_record_t &r, bool valid, u32 m_lo,
                                             u32 m_hi, u32 j, u32 laneoff, u32 tsel_horner, u32x4 &acc, bool finish,
                                             u32 &okw, bool aligned, u32 ekslot = 0, bool w8tree = false)
 {
-    constexpr int G = ENGINE_G;
+    // G lanes per record: ENGINE_G, or 4 in the W8 serial kernel's whole runs (ghash.h, 4-lane groups), whose aligned
+    // streams then put text blocks on 64-byte boundaries (a group stores 64 bytes a step)
+    constexpr int G = GG;
+    static_assert(G == 8 || (G == 4 && W8), "8-lane groups, or 4-lane groups in the W8 kernels");
+    constexpr int GS = G == 8 ? 3 : 2;  // log2 G
     // W8 (a W8 run of the pair's EXT 3 kernel, gcm_chunked_kernel): Horner on the 8-bit H^8 table (gmul8), the lanes'
     // last powers by a serial Horner over the group's ranks with the window-major H table (W8_TAB_H, w8_lane_end)
     constexpr bool COOP = SEG_COOP && !W8;  // the conflict-free segment end (coop_last_powers), both modes
@@ -75,15 +79,14 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     // this lane's last step in the segment and its power there: at the record's end H^(N - p) for its last position p,
     // at a unit's end (a step boundary) H^(G - j)
     const bool at_end = aligned;
-    const int m_last = !valid ? -1 : at_end ? ((int)N - 1 - (int)j) >> 3 : (int)m_hi - 1;
-    const u32 e_last = at_end ? N - (8u * (u32)m_last + j) : (u32)G - j;  // 1..G
+    const int m_last = !valid ? -1 : at_end ? ((int)N - 1 - (int)j) >> GS : (int)m_hi - 1;
+    const u32 e_last = at_end ? N - ((u32)G * (u32)m_last + j) : (u32)G - j;  // 1..G
     const u32 tsel_last = 0x10000u + (e_last - 1) * GHASH_TABLE_BYTES;
     // the first step in which some lane of the group is at its last position (the steady range ends before it)
-    const int m_first_last = at_end ? ((int)N - G) >> 3 : (int)m_hi - 1;
+    const int m_first_last = at_end ? ((int)N - G) >> GS : (int)m_hi - 1;
     const u32 jl = (N - 1) & (G - 1);  // the length block's lane
-    static_assert(G == 8, "m_last uses a shift by 3");
 
-    const u32 Smax = wave_max_per8(m_hi - m_lo);  // m_lo, m_hi are uniform within a group
+    const u32 Smax = wave_max_perg<G>(m_hi - m_lo);  // m_lo, m_hi are uniform within a group
 
     // nonce = iv ^ (0^32 || BE64(seq)) (lib/picotls.c:6587-6601); TLS 1.2 takes the explicit nonce of the record in
     // place of seq, read as stored (big endian), so its two words need no swap
@@ -229,8 +232,8 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     int sb = min(me - 1, m_first_last - 1) + 1 - (int)m_lo;
     if (!valid || m_hi <= m_lo)
         sa = 1, sb = 0;
-    sa = wave_smax_per8(sa);
-    sb = wave_smin_per8(sb);
+    sa = wave_smax_perg<G>(sa);
+    sb = wave_smin_perg<G>(sb);
 
     for (u32 s0 = 0; s0 < Smax; ++s0) {
         if ((int)s0 == sa && sb > sa) {
@@ -260,6 +263,76 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             }
             s0 = (u32)sb;
         }
+#if W8_LEAN_STEP
+        if constexpr (W8 && FRAME == 0) {
+            // (round 5) the W8 kernels' steps outside the steady range, unframed: every input that is not a full text
+            // block (the AAD block, the record's partial last text block) is loaded before the AES, where its latency
+            // hides, and the output cases are one chain of exec-masked branches instead of the per-case dispatch
+            const u32 m0 = m_lo + s0;
+            const bool act = m0 < m_hi;
+            const int logical = (int)(j + G * m0) - P;
+            const int b = logical - (int)na;
+            const bool is_data = act && logical >= (int)na && b < (int)nb;
+            const bool is_aad = act && logical >= 0 && logical < (int)na;
+            const bool is_len = act && logical == (int)(na + nb);
+            const u32 rem = L - 16u * (u32)b;  // (data positions)
+            const bool full = is_data && rem >= 16;
+            u32x4 xin = nxt[0];
+            int bn;
+            if (full_block(m0 + 1, bn))
+                nxt[0] = *(const u32x4_u *)(src + 16u * (u32)bn);
+            if (is_aad) {
+                const u32 arem = A - 16u * (u32)logical;
+                const uint8_t *ap = aadp + 16u * (u32)logical;
+                xin = arem >= 16 ? *(const u32x4_u *)ap : load_partial(ap, arem);
+            } else if (is_data && !full) {
+                xin = load_partial(src + 16u * (u32)b, rem);
+            }
+            // AES-CTR input: data positions encrypt counter 2 + b, all others J0 (the length lane keeps E(K, J0))
+            const u32 ctr = is_data ? (u32)(b + 2) : 1u;
+            u32 st[1][4] = {{n0, n1, n2, bswap32(ctr) ^ rk[0][3]}};
+            if ((ctr >> 8) != cc1_key) {
+                cc1 = ctr_cache1_init<NR>(lds, laneoff, rk, n0, n1, n2, st[0][3]);
+                cc1_key = ctr >> 8;
+            }
+            aes_ctr_cached1<NR>(lds, laneoff, rk, cc1, st);
+            __builtin_amdgcn_sched_barrier(0);
+            const u32x4 ks = {st[0][0], st[0][1], st[0][2], st[0][3]};
+            u32x4 X = {0, 0, 0, 0};
+            if (full) {
+                const u32x4 o = xin ^ ks;
+                *(u32x4_u *)(dst + 16u * (u32)b) = o;
+                X = OPEN ? xin : o;
+            } else if (is_aad) {
+                X = xin;
+            } else if (is_data) {
+                const u32x4 o = mask_tail(xin ^ ks, rem);
+                store_partial(dst + 16u * (u32)b, o, rem);
+                X = OPEN ? xin : o;
+            } else if (is_len) {
+                u32 Ah = A, Lh = L;
+                asm volatile("" : "+v"(Ah), "+v"(Lh));
+                const u64 abits = (u64)Ah * 8, cbits = (u64)Lh * 8;
+                X = u32x4{bswap32((u32)(abits >> 32)), bswap32((u32)abits), bswap32((u32)(cbits >> 32)),
+                          bswap32((u32)cbits)};
+                *(lds_u32x4 *)(const_cast<lds_u8 *>(lds) + ekslot) = ks;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            // Horner with H^8 except at the lane's last position (its power comes in w8_lane_end); none in the wave's
+            // last step
+            const u32x4 t = acc ^ X;
+            u32x4 prod = t;
+            if (s0 + 1 < Smax) {
+                prod = gmul8(lds, t, lane_here(), w8);
+                if ((int)m0 == m_last)
+                    prod = t;
+            }
+            if ((int)m0 <= m_last)
+                acc = prod;
+            __builtin_amdgcn_sched_barrier(0);
+            continue;
+        }
+#endif
         const u32 m0 = m_lo + s0;
         u32 st[1][4];
         setup_step(m0, st);
@@ -316,14 +389,16 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         __builtin_amdgcn_sched_barrier(0);
     }
 
-    static_assert(G == 8, "dpp_xor8 reduces groups of 8 lanes");
+    static_assert(G == 8 || W8, "dpp_xor8 reduces groups of 8 lanes");
     if constexpr (W8) {
         // sum over the group of a_l H^(e_l) (rank r = 8 - e owes H^(8 - r)): ((v_0 H + v_1) H + ... + v_7) H by eight
         // group multiplies with the one window-major table H (4 conflict-free lookups per lane each: 32, as
         // coop_last_powers, with one table instead of seven)
         // (w8tree, the EXT 3 kernel's long whole records: the butterfly over the ranks with H and H^2 nibble-major)
         const u32 rank = valid ? (u32)G - e_last : j;
-        if (w8tree)
+        if constexpr (G == 4)
+            acc = w8_lane_end4(lds, acc, lane_here(), rank);
+        else if (w8tree)
             acc = w8_tree_end(lds, acc, lane_here(), rank);
         else
             acc = w8_lane_end(lds, acc, lane_here(), rank);

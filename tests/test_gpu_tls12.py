@@ -383,14 +383,17 @@ def _tls12_expect(ref, keys, ivs, key_size, recs, arena, i):
                      arena[p + 8:p + 8 + ln].tobytes()))
 
 
-@pytest.mark.parametrize("key_size,nkeys,n,long_runs", [(16, 3, 2600, False), (32, 1, 2100, False), (16, 1, 256 * 130, True)])
-def test_tls12_w8_kernels_vs_fusion(ref, key_size, nkeys, n, long_runs):
+@pytest.mark.parametrize("key_size,nkeys,n,uniform", [(16, 3, 2600, 0), (32, 1, 2100, 0), (16, 1, 256 * 130, 16384),
+                                                       (32, 2, 256 * 130, 1200), (16, 1, 256 * 130, 3001)])
+def test_tls12_w8_kernels_vs_fusion(ref, key_size, nkeys, n, uniform):
     """TLS 1.2 framing in the W8 kernels (batches of at least W8_MIN_RECS = 2048 records): random lengths (EXT 4's cut
-    runs), and 33,280 records of 16 KiB, 130 per workgroup (EXT 3's whole runs of long records). Every record (the long
-    batch: 400 sampled and the ends) equals lib/fusion.c's seal with the record-layer nonce and AAD, nothing outside the
-    wire records is written, and every record opens back to its payload."""
-    rng = np.random.default_rng(1200 + n + key_size)
-    lens = np.full(n, 16384) if long_runs else rng.integers(0, 16385, n)
+    runs), 33,280 records of 16 KiB, 130 per workgroup (EXT 3's whole runs of long records), and 33,280 records of 1200
+    or 3001 bytes (EXT 4's whole runs, in 4-lane groups since round 5). Every record (the uniform batches: 400 sampled
+    and the ends) equals lib/fusion.c's seal with the record-layer nonce and AAD, nothing outside the wire records is
+    written, and every record opens back to its payload."""
+    long_runs = uniform != 0
+    rng = np.random.default_rng(1200 + n + key_size + uniform)
+    lens = np.full(n, uniform) if long_runs else rng.integers(0, 16385, n)
     keys, ivs, recs, arena = _tls12_batch(rng, lens, nkeys, key_size)
     ks = pa.Keyset(keys, ivs, key_size)
     wire_len = int((lens + 29).sum())
@@ -406,18 +409,19 @@ def test_tls12_w8_kernels_vs_fusion(ref, key_size, nkeys, n, long_runs):
     precs["out_off"] = np.concatenate([[0], np.cumsum(lens)[:-1]])
     plain, ok, res = _open(ks, precs, out[:wire_len].tobytes(), int(lens.sum()))
     assert ok.all() and (res["status"] == pa.TLS_OK).all()
-    src = arena.reshape(n, 8 + 16384)[:, 8:].reshape(-1) if long_runs else np.concatenate(
+    src = arena.reshape(n, 8 + uniform)[:, 8:].reshape(-1) if long_runs else np.concatenate(
         [arena[int(recs["in_off"][i]) + 8:int(recs["in_off"][i]) + 8 + int(lens[i])] for i in range(n)])
     assert np.array_equal(plain[:int(lens.sum())], src)
     ks.free()
 
 
-def test_tls13_w8_tree_kernel_long_records_vs_fusion(ref):
-    """TLS 1.3 framing in the EXT 3 kernel: 33,280 records of 16 KiB (130 per workgroup: whole runs of long records) of
-    two connections; sampled records equal header || fusion's seal of payload || type under the header as AAD, and every
-    record opens back."""
-    rng = np.random.default_rng(1313)
-    n, nkeys, ln = 256 * 130, 2, 16384
+@pytest.mark.parametrize("ln", [16384, 1200, 37])
+def test_tls13_w8_whole_runs_vs_fusion(ref, ln):
+    """TLS 1.3 framing in the W8 kernels' whole runs: 33,280 records (130 per workgroup) of two connections, of 16 KiB
+    (EXT 3: long records) or 1200 / 37 bytes (EXT 4, in 4-lane groups since round 5); sampled records equal header ||
+    fusion's seal of payload || type under the header as AAD, and every record opens back."""
+    rng = np.random.default_rng(1313 + ln)
+    n, nkeys = 256 * 130, 2
     keys, ivs = rng.bytes(16 * nkeys), rng.bytes(12 * nkeys)
     data = np.frombuffer(rng.bytes(n * ln), np.uint8)
     recs = np.zeros(n, dtype=pa.RECORD_DTYPE)

@@ -194,6 +194,23 @@ def test_w8_pairs_on_many_streams_vs_fusion(ref):
     ks.free()
 
 
+@pytest.mark.parametrize("length,aad,key_size,nkeys", [
+    (1200, 13, 16, 1), (0, 13, 16, 1), (1, 0, 32, 1), (16, 16, 16, 2), (100, 17, 32, 3), (4095, 40, 16, 1),
+    (7800, 5, 32, 1), (1223, 70, 16, 4)])
+def test_w8_g4_whole_runs_vs_fusion(ref, length, aad, key_size, nkeys):
+    """Whole runs of short uniform records (under W8_MIN_STEPS steps: the EXT 4 kernel) in 4-lane groups (ghash.h,
+    round 5): 33,280 records (130 per workgroup at 256 CUs) of empty to 7800-byte records, AADs of 0 to 70 bytes
+    (several blocks), one to four keys; every record and tag against fusion, then opened with tampering. The counters
+    show the runs taken in 4-lane groups."""
+    rng = np.random.default_rng(8300 + length + aad)
+    n = 256 * 130
+    pa.debug_counters(reset=True)
+    _check(ref, rng, np.full(n, length), np.full(n, aad), key_size, nkeys, tamper=12)
+    c = pa.debug_counters(reset=True)
+    # (a run cut at a key change with fewer than 128 records left in its workgroup's range is cut into units instead)
+    assert c["runs"]["w8_g4"] >= 2 * 200 and c["runs"]["w8_g4"] >= 0.9 * c["runs"]["w8_serial"], c
+
+
 @pytest.mark.parametrize("key_size,nkeys", [(16, 1), (32, 3)])
 def test_w8_tree_kernel_long_whole_runs_vs_fusion(ref, key_size, nkeys):
     """The EXT 3 kernel (butterfly segment ends) takes whole runs of records of at least W8_MIN_STEPS steps, which need

@@ -167,3 +167,77 @@ def test_scattered_serial_chain_equals_the_powers():
             cur = from_w([g[2 * q] for q in range(4)])
             assert all(g[y] == to_w(cur)[y >> 1] for y in range(8))
         assert gmul(cur, h) == want
+
+
+# ---- 4-lane groups (ghash.h group4_*, round 5: the W8 serial kernel's whole runs)
+
+def _scatter4(t):  # t[y] = the 4 dwords of lane y of a quad
+    b = [(y & 2) != 0 for y in range(4)]
+    c = [(y & 1) != 0 for y in range(4)]
+    k0 = [t[y][2] if b[y] else t[y][0] for y in range(4)]
+    k1 = [t[y][3] if b[y] else t[y][1] for y in range(4)]
+    s0 = [t[y][0] if b[y] else t[y][2] for y in range(4)]
+    s1 = [t[y][1] if b[y] else t[y][3] for y in range(4)]
+    m0 = [k0[y] ^ s0[y ^ 2] for y in range(4)]  # quad_perm [2,3,0,1]
+    m1 = [k1[y] ^ s1[y ^ 2] for y in range(4)]
+    kk = [m1[y] if c[y] else m0[y] for y in range(4)]
+    ss = [m0[y] if c[y] else m1[y] for y in range(4)]
+    return [kk[y] ^ ss[y ^ 1] for y in range(4)]  # quad_perm [1,0,3,2]
+
+
+def test_group4_scatter_gives_each_lane_its_dword_of_the_sum():
+    rng = np.random.default_rng(21)
+    for _ in range(200):
+        t = [[int(x) for x in rng.integers(0, 2**32, 4, dtype=np.uint64)] for _ in range(4)]
+        total = [t[0][c] ^ t[1][c] ^ t[2][c] ^ t[3][c] for c in range(4)]
+        assert _scatter4(t) == total
+
+
+def _g8_window(w):  # gmul_group_w: window w -> (dword, bit offset in it, bank group, table row offset)
+    y, u = w >> 2, w & 3
+    return (y >> 1, 16 * (y & 1) + 4 * (u ^ 1), w & 15, (w >> 4) * 4096 + (w & 15) * 16)
+
+
+def test_group4_lookups_read_the_same_windows_as_gmul_group_w():
+    # lane y of a quad, lookup i: window 8y + (i ^ f), f = (lane >> 1) & 7, from its dword y at bit sh[i] and address
+    # Wi[i] - T (group4_ws); every window of the operand once per group, at gmul_group_w's bit and table entry
+    for lane in range(64):
+        y, f = lane & 3, (lane >> 1) & 7
+        B = (y >> 1) * 4096 + (y & 1) * 128 + f * 16
+        ws = set()
+        for i in range(8):
+            w = 8 * y + (i ^ f)
+            ws.add(w)
+            dword, bit, _, off = _g8_window(w)
+            assert dword == y and bit == 4 * ((i ^ f) ^ 1) and off == B ^ (i << 4)
+        assert ws == set(range(8 * y, 8 * y + 8))
+
+
+def test_group4_lookups_are_conflict_free_per_phase():
+    # the 16 lanes of a ds_read_b128 phase (4 quads) read 16 distinct bank groups at every lookup
+    for p0 in range(0, 64, 16):
+        for i in range(8):
+            banks = {_g8_window(8 * (l & 3) + (i ^ ((l >> 1) & 7)))[2] for l in range(p0, p0 + 16)}
+            assert len(banks) == 16
+
+
+def test_group4_scattered_chain_equals_the_powers():
+    rng = np.random.default_rng(22)
+    h = int.from_bytes(rng.bytes(16), "big")
+    to_w = lambda x: [(x >> (96 - 32 * c)) & 0xFFFFFFFF for c in range(4)]
+    from_w = lambda w: (w[0] << 96) | (w[1] << 64) | (w[2] << 32) | w[3]
+    for _ in range(10):
+        v = [int.from_bytes(rng.bytes(16), "big") for _ in range(4)]
+        rot = int(rng.integers(0, 4))
+        rank = [(j - rot) % 4 for j in range(4)]
+        want = 0
+        for j in range(4):
+            want ^= gmul(v[j], gpow(h, 4 - rank[j]))
+        cur = 0
+        for r in range(4):
+            prod = gmul(cur, h) if r else 0
+            parts = [int.from_bytes(rng.bytes(16), "big") for _ in range(3)]
+            terms = parts + [prod ^ parts[0] ^ parts[1] ^ parts[2]]
+            g = _scatter4([to_w(terms[y] ^ (v[y] if rank[y] == r else 0)) for y in range(4)])
+            cur = from_w(g)
+        assert gmul(cur, h) == want

@@ -24,6 +24,7 @@ def main():
     p.add_argument("--lib", default=None, help="engine build to probe (default: picotls_amd/_lib/libptls_mi355x.so)")
     p.add_argument("--ct", action="store_true", help="the constant-time GHASH variant (ptls_mi355x_keyset_set_constant_time)")
     p.add_argument("--permute", type=int, default=0, help="seed of a permutation of the record lengths (0: none)")
+    p.add_argument("--keys", type=int, default=0, help="override the workload's key count (0: keep it)")
     p.add_argument("--no-check", action="store_true", help="skip the ok check (a CT_PROBE_CONST diagnosis build)")
     a = p.parse_args()
 
@@ -36,6 +37,10 @@ def main():
     from picotls_amd.workloads import WORKLOADS, payload_torch
 
     wl = WORKLOADS[a.workload].scaled(a.records)
+    if a.keys:
+        from dataclasses import replace
+
+        wl = replace(wl, nkeys=a.keys)
     if a.permute:  # the same lengths in another order (keys and sequence numbers as before)
         from picotls_amd.records import RecordBatch
 
@@ -69,7 +74,7 @@ def main():
     assert a.no_check or bool(d_ok.min().item() == 1)
     ks.free()
     print(f"ct_probe: key_seed={a.key_seed} payload={a.payload} workload={a.workload} records={b.n} ct={a.ct} "
-          f"permute={a.permute} ok")
+          f"permute={a.permute} keys={wl.nkeys} ok")
 
 
 if __name__ == "__main__":

@@ -80,6 +80,26 @@ python3 tools/ct_summary.py gpurun_out/ct6 > gpurun_out/ct6_mixed.txt; cat gpuru
 exit 0
   )
   ;;
+ctsite)
+  # (round 5) which batch property the many-key mixed kernel's conflict cycles follow: the same length mix under one
+  # key and under 64K keys, uniform lengths under 64K keys, and the sorted mix (rocprofv3 --pmc, 2 seals + 2 opens)
+  (
+R=$GRAFT_REPO_ROOT; cd /tmp && export TMPDIR=/tmp
+run() {  # name, extra args
+  timeout -k 10 240 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS --output-format csv -d $R/gpurun_out/ctsite/$1 -o p -- python3 $R/tools/ct_probe.py --records 4194304 --reps 2 ${@:2} > $R/gpurun_out/ctsite_$1.log 2>&1
+  rc=$?; echo "$1 rc=$rc"; [ $rc -ne 0 ] && { tail -5 $R/gpurun_out/ctsite_$1.log; exit $rc; }
+}
+run mixed_1key --workload mixed --keys 1
+run mixed_64k --workload mixed
+run mixed_4k --workload mixed --keys 4096
+run quic1200_64k --workload quic1200 --keys 65536
+run u8k_64k --workload u8k256 --keys 65536
+run mixedsorted_1key --workload mixedsorted
+cd $R
+python3 tools/ct_summary.py gpurun_out/ctsite > gpurun_out/ctsite.txt; cat gpurun_out/ctsite.txt
+exit 0
+  )
+  ;;
 ab)
   # interleaved A/B (tools/ab.py, one process per workload) of tools/gv/<name> engines at the full BASELINE sizes:
   #   bash tools/gpu_r5.sh ab "base scat" [tag] [workloads...]
