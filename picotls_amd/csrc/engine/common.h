@@ -184,6 +184,10 @@ __device__ __forceinline__ u32 lane_here()
 #ifndef W8_G4
 #define W8_G4 1
 #endif
+// ... and its cut runs too (the units keep their 8-lane-step bounds and combine power; gcm_chunked_kernel)
+#ifndef W8_G4_CUT
+#define W8_G4_CUT 0
+#endif
 #ifndef W8_LEAN_STEP
 #define W8_LEAN_STEP 1
 #endif

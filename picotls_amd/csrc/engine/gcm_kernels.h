@@ -923,7 +923,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         constexpr bool w8run = W8K;
         // W8 segment ends: the serial chain (1), the tree (2), or a whole run of the serial kernel in 4-lane groups (3:
         // Horner with H^4)
-        const bool g4run = W8K && !W8TREE && W8_G4 && whole;
+        const bool g4run = W8K && !W8TREE && (whole ? W8_G4 : W8_G4_CUT);
         const u32 w8mode = !w8run ? 0u : W8TREE ? 2u : g4run ? 3u : 1u;
         if (w8run && (key_idx != loaded_key || loaded_w8 != w8mode)) {
             // the 8-bit H^8 (H^4) table over slots 0..7, H in slot 8, and a cut run's combine power (or the tree's H^2)
@@ -992,10 +992,13 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             }
         };
         bool g4done = false;
-        if constexpr (W8K && !W8TREE && W8_G4) {
+        if constexpr (W8K && !W8TREE && (W8_G4 || W8_G4_CUT)) {
             if (g4run) {
-                // (round 5) a whole run of the serial W8 kernel: 16 records a wave in 4-lane groups (ghash.h), each a
-                // record's whole stream in 64-byte aligned steps; no partials, no combine
+                // (round 5) the serial W8 kernel's whole runs (and with W8_G4_CUT its cut runs): 16 units a wave in
+                // 4-lane groups (ghash.h). A whole run gives each group a record on 64-byte aligned steps; a cut run's
+                // units keep their 8-lane-step bounds (the stream padded to a multiple of 8 positions, unit k of a
+                // record ending 128 * k positions before its end), each taken in twice as many 4-lane steps, so the
+                // partials, their slots and the combine power are the 8-lane kernel's
                 constexpr u32 G4 = 4, RPW4 = 64 / G4;
                 if (threadIdx.x == 0)  // (ptls_mi355x_debug_counters: runs in 4-lane groups)
                     atomicAdd(&g_ext_runs[blockIdx.x % EXT_RUN_ROWS][7], 1ull);
@@ -1012,24 +1015,79 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                         const u32 lane = lane_here(), j = lane % G4, u = ub + lane / G4;
                         const u32 laneoff = (lane & 31) * 4 | W8_AES_BASE;
                         const bool valid = u < total_units;
+                        u32 lo, first, unc, k_back;
+                        unit_of(valid ? u : 0u, lo, first, unc, k_back);
                         ptls_mi355x_record_t r = {};
                         if (valid)
-                            r = recs[pos + u];
+                            r = recs[pos + lo];
                         const bool live = valid && record_ok<FRAME>(args, r);
-                        if (valid && !live) {  // rejected descriptor: nothing is written
+                        if (valid && !live) {  // rejected descriptor (one unit): nothing is written
                             r.len = 0, r.aad_len = 0, r.flags = 0;
                             if (OPEN && j == 0)
-                                args.ok[ok_at(pos + u)] = 0;
+                                args.ok[ok_at(pos + lo)] = 0;
                         }
-                        const u32 ekslot = CLDS_PART + 16u * (threadIdx.x / G4);
-                        gcm_segment<NR, OPEN, 1, FRAME, CT, true, (int)G4>(args, lds, rk, iv0, iv1, iv2, r, live, 0u,
-                                                                         live ? 1u : 0u, j, laneoff, tsel_horner, acc,
-                                                                         true, okw, true, ekslot, false);
+                        // the unit's 8-lane steps [m_lo, m_hi), as the 8-lane loop computes them
+                        const u32 steps = gcm_steps<OPEN, FRAME>(r);
+                        u32 m_hi = steps, m_lo = 0;
+                        if (!whole) {
+                            const u32 ulen = unit_mul(steps, ulog2, run_unit_cap(args)) * ustep;
+                            m_hi = steps - k_back * ulen;
+                            m_lo = k_back + 1 == unc ? 0u : m_hi - ulen;
+                        }
+                        if (!live)
+                            m_lo = m_hi = 0;
+                        const u32 ekslot = CLDS_PART + 16u * (whole ? threadIdx.x / G4 : first + unc - 1);
+                        gcm_segment<NR, OPEN, 1, FRAME, CT, true, (int)G4>(args, lds, rk, iv0, iv1, iv2, r, live, 2u * m_lo,
+                                                                         2u * m_hi, j, laneoff, tsel_horner, acc,
+                                                                         unc == 1, okw, whole, ekslot, false);
                     }
                     asm volatile("" ::: "memory");
-                    const u32 u = ub + lane_here() / G4;
-                    if (OPEN && okw <= 1 && u < total_units)  // a record's tag check (its length lane)
-                        args.ok[ok_at(pos + u)] = (uint8_t)okw;
+                    const u32 lane = lane_here(), j = lane % G4, u = ub + lane / G4;
+                    if (u >= total_units)
+                        continue;  // (uniform over the group)
+                    u32 lo, first, unc, k_back;
+                    unit_of(u, lo, first, unc, k_back);
+                    if (OPEN && okw <= 1)  // a whole record's tag check (its length lane)
+                        args.ok[ok_at(pos + lo)] = (uint8_t)okw;
+                    if constexpr (W8_G4_CUT) {
+                        if (unc > 1) {  // uniform over the group; a rejected descriptor is always one unit
+                            u32 last = 0;
+                            if (j == G4 - 1) {
+                                s_part[first + unc - 1 - k_back] = acc;
+                                __threadfence_block();  // the partial lands before the count that publishes it
+                                last = atomicAdd((u32 *)&s_done[lo], 1u) == unc - 1;
+                            }
+                            last = (u32)__builtin_amdgcn_update_dpp(0, (int)last, 0xFF, 0xF, 0xF, false);  // quad lane 3
+                            if (last) {
+                                // the record's GHASH: Horner over its partials with the unit power (W8_TAB_COMB), a
+                                // scattered chain over the quad (lane j carries dword j)
+                                const ptls_mi355x_record_t r = recs[pos + lo];
+                                const u32 mul = unit_mul(gcm_steps<OPEN, FRAME>(r), ulog2, run_unit_cap(args));
+                                const Group4Ws k = group4_ws(tsel_chunk, lane);
+                                const u32x4 z = {0, 0, 0, 0};
+                                u32 gs = ((const lds_u32 *)(s_part + first))[j];
+                                for (u32 i = 1; i < unc; ++i) {
+                                    for (u32 t = 0; t < mul; ++t)  // (mul > 1: huge records only)
+                                        gs = group4_scatter(group4_ws_terms(gs, k, z), lane);
+                                    gs ^= ((const lds_u32 *)(s_part + first + i))[j];
+                                }
+                                const u32x4 tag = {(u32)__builtin_amdgcn_update_dpp(0, (int)gs, 0x00, 0xF, 0xF, false),
+                                                   (u32)__builtin_amdgcn_update_dpp(0, (int)gs, 0x55, 0xF, 0xF, false),
+                                                   (u32)__builtin_amdgcn_update_dpp(0, (int)gs, 0xAA, 0xF, 0xF, false),
+                                                   (u32)__builtin_amdgcn_update_dpp(0, (int)gs, 0xFF, 0xF, 0xF, false)};
+                                if (j != G4 - 1) {
+                                } else if (OPEN) {
+                                    const u32x4 rt = *(const u32x4_u *)(args.in + r.in_off + frame_in_skip<OPEN, FRAME>() +
+                                                                        gcm_text_len<OPEN, FRAME>(r));
+                                    const u32x4 d = rt ^ tag;
+                                    args.ok[ok_at(pos + lo)] = (d[0] | d[1] | d[2] | d[3]) == 0;
+                                } else {
+                                    *(u32x4_u *)(args.out + r.out_off + frame_out_skip<OPEN, FRAME>() +
+                                                 gcm_text_len<OPEN, FRAME>(r)) = tag;
+                                }
+                            }
+                        }
+                    }
                 }
                 g4done = true;
             }

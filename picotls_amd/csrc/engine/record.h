@@ -34,6 +34,20 @@ __device__ __forceinline__ u32x4 load_partial(const uint8_t *p, u32 n)
     return v;
 }
 
+// load_partial without the mask, for a load issued ahead of its use: bytes n..15 are unspecified until mask_tail (so
+// the wait for the load can sit after the work issued behind it)
+__device__ __forceinline__ u32x4 load_partial_raw(const uint8_t *p, u32 n)
+{
+    if (n != 0 && ((uintptr_t)p & 4095u) <= 4096u - 16u)
+        return *(const u32x4_u *)p;
+    u32x4 v = {0, 0, 0, 0};
+#pragma unroll
+    for (u32 i = 0; i < 15; ++i)
+        if (i < n)
+            v[i >> 2] |= (u32)p[i] << (8 * (i & 3));
+    return v;
+}
+
 __device__ __forceinline__ void store_partial(uint8_t *p, u32x4 v, u32 n)
 {
     for (u32 i = 0; i < n; ++i)

@@ -71,10 +71,10 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         N = (u32)P + total;
         if (valid)
             m_hi = (N + G - 1) / G;
-    } else {
-        const u32 K = (total + G - 1) / G;
-        P = (int)(K * G) - (int)total;
-        N = K * G;
+    } else {  // (padded to a multiple of ENGINE_G positions for any G: 4-lane groups take the 8-lane units' bounds)
+        const u32 K = (total + ENGINE_G - 1) / ENGINE_G;
+        P = (int)(K * ENGINE_G) - (int)total;
+        N = K * ENGINE_G;
     }
     // this lane's last step in the segment and its power there: at the record's end H^(N - p) for its last position p,
     // at a unit's end (a step boundary) H^(G - j)
@@ -281,12 +281,16 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             int bn;
             if (full_block(m0 + 1, bn))
                 nxt[0] = *(const u32x4_u *)(src + 16u * (u32)bn);
+            // (masked after the AES: a mask here would wait for the load before it)
+            u32 nin = 16;
             if (is_aad) {
                 const u32 arem = A - 16u * (u32)logical;
                 const uint8_t *ap = aadp + 16u * (u32)logical;
-                xin = arem >= 16 ? *(const u32x4_u *)ap : load_partial(ap, arem);
+                xin = arem >= 16 ? *(const u32x4_u *)ap : load_partial_raw(ap, arem);
+                nin = min(arem, 16u);
             } else if (is_data && !full) {
-                xin = load_partial(src + 16u * (u32)b, rem);
+                xin = load_partial_raw(src + 16u * (u32)b, rem);
+                nin = rem;
             }
             // AES-CTR input: data positions encrypt counter 2 + b, all others J0 (the length lane keeps E(K, J0))
             const u32 ctr = is_data ? (u32)(b + 2) : 1u;
@@ -304,11 +308,12 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                 *(u32x4_u *)(dst + 16u * (u32)b) = o;
                 X = OPEN ? xin : o;
             } else if (is_aad) {
-                X = xin;
+                X = mask_tail(xin, nin);
             } else if (is_data) {
-                const u32x4 o = mask_tail(xin ^ ks, rem);
+                const u32x4 v = mask_tail(xin, nin);
+                const u32x4 o = mask_tail(v ^ ks, rem);
                 store_partial(dst + 16u * (u32)b, o, rem);
-                X = OPEN ? xin : o;
+                X = OPEN ? v : o;
             } else if (is_len) {
                 u32 Ah = A, Lh = L;
                 asm volatile("" : "+v"(Ah), "+v"(Lh));
