@@ -177,19 +177,22 @@ __device__ __forceinline__ u32 lane_here()
 // loop, and the AES addresses take their 64 KiB slot from laneoff's byte 2 in the same v_perm (aes_tt.h TE_ADDR)
 #define W8_SWAP 1
 #endif
-// (round 5) the W8 kernels' unframed steps outside the steady range as one pass with the non-text inputs loaded ahead of
-// the AES (segment.h); 0 keeps the per-case setup_step / finish_step
 // (round 5) whole runs of the W8 serial kernel (EXT 4: uniform records under W8_MIN_STEPS steps) in 4-lane groups
-// (ghash.h, gcm_chunked_kernel); 0 keeps 8-lane groups
+// (ghash.h, gcm_chunked_kernel): quic1200 +3.3-3.9 % (profiles/r5/g4_ab.txt); 0 keeps 8-lane groups
 #ifndef W8_G4
 #define W8_G4 1
 #endif
-// ... and its cut runs too (the units keep their 8-lane-step bounds and combine power; gcm_chunked_kernel)
+// ... and its cut runs too (the units keep their 8-lane-step bounds and combine power; gcm_chunked_kernel): measured
+// -6 % on mixed (units twice as long in time, so the run tails wait twice as long), also with the run's units sized
+// for 256 groups (RUN_FILL_UNITS_G4 128): off
 #ifndef W8_G4_CUT
 #define W8_G4_CUT 0
 #endif
+// (round 5) the W8 kernels' unframed steps outside the steady range as one pass with the non-text inputs loaded ahead of
+// the AES (segment.h): measured within +-0.5 % of the per-case setup_step / finish_step on quic1200 and mixed
+// (profiles/r5/g4_ab.txt): off
 #ifndef W8_LEAN_STEP
-#define W8_LEAN_STEP 1
+#define W8_LEAN_STEP 0
 #endif
 #define W8_H8_BASE (W8_SWAP ? 0u : (u32)LDS_AES_BYTES)   // the W8 kernels' 8-bit H^8 table
 #define W8_AES_BASE (W8_SWAP ? (u32)LDS_AES_BYTES : 0u)  // ... and their AES T-tables
