@@ -125,7 +125,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     // step m, part 1: the next step's input prefetch and this step's counter block (refreshing the counter cache when
     // the lane enters a new 256-counter window)
     u32x4 cur;
-    auto setup_step = [&](u32 m0, u32 (&st)[1][4]) {
+    auto setup_step = [&](u32 m0, u32 (&st)[1][4], bool wave_ks) {
         cur = nxt[0];
         int bn;
         if (full_block(m0 + 1, bn))
@@ -137,7 +137,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         st[0][0] = n0, st[0][1] = n1, st[0][2] = n2;
         const u32 ctr = is_data ? (u32)(b + 2) : 1u;
         st[0][3] = bswap32(ctr) ^ rk[0][3];
-        if ((ctr >> 8) != cc1_key) {  // entering a new 256-counter window (divergent; skipped when no lane does)
+        if (wave_ks && (ctr >> 8) != cc1_key) {  // entering a new 256-counter window (divergent; skipped when no lane does)
             cc1 = ctr_cache1_init<NR>(lds, laneoff, rk, n0, n1, n2, st[0][3]);
             cc1_key = ctr >> 8;
         }
@@ -339,9 +339,15 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         }
 #endif
         const u32 m0 = m_lo + s0;
+        // (round 5) a step in which no lane of the wave holds a text or length position (front padding and AAD only:
+        // the first step of 4-lane groups on short records) needs no keystream and skips the AES; the lengths decide
+        // it, not the data
+        const int lg = (int)(j + G * m0) - P;
+        const bool wave_ks = __any(m0 < m_hi && lg >= (int)na && lg <= (int)(na + nb)) != 0;
         u32 st[1][4];
-        setup_step(m0, st);
-        aes_ctr_cached1<NR>(lds, laneoff, rk, cc1, st);
+        setup_step(m0, st, wave_ks);
+        if (wave_ks)
+            aes_ctr_cached1<NR>(lds, laneoff, rk, cc1, st);
         __builtin_amdgcn_sched_barrier(0);
         u32x4 ek0 = {0, 0, 0, 0};
         const u32x4 X = finish_step(m0, u32x4{st[0][0], st[0][1], st[0][2], st[0][3]}, ek0);
