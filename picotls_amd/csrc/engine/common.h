@@ -183,8 +183,8 @@ __device__ __forceinline__ u32 lane_here()
 #define W8_G4 1
 #endif
 // ... and its cut runs too (the units keep their 8-lane-step bounds and combine power; gcm_chunked_kernel): measured
-// -6 % on mixed (units twice as long in time, so the run tails wait twice as long), also with the run's units sized
-// for 256 groups (RUN_FILL_UNITS_G4 128): off
+// -6 % on mixed (units twice as long in time, so the run tails wait twice as long; also with each run cut into at least
+// 128 units), -18 % with units of half the length (twice the partials and combine links): off (profiles/r5/g4_ab.txt)
 #ifndef W8_G4_CUT
 #define W8_G4_CUT 0
 #endif

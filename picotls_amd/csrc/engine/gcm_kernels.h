@@ -212,13 +212,10 @@ __device__ unsigned long long g_ext_runs[EXT_RUN_ROWS][8];
 // partials (a chain is serial, ~0.15 us a link; 36 admits a 16 KiB TLS record, 129 steps, in 4-step units). Big
 // batches keep 2 KiB units; a run of a few records -- a small batch -- is cut finer, so its records spread over the
 // waves. (A launch of one record passes its own length rule, single() in aesgcm_engine.hip.)
-#ifndef RUN_FILL_UNITS_G4
-#define RUN_FILL_UNITS_G4 RUN_FILL_UNITS  // ... in the W8 serial kernel when its cut runs take 4-lane groups (W8_G4_CUT)
-#endif
-__device__ __forceinline__ u32 run_unit_log2(u32 total_steps, u32 smax, u32 cap, u32 fill_units = RUN_FILL_UNITS)
+__device__ __forceinline__ u32 run_unit_log2(u32 total_steps, u32 smax, u32 cap)
 {
     u32 fill = 0, chain = 0;
-    while (fill < cap && (total_steps >> (fill + 1)) >= fill_units)
+    while (fill < cap && (total_steps >> (fill + 1)) >= (u32)RUN_FILL_UNITS)
         ++fill;
     while (chain < cap && ((smax + (1u << chain) - 1) >> chain) > (u32)RUN_MAX_CHAIN)
         ++chain;
@@ -277,8 +274,7 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
             tot += q * 64 + lane < n ? steps[q] : 0u;
         const u32 tot_incl = wave_incl_sum(tot);
         if (log2 == CHUNK_LOG2)
-            log2 = run_unit_log2((u32)__builtin_amdgcn_readlane((int)tot_incl, 63), smax, CHUNK_LOG2,
-                                 EXT == 4 && W8_G4_CUT ? (u32)RUN_FILL_UNITS_G4 : (u32)RUN_FILL_UNITS);
+            log2 = run_unit_log2((u32)__builtin_amdgcn_readlane((int)tot_incl, 63), smax, CHUNK_LOG2);
         const u32 ustep = 1u << log2;
 #pragma unroll
         for (u32 q = 0; q < Q; ++q) {
