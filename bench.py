@@ -159,6 +159,9 @@ def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(steps)]
     clk = torch.zeros(8, dtype=torch.int64, device=dev)  # two (s_memtime, s_memrealtime, XCD) samples of XCD 0
+    kcap = 4 * steps + 8  # in-kernel samples: workgroup 0 of each chunked launch (a W8 pair is two launches)
+    kclk = torch.zeros(4 * kcap, dtype=torch.int64, device=dev)
+    pa.debug_kernel_clock(kclk.data_ptr(), kcap)
     torch.cuda.synchronize(dev)
     R.barrier()
     torch.cuda.synchronize(dev)
@@ -177,9 +180,11 @@ def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool
     wall = t1 - t0
     seal_ms = float(np.mean([a.elapsed_time(bb) for a, bb, _ in ev]))
     open_ms = float(np.mean([bb.elapsed_time(c) for _, bb, c in ev]))
+    nk = min(pa.debug_kernel_clock_count(), kcap)
+    pa.debug_kernel_clock(0, 0)
 
     res = {"records": b.n, "payload_bytes": b.payload_bytes, "wall_s": wall, "seal_ms": seal_ms, "open_ms": open_ms,
-           "shard": [begin, end], "clock": shader_clock(clk.cpu().numpy())}
+           "shard": [begin, end], "clock": shader_clock(clk.cpu().numpy(), kclk[:4 * nk].cpu().numpy())}
     res["sclk_mhz"] = res["clock"]["sclk_mhz"]
     lens = b.seal["len"]
     res["seal_alg_bytes"] = algorithmic_bytes(lens, b.seal["aad_len"], True)
@@ -201,16 +206,28 @@ def run_workload(R, wl, steps: int, warmup: int, verify: int, shard_global: bool
     return res
 
 
-def shader_clock(c) -> dict:
-    """The shader clock right after a timed leg's first and last kernels (ptls_mi355x_debug_clock_sample: s_memtime
-    cycles over a ~20 us spin of one wave, against the real-time counter at the rate the runtime reports), so that
-    box-to-box spread in the line can be attributed; sclk_mhz is the mean of the two samples."""
+def shader_clock(c, k=None) -> dict:
+    """The shader clock over a timed leg. sclk_mhz: inside the kernels (ptls_mi355x_debug_kernel_clock: workgroup 0 of
+    every chunked launch reads s_memtime and s_memrealtime at its start and end; cycles over real-time ticks, weighted by
+    duration), the clock the chip holds under the load. after_*_mhz: a one-wave probe right after the leg's first and
+    last steps (ptls_mi355x_debug_clock_sample: s_memtime over a ~20 us spin), the clock once the load has stopped, which
+    runs higher under a power limit."""
     import picotls_amd as pa
 
     khz = pa.debug_wallclock_khz()
     mhz = [round(int(c[i]) / (int(c[i + 1]) / (khz * 1e3)) / 1e6, 1) if khz > 0 and int(c[i + 1]) > 0 else None for i in (0, 4)]
     ok = [m for m in mhz if m is not None]
-    return {"sclk_mhz": round(sum(ok) / len(ok), 1) if ok else None, "after_first_step_mhz": mhz[0],
+    inside, launches = None, 0
+    if k is not None and len(k) >= 4 and khz > 0:
+        s = np.asarray(k, dtype=np.int64).reshape(-1, 4)
+        cyc, ticks = (s[:, 1] - s[:, 0]).astype(np.float64), (s[:, 3] - s[:, 2]).astype(np.float64)
+        keep = (ticks > 0) & (cyc > 0)
+        launches = int(keep.sum())
+        if launches:
+            inside = round(float(cyc[keep].sum() / (ticks[keep].sum() / (khz * 1e3)) / 1e6), 1)
+    return {"sclk_mhz": inside if inside is not None else (round(sum(ok) / len(ok), 1) if ok else None),
+            "in_kernel_mhz": inside, "in_kernel_launches": launches,
+            "after_probe_mhz": round(sum(ok) / len(ok), 1) if ok else None, "after_first_step_mhz": mhz[0],
             "after_last_step_mhz": mhz[1], "xcd": [int(c[2]), int(c[6])], "rtc_khz": khz}
 
 

@@ -41,6 +41,16 @@ int ptls_mi355x_debug_clock_sample(void *out, void *stream);
 /* the real-time counter's rate in kHz (hipDeviceAttributeWallClockRate of the current device), 0 if unknown */
 int ptls_mi355x_debug_wallclock_khz(void);
 
+/**
+ * Samples the shader clock inside the chunked batch kernels: from the next launch on, workgroup 0 of every chunked launch
+ * that has work appends four 64-bit words to the device buffer `buf` (room for `cap` launches): shader-clock cycles
+ * (s_memtime) at its start and end, then real-time counter ticks (s_memrealtime) at its start and end. buf = NULL stops
+ * sampling. Waits for the device. Returns 0 or -1.
+ */
+int ptls_mi355x_debug_kernel_clock(void *buf, unsigned cap);
+/* the number of launches sampled since the last ptls_mi355x_debug_kernel_clock (may exceed cap); waits for the device */
+int ptls_mi355x_debug_kernel_clock_count(void);
+
 #ifdef __cplusplus
 }
 #endif

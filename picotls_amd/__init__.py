@@ -71,6 +71,8 @@ DEBUG_FUNCTIONS = (
     "ptls_mi355x_debug_inject_error",
     "ptls_mi355x_debug_clock_sample",
     "ptls_mi355x_debug_wallclock_khz",
+    "ptls_mi355x_debug_kernel_clock",
+    "ptls_mi355x_debug_kernel_clock_count",
 )
 
 SIZE_MAX = ctypes.c_size_t(-1).value
@@ -138,6 +140,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.ptls_mi355x_debug_inject_error.restype = ci
     lib.ptls_mi355x_debug_clock_sample.argtypes = [vp, vp]
     lib.ptls_mi355x_debug_wallclock_khz.restype = ci
+    lib.ptls_mi355x_debug_kernel_clock.argtypes = [vp, ctypes.c_uint]
+    lib.ptls_mi355x_debug_kernel_clock_count.restype = ci
     _lib = lib
     return lib
 
@@ -483,6 +487,21 @@ def debug_clock_sample(dev_ptr: int, stream: int = 0) -> None:
 
 def debug_wallclock_khz() -> int:
     return int(load_library().ptls_mi355x_debug_wallclock_khz())
+
+
+def debug_kernel_clock(dev_ptr: int, cap: int) -> None:
+    """From the next launch on, workgroup 0 of each chunked launch appends (memtime start, end, realtime start, end) as
+    4 x u64 to the device buffer at dev_ptr (room for cap launches); dev_ptr 0 stops (ptls_mi355x_debug_kernel_clock)."""
+    if load_library().ptls_mi355x_debug_kernel_clock(dev_ptr or None, cap if dev_ptr else 0) != 0:
+        raise _err("ptls_mi355x_debug_kernel_clock")
+
+
+def debug_kernel_clock_count() -> int:
+    """Launches sampled since the last debug_kernel_clock (may exceed the buffer's cap)."""
+    n = int(load_library().ptls_mi355x_debug_kernel_clock_count())
+    if n < 0:
+        raise _err("ptls_mi355x_debug_kernel_clock_count")
+    return n
 
 
 def aead_new_direct(algo: AeadAlgorithm, is_enc: bool, key: bytes, iv: bytes) -> AeadContext:

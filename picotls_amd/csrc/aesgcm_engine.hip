@@ -875,6 +875,25 @@ int ptls_mi355x_debug_counters(uint64_t *out, int reset)
     return 0;
 }
 
+int ptls_mi355x_debug_kernel_clock(void *buf, unsigned cap)
+{
+    unsigned long long *b = (unsigned long long *)buf;
+    const unsigned zero = 0, c = buf != NULL ? cap : 0;
+    HIP_TRY(hipDeviceSynchronize());  // (test-only: no launch may be sampling while the buffer changes)
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_kclock_n), &zero, sizeof(zero)));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_kclock_cap), &c, sizeof(c)));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_kclock_buf), &b, sizeof(b)));
+    return 0;
+}
+
+int ptls_mi355x_debug_kernel_clock_count(void)
+{
+    unsigned n = 0;
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_kclock_n), sizeof(n)));
+    return (int)n;
+}
+
 int ptls_mi355x_debug_inject_error(void)
 {
     // a handled-looking failure of the kind the per-record path meets (hipHostGetDevicePointer on memory HIP did not

@@ -748,6 +748,13 @@ __device__ __noinline__ void w8_build_tables(lds_u8 *lds, const lds_u8 *keyp, u3
     __syncthreads();
 }
 
+// (test and measurement hook, include/picotls/mi355x_debug.h: ptls_mi355x_debug_kernel_clock) when g_kclock_buf is set,
+// workgroup 0 of every chunked launch that has work appends {s_memtime, s_memrealtime} at its start and at its end: the
+// shader clock the chip holds over the launch itself, which a probe after the launch cannot see
+__device__ unsigned long long *g_kclock_buf;
+__device__ unsigned int g_kclock_cap;
+__device__ unsigned int g_kclock_n;
+
 template <int NR, bool OPEN, int FRAME, bool CT = false, int EXT = 0>
 __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGINE_WAVES_PER_SIMD, ENGINE_WAVES_PER_SIMD))) void gcm_chunked_kernel(BatchArgs args)
 {
@@ -773,6 +780,9 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         if (args.w8_split == 2 && args.w8_flags != nullptr && args.w8_flags[blockIdx.x] == 0)
             return;
     }
+    unsigned long long *const kclock = blockIdx.x == 0 ? g_kclock_buf : nullptr;
+    const u64 kc_t0 = kclock != nullptr ? __builtin_amdgcn_s_memtime() : 0ull;
+    const u64 kc_r0 = kclock != nullptr ? __builtin_amdgcn_s_memrealtime() : 0ull;
     bool skipped_w8 = false;  // (the pair's first kernel: this workgroup left a run to the second one)
     constexpr bool SPREAD = FRAME == 0 && EXT == 1;
     if constexpr (SPREAD) {  // a small one-key batch (spread_pieces): workgroup w < n takes record w unless it is long
@@ -1250,6 +1260,14 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     if constexpr (W8K && !W8TREE) {  // the pair's first kernel, for the second (workgroup-uniform)
         if (args.w8_split == 2 && args.w8_flags != nullptr && threadIdx.x == 0)
             args.w8_flags[blockIdx.x] = skipped_w8 ? 1u : 0u;
+    }
+    if (kclock != nullptr && threadIdx.x == 0) {  // (vector stores and atomics only)
+        const u64 t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        const u32 i = atomicAdd(&g_kclock_n, 1u);
+        if (i < g_kclock_cap) {
+            kclock[4 * i + 0] = kc_t0, kclock[4 * i + 1] = t1;
+            kclock[4 * i + 2] = kc_r0, kclock[4 * i + 3] = r1;
+        }
     }
     publish_done(args.done_flag, args.done_token);  // the per-record path polls these instead of waiting for the stream
 #undef HP_PASS

@@ -81,6 +81,8 @@ def test_bench_single_gpu_line_has_shard1200_by_default():
     # XCD 0's shader clock over each timed leg: a plausible MI355X clock
     for leg in (out, sh):
         assert leg["sclk_mhz"] is not None and 500 < leg["sclk_mhz"] < 3000, leg["sclk_mhz"]
+    # ... sampled inside the kernels (ptls_mi355x_debug_kernel_clock: workgroup 0 of every chunked launch)
+    assert out["clock_probe"]["in_kernel_launches"] >= 2 and out["clock_probe"]["in_kernel_mhz"] == out["sclk_mhz"]
 
 
 def test_bench_nccl_process_group_on_one_gpu():
