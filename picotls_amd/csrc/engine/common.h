@@ -182,6 +182,15 @@ __device__ __forceinline__ u32 lane_here()
 #ifndef W8_G4
 #define W8_G4 1
 #endif
+// (round 5) gmul8's selects by bit 3 of the lane from a constant lane mask (ghash.h)
+// (round 5) steps without a text or length position skip the AES (segment.h)
+#ifndef SKIP_EMPTY_AES
+#define SKIP_EMPTY_AES 1
+#endif
+#ifndef GMUL8_CONST_MASK
+#define GMUL8_CONST_MASK 1
+#endif
+#define GMUL8_LANE() (GMUL8_CONST_MASK && W8_SWAP ? 0u : lane_here())  // (lane_here is a volatile asm: not evaluated unless needed)
 // ... and its cut runs too (the units keep their 8-lane-step bounds and combine power; gcm_chunked_kernel): measured
 // -6 % on mixed (units twice as long in time, so the run tails wait twice as long; also with each run cut into at least
 // 128 units), -18 % with units of half the length (twice the partials and combine links): off (profiles/r5/g4_ab.txt)

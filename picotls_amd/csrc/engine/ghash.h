@@ -136,8 +136,25 @@ __device__ __forceinline__ u32x4 gmul8(const lds_u8 *, u32x4 t, u32 lane, W8Lane
             L[c] = w.base ^ (c * 0x40404040u);
         // p[k] byte c = t byte ((4k + c) ^ l): the dword pair by bit 3 of l (selects), then dword k ^ (bit 2 of l) and
         // the bytes by bits 0-1 in one v_perm of the pair (psel picks from the other dword when bit 2 is set)
+        u32 a0, a1, a2, a3;
+#if GMUL8_CONST_MASK  // (the W8_SWAP form: the other one reads the lane index)
+        // (round 5) the selects by bit 3 of the lane take a constant lane mask (lanes 8-15 of every 16:
+        // 0xff00ff00ff00ff00) in VCC instead of a compare of the lane index, which the loop re-derived every step
+        // (v_mbcnt x2, v_and, v_cmp: the kernel is short of SGPRs to keep the mask)
+        (void)lane;
+        asm("s_mov_b32 vcc_lo, 0xff00ff00\n\t"
+            "s_mov_b32 vcc_hi, 0xff00ff00\n\t"
+            "v_cndmask_b32 %0, %4, %6, vcc\n\t"
+            "v_cndmask_b32 %1, %5, %7, vcc\n\t"
+            "v_cndmask_b32 %2, %6, %4, vcc\n\t"
+            "v_cndmask_b32 %3, %7, %5, vcc"
+            : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3)
+            : "v"(t[0]), "v"(t[1]), "v"(t[2]), "v"(t[3])
+            : "vcc");
+#else
         const bool s2 = (lane & 8) != 0;
-        const u32 a0 = s2 ? t[2] : t[0], a1 = s2 ? t[3] : t[1], a2 = s2 ? t[0] : t[2], a3 = s2 ? t[1] : t[3];
+        a0 = s2 ? t[2] : t[0], a1 = s2 ? t[3] : t[1], a2 = s2 ? t[0] : t[2], a3 = s2 ? t[1] : t[3];
+#endif
         u32 p[4] = {__builtin_amdgcn_perm(a1, a0, w.psel), __builtin_amdgcn_perm(a0, a1, w.psel),
                     __builtin_amdgcn_perm(a3, a2, w.psel), __builtin_amdgcn_perm(a2, a3, w.psel)};
         if (CT_PROBE_CONST)

@@ -254,7 +254,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                 *(u32x4_u *)(dst + off) = o;
                 __builtin_amdgcn_sched_barrier(0);
                 if constexpr (W8)
-                    acc = gmul8(lds, acc ^ (OPEN ? cur : o), lane_here(), w8);
+                    acc = gmul8(lds, acc ^ (OPEN ? cur : o), GMUL8_LANE(), w8);
                 else
                     acc = gmul_tab(lds, acc ^ (OPEN ? cur : o), tsel_horner);
                 __builtin_amdgcn_sched_barrier(0);
@@ -328,7 +328,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             const u32x4 t = acc ^ X;
             u32x4 prod = t;
             if (s0 + 1 < Smax) {
-                prod = gmul8(lds, t, lane_here(), w8);
+                prod = gmul8(lds, t, GMUL8_LANE(), w8);
                 if ((int)m0 == m_last)
                     prod = t;
             }
@@ -343,7 +343,8 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         // the first step of 4-lane groups on short records) needs no keystream and skips the AES; the lengths decide
         // it, not the data
         const int lg = (int)(j + G * m0) - P;
-        const bool wave_ks = __any(m0 < m_hi && lg >= (int)na && lg <= (int)(na + nb)) != 0;
+        // (4-lane groups only: in 8-lane kernels such a step is rare, and the test cost the TLS 1.3 open kernel spills)
+        const bool wave_ks = !(SKIP_EMPTY_AES && G == 4) || __any(m0 < m_hi && lg >= (int)na && lg <= (int)(na + nb)) != 0;
         u32 st[1][4];
         setup_step(m0, st, wave_ks);
         if (wave_ks)
@@ -386,7 +387,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             prod = t;
             if (s0 + 1 < Smax) {
                 if constexpr (W8)
-                    prod = gmul8(lds, t, lane_here(), w8);
+                    prod = gmul8(lds, t, GMUL8_LANE(), w8);
                 else
                     prod = gmul_tab(lds, t, tsel_horner);
                 if (last_here)
