@@ -656,9 +656,14 @@ def lds_model(res, key_size: int, nrecs: int):
     sec_per_block = lookups * 4 / 75e12 + ghash * 16 / 150e12
     peak = 1.0 / sec_per_block
     achieved = res["stream_blocks"] / (res["seal_ms"] / 1e3)
-    return {"bound": "lds", "unit": "stream blocks/s", "achieved": round(achieved, -6), "peak_at_2.4GHz": round(peak, -6),
-            "frac": round(achieved / peak, 4),
-            "per_block": f"{lookups} ds_read_b32 (AES) + {ghash} ds_read_b128 (GHASH)"}
+    out = {"bound": "lds", "unit": "stream blocks/s", "achieved": round(achieved, -6), "peak_at_2.4GHz": round(peak, -6),
+           "frac": round(achieved / peak, 4),
+           "per_block": f"{lookups} ds_read_b32 (AES) + {ghash} ds_read_b128 (GHASH)"}
+    mhz = (res.get("clock") or {}).get("in_kernel_mhz")
+    if mhz:  # the same ceiling at the shader clock measured inside the kernels over this leg
+        out["sclk_mhz"] = mhz
+        out["frac_at_sclk"] = round(achieved / (peak * mhz / 2400.0), 4)
+    return out
 
 
 def traffic_from_profiles(workload: str, records: int, key: str = "seal_hbm_bytes_per_launch"):
