@@ -222,16 +222,10 @@ __device__ __forceinline__ u32 run_unit_log2(u32 total_steps, u32 smax, u32 cap)
     return fill > chain ? fill : chain;
 }
 
-#ifndef FRONT_MERGE_DEN
-#define FRONT_MERGE_DEN 0  // (round 5) the W8 kernels' cut runs merge first units of at most ustep / this (0: off)
-#endif
 template <bool OPEN, int FRAME, bool FIRST = false, int EXT = 0>
 __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355x_record_t *__restrict__ recs, u64 p, u64 end,
                                       lds_u32 *rs)
 {
-    // (both kernels of a W8 pair: their scans must cut the runs alike)
-    constexpr bool FRONT_MERGE = FRONT_MERGE_DEN != 0 && (EXT == 3 || EXT == 4);
-    constexpr u32 NBKT = FRONT_MERGE ? 2 * CHUNK_STEPS : CHUNK_STEPS;  // the largest bucket
     constexpr u32 Q = CRUN_RECS / 64;
     lds_u32 *ubase = rs + RUN_UBASE_OFF, *done = rs + RUN_DONE_OFF, *front = rs + RUN_FRONT_OFF;
     const u32 lane = lane_here();
@@ -290,20 +284,8 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
             nc[q] = (steps[q] + ustep - 1) >> log2;
             if (mul > 1)  // rare: the only division
                 nc[q] = (steps[q] + mul * ustep - 1) / (mul * ustep);
-            u32 front = steps[q] - (nc[q] - 1) * ustep;
-            if constexpr (FRONT_MERGE) {
-                // (round 5) a short first unit joins the record's next one (units end where they ended, so the
-                // partials and combine powers do not change): one unit fewer, its per-unit work saved. Merged first
-                // units (longer than ustep) go first with the huge records' (buckets 1..ustep), the others last, by
-                // size (buckets ustep + 1..2 ustep)
-                if (mul == 1 && nc[q] >= 2 && front * FRONT_MERGE_DEN <= ustep)
-                    nc[q] -= 1, front += ustep;
-                bkt[q] = mul > 1 ? 0u : 2 * ustep + 1 - front;
-            } else {
-                bkt[q] = mul > 1 ? 0u : ustep + 1 - front;
-            }
+            bkt[q] = mul > 1 ? 0u : ustep + 1 - (steps[q] - (nc[q] - 1) * ustep);
         }
-        const u32 first_max = FRONT_MERGE ? ustep : 0u;  // buckets whose units go first (huge and merged records)
         // unit prefix in record order; the first record whose units overflow the run's partial slots ends the run
         // (never the first record)
         u32 carry = 0, cut = n;
@@ -324,7 +306,7 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
             ubase[0] = 0;
         n = __builtin_amdgcn_readfirstlane(min(n, max(cut, 1u)));
         if (FIRST && n == 1) {  // a lone record (the per-record picotls path): no sort
-            nhuge = __builtin_amdgcn_readfirstlane(bkt[0]) <= first_max;
+            nhuge = __builtin_amdgcn_readfirstlane(bkt[0]) == 0;
             if (lane == 0)
                 front[0] = 0;
         } else if (FIRST && n <= 64) {
@@ -336,7 +318,7 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
             for (u32 i = 0; i < n; ++i) {
                 const u32 bi = (u32)__builtin_amdgcn_readlane((int)bkt[0], (int)i);
                 rank += bi < mine || (bi == mine && i < lane) ? 1u : 0u;
-                huge += bi <= first_max ? 1u : 0u;
+                huge += bi == 0 ? 1u : 0u;
             }
             nhuge = __builtin_amdgcn_readfirstlane(huge);
             if (lane < n)
@@ -350,20 +332,19 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
                 if (FIRST && q * 64 >= n)
                     break;
 #pragma unroll 1
-                for (u32 b = 0; b <= NBKT; ++b) {
+                for (u32 b = 0; b <= CHUNK_STEPS; ++b) {
                     const u32 c = (u32)__popcll(__ballot(q * 64 + lane < n && bkt[q] == b));
                     cnt += lane == b ? c : 0u;
                 }
             }
-            const u32 cincl = wave_incl_sum(cnt);
-            u32 next = cincl - cnt;  // lane b: next free slot of bucket b
-            nhuge = (u32)__builtin_amdgcn_readlane((int)cincl, (int)first_max);
+            u32 next = wave_incl_sum(cnt) - cnt;  // lane b: next free slot of bucket b
+            nhuge = (u32)__builtin_amdgcn_readlane((int)cnt, 0);
 #pragma unroll
             for (u32 q = 0; q < Q; ++q) {
                 if (FIRST && q * 64 >= n)
                     break;
 #pragma unroll 1
-                for (u32 b = 0; b <= NBKT; ++b) {
+                for (u32 b = 0; b <= CHUNK_STEPS; ++b) {
                     const bool in = q * 64 + lane < n && bkt[q] == b;
                     const u64 m = __ballot(in);
                     if (m == 0)
