@@ -148,23 +148,23 @@ static int is_mi355x_ctr(ptls_cipher_context_t *c)
     return c->algo == &ptls_mi355x_aes128ctr || c->algo == &ptls_mi355x_aes256ctr;
 }
 
-static void aead_do_encrypt(ptls_aead_context_t *_ctx, void *output, const void *input, size_t inlen, uint64_t seq,
-                            const void *aad, size_t aadlen, ptls_aead_supplementary_encryption_t *supp)
+/* a seal of one record on key 0 of ks, with the optional supplementary (header protection) block; fails closed */
+static void seal_one(ptls_mi355x_keyset_t *ks, void *output, const void *input, size_t inlen, uint64_t seq, const void *aad,
+                     size_t aadlen, ptls_aead_supplementary_encryption_t *supp)
 {
-    struct mi355x_aead_context *ctx = (struct mi355x_aead_context *)_ctx;
     if (supp != NULL && is_mi355x_ctr(supp->ctx) &&
-        ptls_mi355x_keyset_device(((struct mi355x_ctr_context *)supp->ctx)->ks) == ptls_mi355x_keyset_device(ctx->ks) &&
+        ptls_mi355x_keyset_device(((struct mi355x_ctr_context *)supp->ctx)->ks) == ptls_mi355x_keyset_device(ks) &&
         (const uint8_t *)supp->input >= (const uint8_t *)output &&
         (const uint8_t *)supp->input + 16 <= (const uint8_t *)output + inlen + PTLS_AESGCM_TAG_SIZE) {
         /* the header-protection mask of a sample inside the sealed output, computed in the seal's round trip (fusion
          * computes it inside the seal, lib/fusion.c:425-430,636-651) */
         struct mi355x_ctr_context *hp = (struct mi355x_ctr_context *)supp->ctx;
-        if (ptls_mi355x_encrypt_s(ctx->ks, 0, output, input, inlen, seq, aad, aadlen, hp->ks, 0,
+        if (ptls_mi355x_encrypt_s(ks, 0, output, input, inlen, seq, aad, aadlen, hp->ks, 0,
                                   (size_t)((const uint8_t *)supp->input - (const uint8_t *)output), supp->output) != 0)
             seal_failed(output, inlen, supp);
         return;
     }
-    if (ptls_mi355x_encrypt(ctx->ks, 0, output, input, inlen, seq, aad, aadlen) != 0) {
+    if (ptls_mi355x_encrypt(ks, 0, output, input, inlen, seq, aad, aadlen) != 0) {
         seal_failed(output, inlen, supp);
         return;
     }
@@ -174,6 +174,12 @@ static void aead_do_encrypt(ptls_aead_context_t *_ctx, void *output, const void 
         memset(supp->output, 0, sizeof(supp->output));
         supp->ctx->do_transform(supp->ctx, supp->output, supp->output, sizeof(supp->output));
     }
+}
+
+static void aead_do_encrypt(ptls_aead_context_t *_ctx, void *output, const void *input, size_t inlen, uint64_t seq,
+                            const void *aad, size_t aadlen, ptls_aead_supplementary_encryption_t *supp)
+{
+    seal_one(((struct mi355x_aead_context *)_ctx)->ks, output, input, inlen, seq, aad, aadlen, supp);
 }
 
 static void aead_do_encrypt_v(ptls_aead_context_t *_ctx, void *output, ptls_iovec_t *input, size_t incnt, uint64_t seq,
@@ -282,6 +288,137 @@ ptls_cipher_algorithm_t ptls_mi355x_quiclb = {"QUICLB", PTLS_QUICLB_KEY_SIZE, PT
 ptls_mi355x_keyset_t *ptls_mi355x_aead_get_keyset(ptls_aead_context_t *ctx)
 {
     return ((struct mi355x_aead_context *)ctx)->ks;
+}
+
+/* ------------------------------------------------------------------ raw contexts (include/picotls/fusion.h:40-94) */
+
+struct ptls_mi355x_aesgcm_context {
+    ptls_mi355x_keyset_t *ks; /* key 0; its IV holds the first 4 nonce bytes of the last call, the rest zero */
+    uint8_t iv_hi[4];
+    size_t capacity;
+    uint8_t *bounce; /* decrypt: ciphertext || tag, contiguous as the engine's open takes them (capacity + 16 bytes) */
+};
+
+ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_new(const void *key, size_t key_size, size_t capacity)
+{
+    static const uint8_t zero_iv[PTLS_AESGCM_IV_SIZE] = {0};
+    ptls_mi355x_aesgcm_context_t *ctx = calloc(1, sizeof(*ctx));
+    if (ctx == NULL)
+        return NULL;
+    if ((ctx->bounce = malloc(capacity + PTLS_AESGCM_TAG_SIZE)) == NULL ||
+        (ctx->ks = ptls_mi355x_keyset_new(key, zero_iv, 1, key_size)) == NULL ||
+        ptls_mi355x_keyset_set_constant_time(ctx->ks, aead_constant_time()) != 0) {
+        ptls_mi355x_aesgcm_free(ctx);
+        return NULL;
+    }
+    ctx->capacity = capacity;
+    return ctx;
+}
+
+ptls_mi355x_aesgcm_context_t *ptls_mi355x_aesgcm_set_capacity(ptls_mi355x_aesgcm_context_t *ctx, size_t capacity)
+{
+    if (capacity <= ctx->capacity)
+        return ctx;
+    uint8_t *b = malloc(capacity + PTLS_AESGCM_TAG_SIZE);
+    if (b == NULL)
+        return NULL;
+    ptls_clear_memory(ctx->bounce, ctx->capacity + PTLS_AESGCM_TAG_SIZE);
+    free(ctx->bounce);
+    ctx->bounce = b;
+    ctx->capacity = capacity;
+    return ctx;
+}
+
+void ptls_mi355x_aesgcm_free(ptls_mi355x_aesgcm_context_t *ctx)
+{
+    if (ctx == NULL)
+        return;
+    if (ctx->ks != NULL)
+        ptls_mi355x_keyset_free(ctx->ks);
+    if (ctx->bounce != NULL) {
+        ptls_clear_memory(ctx->bounce, ctx->capacity + PTLS_AESGCM_TAG_SIZE);
+        free(ctx->bounce);
+    }
+    ptls_clear_memory(ctx, sizeof(*ctx));
+    free(ctx);
+}
+
+/* fusion's counter register as stored -> the engine's (IV, seq) form: nonce byte i is ctr byte 15 - i; the keyset IV
+ * carries nonce bytes 0-3 (updated on device only when they change: a connection's static IV keeps them), seq the
+ * big-endian nonce bytes 4-11, and iv ^ (0^32 || BE64(seq)) is the nonce again (lib/picotls.c:6587-6601) */
+static int raw_nonce(ptls_mi355x_aesgcm_context_t *ctx, const void *ctr, uint64_t *seq)
+{
+    const uint8_t *c = ctr;
+    uint8_t nonce[PTLS_AESGCM_IV_SIZE];
+    for (int i = 0; i < PTLS_AESGCM_IV_SIZE; ++i)
+        nonce[i] = c[15 - i];
+    if (memcmp(nonce, ctx->iv_hi, 4) != 0) {
+        uint8_t iv[PTLS_AESGCM_IV_SIZE] = {0};
+        memcpy(iv, nonce, 4);
+        if (ptls_mi355x_keyset_set_iv(ctx->ks, 0, iv) != 0)
+            return -1;
+        memcpy(ctx->iv_hi, nonce, 4);
+    }
+    uint64_t s = 0;
+    for (int i = 4; i < PTLS_AESGCM_IV_SIZE; ++i)
+        s = s << 8 | nonce[i];
+    *seq = s;
+    return 0;
+}
+
+void ptls_mi355x_aesgcm_encrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, const void *input, size_t inlen,
+                                const void *ctr, const void *aad, size_t aadlen, ptls_aead_supplementary_encryption_t *supp)
+{
+    uint64_t seq;
+    if (inlen + aadlen > ctx->capacity || raw_nonce(ctx, ctr, &seq) != 0) { /* fusion asserts the capacity */
+        seal_failed(output, inlen, supp);
+        return;
+    }
+    seal_one(ctx->ks, output, input, inlen, seq, aad, aadlen, supp);
+}
+
+int ptls_mi355x_aesgcm_decrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, const void *input, size_t inlen,
+                               const void *ctr, const void *aad, size_t aadlen, const void *tag)
+{
+    uint64_t seq;
+    const uint8_t *c = ctr;
+    if ((c[0] | c[1] | c[2] | c[3]) != 0) {
+        /* fusion's decrypt counts from the low 32 bits (lib/fusion.c:680; its encrypt sets them to 1), so a record of
+         * either encrypt fails its tag; the engine's counter starts at 1, so nothing is decrypted here */
+        memset(output, 0, inlen);
+        return 0;
+    }
+    if (inlen + aadlen > ctx->capacity || raw_nonce(ctx, ctr, &seq) != 0)
+        return 0;
+    memcpy(ctx->bounce, input, inlen);
+    memcpy(ctx->bounce + inlen, tag, PTLS_AESGCM_TAG_SIZE);
+    const size_t r = ptls_mi355x_decrypt(ctx->ks, 0, output, ctx->bounce, inlen + PTLS_AESGCM_TAG_SIZE, seq, aad, aadlen);
+    ptls_clear_memory(ctx->bounce, inlen + PTLS_AESGCM_TAG_SIZE);
+    return r == inlen;
+}
+
+int ptls_mi355x_aesecb_init(ptls_mi355x_aesecb_context_t *ctx, int is_enc, const void *key, size_t key_size)
+{
+    static const uint8_t zero_iv[PTLS_AESGCM_IV_SIZE] = {0};
+    ctx->ks = NULL;
+    if (!is_enc) /* fusion: assert(is_enc && "decryption is not supported (yet)"), lib/fusion.c */
+        return PTLS_ERROR_NOT_AVAILABLE;
+    if ((ctx->ks = ptls_mi355x_keyset_new(key, zero_iv, 1, key_size)) == NULL)
+        return PTLS_ERROR_LIBRARY;
+    return 0;
+}
+
+void ptls_mi355x_aesecb_dispose(ptls_mi355x_aesecb_context_t *ctx)
+{
+    if (ctx->ks != NULL)
+        ptls_mi355x_keyset_free(ctx->ks);
+    ctx->ks = NULL;
+}
+
+void ptls_mi355x_aesecb_encrypt(ptls_mi355x_aesecb_context_t *ctx, void *dst, const void *src)
+{
+    if (ptls_mi355x_encrypt_block(ctx->ks, 0, dst, src) != 0)
+        engine_fatal("AES-ECB block");
 }
 
 ptls_cipher_algorithm_t ptls_mi355x_aes128ctr = {"AES128-CTR", PTLS_AES128_KEY_SIZE, 1, PTLS_AES_IV_SIZE,

@@ -562,6 +562,85 @@ static int failclosed_main(void)
     return nfail == 0 ? 0 : 1;
 }
 
+/* the raw context API against fusion's (include/picotls/fusion.h:40-94): the same __m128i counter (stored to bytes for
+ * ours), random low 32 bits (ignored by both), capacity growth, tampering, a new static IV half-way, and AES-ECB */
+static void raw_context_test(size_t key_size)
+{
+    static uint8_t text[70000], aad[300], out_f[70000 + 16], out_m[70000 + 16], dec[70000];
+    uint8_t key[32];
+    rnd(key, sizeof(key));
+    ptls_fusion_aesgcm_context_t *f = ptls_fusion_aesgcm_new(key, key_size, 2048);
+    ptls_mi355x_aesgcm_context_t *m = ptls_mi355x_aesgcm_new(key, key_size, 2048);
+    OK(f != NULL && m != NULL, "raw: aesgcm_new (key %zu)", key_size);
+    if (f == NULL || m == NULL)
+        return;
+    static const size_t lens[] = {0, 1, 15, 16, 17, 100, 1200, 2000, 16384, 69999};
+    for (size_t i = 0; i < sizeof(lens) / sizeof(lens[0]); ++i) {
+        const size_t len = lens[i], aadlen = (i * 29) % 300;
+        if (len + aadlen > 2048 && i % 2 == 0) {
+            f = ptls_fusion_aesgcm_set_capacity(f, len + aadlen);
+            m = ptls_mi355x_aesgcm_set_capacity(m, len + aadlen);
+            OK(f != NULL && m != NULL, "raw: set_capacity %zu", len + aadlen);
+        } else if (len + aadlen > 2048) {
+            f = ptls_fusion_aesgcm_set_capacity(f, 70000 + 300);
+            m = ptls_mi355x_aesgcm_set_capacity(m, 70000 + 300);
+        }
+        /* the counter as calc_counter builds it (lib/fusion.c:1126-1133): low 32 bits zero, the nonce byte-reversed above */
+        uint8_t ctrb[16];
+        rnd(ctrb, sizeof(ctrb));
+        if (i >= 5) /* a connection's static IV: the nonce's first 4 bytes stay, the rest follows the sequence number */
+            memset(ctrb + 12, 0x5a, 4);
+        rnd(text, len), rnd(aad, aadlen);
+        /* encrypt ignores the low 32 bits (fusion sets them to 1, lib/fusion.c:489): random ones give the same record */
+        ptls_fusion_aesgcm_encrypt(f, out_f, text, len, _mm_loadu_si128((const __m128i *)ctrb), aad, aadlen, NULL);
+        memset(ctrb, 0, 4);
+        __m128i ctr = _mm_loadu_si128((const __m128i *)ctrb);
+        ptls_mi355x_aesgcm_encrypt(m, out_m, text, len, ctrb, aad, aadlen, NULL);
+        OK(memcmp(out_f, out_m, len + 16) == 0, "raw: encrypt equals fusion (key %zu, len %zu, aad %zu)", key_size, len, aadlen);
+        memset(dec, 0, len);
+        OK(ptls_mi355x_aesgcm_decrypt(m, dec, out_f, len, ctrb, aad, aadlen, out_f + len) == 1 && memcmp(dec, text, len) == 0,
+           "raw: decrypt of fusion's record (len %zu)", len);
+        OK(ptls_fusion_aesgcm_decrypt(f, dec, out_m, len, ctr, aad, aadlen, out_m + len) == 1 && memcmp(dec, text, len) == 0,
+           "raw: fusion decrypts ours (len %zu)", len);
+        {   /* decrypt with nonzero low counter bits: fusion's counts from them (lib/fusion.c:680), so the tag fails */
+            uint8_t c2[16];
+            memcpy(c2, ctrb, 16), c2[0] = 1 + (uint8_t)i;
+            OK(ptls_fusion_aesgcm_decrypt(f, dec, out_f, len, _mm_loadu_si128((const __m128i *)c2), aad, aadlen, out_f + len) == 0 &&
+                   ptls_mi355x_aesgcm_decrypt(m, dec, out_f, len, c2, aad, aadlen, out_f + len) == 0,
+               "raw: decrypt with nonzero low counter bits fails in both (len %zu)", len);
+        }
+        out_f[len + (i % 16)] ^= 0x10; /* a tag bit */
+        OK(ptls_mi355x_aesgcm_decrypt(m, dec, out_f, len, ctrb, aad, aadlen, out_f + len) == 0, "raw: bad tag rejected (len %zu)", len);
+        out_f[len + (i % 16)] ^= 0x10;
+        if (len != 0) {
+            out_f[len / 2] ^= 1;
+            uint8_t *df = malloc(len), *dm = malloc(len);
+            const int rf = ptls_fusion_aesgcm_decrypt(f, df, out_f, len, ctr, aad, aadlen, out_f + len);
+            const int rm = ptls_mi355x_aesgcm_decrypt(m, dm, out_f, len, ctrb, aad, aadlen, out_f + len);
+            OK(rf == 0 && rm == 0 && memcmp(df, dm, len) == 0, "raw: tampered ciphertext rejected, plaintext written as fusion's (len %zu)", len);
+            free(df), free(dm);
+            out_f[len / 2] ^= 1;
+        }
+    }
+    ptls_fusion_aesgcm_free(f);
+    ptls_mi355x_aesgcm_free(m);
+
+    ptls_fusion_aesecb_context_t fe;
+    ptls_mi355x_aesecb_context_t me;
+    ptls_fusion_aesecb_init(&fe, 1, key, key_size, 0);
+    OK(ptls_mi355x_aesecb_init(&me, 1, key, key_size) == 0, "raw: aesecb_init");
+    OK(ptls_mi355x_aesecb_init(&(ptls_mi355x_aesecb_context_t){NULL}, 0, key, key_size) != 0, "raw: aesecb decryption refused");
+    for (int i = 0; i < 4; ++i) {
+        uint8_t in[16], bf[16], bm[16];
+        rnd(in, sizeof(in));
+        ptls_fusion_aesecb_encrypt(&fe, bf, in);
+        ptls_mi355x_aesecb_encrypt(&me, bm, in);
+        OK(memcmp(bf, bm, 16) == 0, "raw: aesecb block equals fusion (key %zu)", key_size);
+    }
+    ptls_fusion_aesecb_dispose(&fe);
+    ptls_mi355x_aesecb_dispose(&me);
+}
+
 int main(int argc, char **argv)
 {
     if (!ptls_fusion_is_supported_by_cpu()) {
@@ -574,6 +653,12 @@ int main(int argc, char **argv)
         return stress_main(atoi(argv[2]));
     if (argc > 1 && strcmp(argv[1], "lasterr") == 0)
         return lasterr_main();
+    if (argc > 1 && strcmp(argv[1], "raw") == 0) {
+        raw_context_test(16);
+        raw_context_test(32);
+        printf("1..%d\n# %d failed\n", ntest, nfail);
+        return nfail == 0 ? 0 : 1;
+    }
     OK(strcmp(ptls_mi355x_aes128gcm.name, ptls_fusion_aes128gcm.name) == 0 && ptls_mi355x_aes128gcm.key_size == 16 &&
            ptls_mi355x_aes128gcm.iv_size == 12 && ptls_mi355x_aes128gcm.tag_size == 16 &&
            ptls_mi355x_aes128gcm.confidentiality_limit == ptls_fusion_aes128gcm.confidentiality_limit &&
@@ -590,6 +675,8 @@ int main(int argc, char **argv)
         ptls_aead_free(c);
     }
     ecb_kat();
+    raw_context_test(16);
+    raw_context_test(32);
     pair_test(&ptls_fusion_aes128gcm, &ptls_mi355x_aes128gcm, "aes128gcm fusion<->mi355x", 60);
     pair_test(&ptls_fusion_aes256gcm, &ptls_mi355x_aes256gcm, "aes256gcm fusion<->mi355x", 60);
     iv96_test(&ptls_mi355x_aes128gcm);

@@ -730,6 +730,22 @@ def test_picotls_vtable_tls12_with_handled_errors_left_on_the_thread():
     assert "not ok" not in r.stdout and "# 0 failed" in r.stdout
 
 
+def test_raw_context_api_vs_fusion():
+    """The counterparts of fusion's raw context API (include/picotls/mi355x_picotls.h ptls_mi355x_aesgcm_* /
+    ptls_mi355x_aesecb_*; include/picotls/fusion.h:40-94), driven beside ptls_fusion_aesgcm_* with the same __m128i
+    counter: records of 0-69,999 bytes with AADs to 290 bytes, both key sizes, capacity growth, decryption of each
+    other's records, bad tags and tampered ciphertext (plaintext written as fusion's), AES-ECB blocks (tests/c/test_vtable.c
+    raw_context_test)."""
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c", "_bin", "test_vtable")
+    if not os.path.exists(exe):
+        pytest.skip("tests/c/_bin/test_vtable not built (needs picotls headers at build time)")
+    r = subprocess.run([exe, "raw"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    assert "not ok" not in r.stdout and "# 0 failed" in r.stdout
+
+
 def test_picotls_vtable_pairs_copy_path():
     # the whole vtable suite with the staging round trip copying through device memory (PTLS_MI355X_STAGE_COPY=1)
     import subprocess
