@@ -203,6 +203,12 @@ __device__ __forceinline__ u32 lane_here()
 #ifndef W8_LEAN_STEP
 #define W8_LEAN_STEP 0
 #endif
+// (round 5) 4-lane groups store a line's two 64-byte halves together: a lane holds the first half's block one steady
+// step and stores it beside the second (segment.h). Half lines stored a step apart leave the L2 as two write-backs of
+// the line (tools/mb/wcal.hip: 1.07-1.08x the bytes; paired, 1.00x)
+#ifndef G4_PAIR_STORES
+#define G4_PAIR_STORES 1
+#endif
 #define W8_H8_BASE (W8_SWAP ? 0u : (u32)LDS_AES_BYTES)   // the W8 kernels' 8-bit H^8 table
 #define W8_AES_BASE (W8_SWAP ? (u32)LDS_AES_BYTES : 0u)  // ... and their AES T-tables
 #define W8_RUN_UNITS 512  // units per run of a launch pair (both kernels: their runs must be the same)

@@ -240,6 +240,10 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             const int b0 = (int)(j + G * (m_lo + (u32)sa)) - D0;  // this lane's text block at step sa
             u32 off = 16u * (u32)b0;                               // its byte offset in the text
             u32 ctr = (u32)b0 + 2;
+            // G4_PAIR_STORES: the block held from the previous step (the first half of its line), stored with this one
+            constexpr bool PAIR = G4_PAIR_STORES && G == 4;
+            u32x4 held = {0, 0, 0, 0};
+            bool have = false;
             for (int s = sa; s < sb; ++s) {
                 cur = nxt[0];
                 nxt[0] = *(const u32x4_u *)(src + off + 16 * G);
@@ -251,7 +255,19 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                 aes_ctr_cached1<NR>(lds, laneoff, rk, cc1, st);
                 __builtin_amdgcn_sched_barrier(0);
                 const u32x4 o = cur ^ u32x4{st[0][0], st[0][1], st[0][2], st[0][3]};
-                *(u32x4_u *)(dst + off) = o;
+                if constexpr (PAIR) {
+                    if ((((uintptr_t)(dst + off)) & 64u) == 0 && s + 1 < sb) {
+                        held = o;
+                        have = true;
+                    } else {
+                        if (have)
+                            *(u32x4_u *)(dst + off - 16 * G) = held;
+                        *(u32x4_u *)(dst + off) = o;
+                        have = false;
+                    }
+                } else {
+                    *(u32x4_u *)(dst + off) = o;
+                }
                 __builtin_amdgcn_sched_barrier(0);
                 if constexpr (W8)
                     acc = gmul8(lds, acc ^ (OPEN ? cur : o), GMUL8_LANE(), w8);
@@ -261,7 +277,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                 ctr += G;
                 off += 16 * G;
             }
-            s0 = (u32)sb;
+            s0 = (u32)sb;  // (PAIR: a first half in the range's last step was stored at once, nothing is held past it)
         }
 #if W8_LEAN_STEP
         if constexpr (W8 && FRAME == 0) {

@@ -112,6 +112,50 @@ ab)
   done
   exit 0
   ;;
+wcal)
+  # (round 5) WRITE_SIZE / FETCH_SIZE against known byte counts for the engine's access shapes (tools/mb/wcal.hip):
+  # wave-wide 16 B per lane, 128-byte lines per 8-lane group, 64-byte half lines per quad; 1M packed 1216-byte records
+  # (the QUIC batch's sealed records) and 1280-byte ones (line multiples), with and without work between steps
+  (
+R=$GRAFT_REPO_ROOT; cd /tmp && export TMPDIR=/tmp
+run() {  # name, counter, wcal args
+  timeout -k 10 120 rocprofv3 --pmc $2 --output-format csv -d $R/gpurun_out/wcal/$1 -o p -- $R/tools/mb/wcal.bin ${@:3} > $R/gpurun_out/wcal/$1.log 2>&1
+  rc=$?; echo "$1 rc=$rc"; [ $rc -ne 0 ] && { tail -5 $R/gpurun_out/wcal/$1.log; exit $rc; }
+}
+mkdir -p $R/gpurun_out/wcal
+if [ "$1" = 2 ]; then  # (second pass: non-temporal and paired halves, longer gaps; the TCC request counters)
+  timeout -k 10 60 rocprofv3 -L > $R/gpurun_out/wcal/counters_avail.txt 2>&1
+  for m in 1 2 3 4; do for sp in 200 2000; do
+    run st_m${m}_1216_s$sp WRITE_SIZE $m 0 1048576 1216 $sp 2
+    run ld_m${m}_1216_s$sp FETCH_SIZE $m 1 1048576 1216 $sp 2
+  done; done
+else
+for m in 0 1 2; do for sp in 0 200; do
+  run st_m${m}_1216_s$sp WRITE_SIZE $m 0 1048576 1216 $sp 3
+  run ld_m${m}_1216_s$sp FETCH_SIZE $m 1 1048576 1216 $sp 3
+done; done
+run st_m2_1280_s200 WRITE_SIZE 2 0 1048576 1280 200 3
+run ld_m2_1280_s200 FETCH_SIZE 2 1 1048576 1280 200 3
+fi
+cd $R
+python3 tools/wcal_summary.py gpurun_out/wcal > gpurun_out/wcal$1.txt; cat gpurun_out/wcal$1.txt; grep -E "TCC_EA0_(RD|WR)REQ" gpurun_out/wcal/counters_avail.txt | head -20
+exit 0
+  )
+  ;;
+wpmc)
+  # (round 5) WRITE_SIZE and FETCH_SIZE of one workload's seal/open launches per engine variant (tools/gv/<name>):
+  #   bash tools/gpu_r5.sh wpmc "base pair" quic1200 4194304
+  (
+R=$GRAFT_REPO_ROOT; cd /tmp && export TMPDIR=/tmp
+mkdir -p $R/gpurun_out/wpmc
+for n in $1; do for c in WRITE_SIZE FETCH_SIZE; do
+  timeout -k 10 240 rocprofv3 --pmc $c --output-format csv -d $R/gpurun_out/wpmc/${n}_$c -o p -- python3 $R/tools/ab.py $R/tools/gv/$n/libptls_mi355x.so --workload $2 --records $3 --rounds 1 --reps 1 > $R/gpurun_out/wpmc/${n}_$c.log 2>&1
+  rc=$?; echo "$n $c rc=$rc"; [ $rc -ne 0 ] && { tail -5 $R/gpurun_out/wpmc/${n}_$c.log; exit $rc; }
+done; done
+cd $R; python3 tools/wpmc_summary.py gpurun_out/wpmc $2 $3 > gpurun_out/wpmc_$2.txt; cat gpurun_out/wpmc_$2.txt
+exit 0
+  )
+  ;;
 *)
   echo "unknown recipe $recipe"; exit 2 ;;
 esac

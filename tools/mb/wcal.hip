@@ -1,0 +1,142 @@
+// tools/mb/wcal.hip -- calibration of rocprofv3's WRITE_SIZE / FETCH_SIZE for the engine's store and load shapes
+// (MI355X guide: "other access widths are uncalibrated"). Records of LEN bytes packed back to back (16-byte aligned,
+// like the 1200-byte QUIC batch's 1216-byte sealed records); each record's bytes are written once (or read once) by
+//   mode 0: a wave-wide stream, 16 B per lane, 1024 contiguous bytes per instruction (the guide's calibrated shape)
+//   mode 1: an 8-lane group per record, one 128-byte line per step (the 8-lane kernels' aligned streams)
+//   mode 2: a 4-lane quad per record, one 64-byte half line per step (the 4-lane groups of round 5)
+//   mode 3: mode 2 with non-temporal loads and stores
+//   mode 4: mode 2 with a line's two halves accessed together: a store held one step and issued beside the next
+//           one, both halves of a line loaded in its first step
+// with SPIN dependent VALU operations between steps (the AES work between a group's stores in the real kernel).
+//   hipcc --offload-arch=gfx950 -O3 tools/mb/wcal.hip -o tools/mb/wcal.bin
+//   wcal <mode 0..4> <load 0|1> <records> <len> <spin> <reps>
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+typedef unsigned int u32;
+typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+
+template <int GL, int V = 0>  // lanes per record (0: wave-wide stream); V 1 non-temporal, 2 paired halves
+__global__ __launch_bounds__(256) void wcal(unsigned char *buf, unsigned long long nrec, u32 len, u32 spin, int load,
+                                            u32 *sink)
+{
+    const u32 lane = threadIdx.x & 63;
+    u32 acc = lane;
+    if (GL == 0) {
+        const unsigned long long total = nrec * len / 16;
+        for (unsigned long long i = blockIdx.x * 256ull + threadIdx.x; i < total; i += (unsigned long long)gridDim.x * 256) {
+            u32x4 *p = (u32x4 *)(buf + 16 * i);
+            if (load) {
+                const u32x4 v = *p;
+                acc += v.x ^ v.y ^ v.z ^ v.w;
+            } else {
+                *p = u32x4{acc, acc + 1, acc + 2, acc + 3};
+            }
+            for (u32 k = 0; k < spin; ++k)
+                acc = acc * 1664525u + 1013904223u;
+        }
+    } else {
+        const u32 j = lane % GL;
+        const unsigned long long groups = (unsigned long long)gridDim.x * (256 / GL);
+        for (unsigned long long r = (blockIdx.x * 256ull + threadIdx.x) / GL; r < nrec; r += groups) {
+            const unsigned long long s = r * len, e = s + len;
+            const unsigned long long c0 = s / (16 * GL), c1 = (e + 16 * GL - 1) / (16 * GL);
+            u32x4 held = {0, 0, 0, 0};
+            bool have = false;
+            for (unsigned long long c = c0; c < c1; ++c) {
+                const unsigned long long a = c * 16 * GL + 16 * j;
+                const bool in = a >= s && a < e;
+                u32x4 *p = (u32x4 *)(buf + a);
+                if (V == 2) {
+                    // (half lines: c even = a line's first half, c odd its second)
+                    if (load) {
+                        if ((c & 1) == 0 || c == c0) {
+                            const unsigned long long a2 = (c | 1) * 16 * GL + 16 * j;
+                            u32x4 v = in ? *p : u32x4{0, 0, 0, 0};
+                            if ((c & 1) == 0 && a2 >= s && a2 < e)
+                                held = *(u32x4 *)(buf + a2);
+                            acc += v.x ^ v.y ^ v.z ^ v.w;
+                        } else {
+                            acc += held.x ^ held.y ^ held.z ^ held.w;
+                        }
+                    } else {
+                        const u32x4 o = u32x4{acc, acc + 1, acc + 2, acc + 3};
+                        if ((c & 1) == 0 && c + 1 < c1) {  // hold the first half
+                            held = o;
+                            have = in;
+                        } else {
+                            if (have)
+                                *(u32x4 *)(buf + a - 16 * GL) = held;
+                            if (in)
+                                *p = o;
+                            have = false;
+                        }
+                    }
+                } else if (in) {
+                    if (load) {
+                        const u32x4 v = V == 1 ? __builtin_nontemporal_load(p) : *p;
+                        acc += v.x ^ v.y ^ v.z ^ v.w;
+                    } else {
+                        const u32x4 o = u32x4{acc, acc + 1, acc + 2, acc + 3};
+                        if (V == 1)
+                            __builtin_nontemporal_store(o, p);
+                        else
+                            *p = o;
+                    }
+                }
+                for (u32 k = 0; k < spin; ++k)
+                    acc = acc * 1664525u + 1013904223u;
+            }
+        }
+    }
+    if (acc == 0x12345678u)
+        sink[0] = acc;
+}
+
+int main(int argc, char **argv)
+{
+    if (argc < 7) {
+        fprintf(stderr, "usage: wcal <mode 0..4> <load 0|1> <records> <len> <spin> <reps>\n");
+        return 2;
+    }
+    const int mode = atoi(argv[1]), load = atoi(argv[2]), reps = atoi(argv[6]);
+    const unsigned long long nrec = strtoull(argv[3], 0, 10);
+    const u32 len = (u32)atoi(argv[4]), spin = (u32)atoi(argv[5]);
+    if (len % 16 != 0 || mode < 0 || mode > 4 || nrec == 0 || nrec * len > (16ull << 30)) {
+        fprintf(stderr, "bad arguments\n");
+        return 2;
+    }
+    unsigned char *buf;
+    u32 *sink;
+    if (hipMalloc(&buf, nrec * len + 256) != hipSuccess || hipMalloc(&sink, 4) != hipSuccess)
+        return 1;
+    hipMemset(buf, 1, nrec * len + 256);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    const int grid = 256 * 8;
+    float best = 1e30f;
+    for (int i = 0; i < reps; ++i) {
+        hipEventRecord(e0, 0);
+        if (mode == 0)
+            wcal<0><<<grid, 256>>>(buf, nrec, len, spin, load, sink);
+        else if (mode == 1)
+            wcal<8><<<grid, 256>>>(buf, nrec, len, spin, load, sink);
+        else if (mode == 2)
+            wcal<4><<<grid, 256>>>(buf, nrec, len, spin, load, sink);
+        else if (mode == 3)
+            wcal<4, 1><<<grid, 256>>>(buf, nrec, len, spin, load, sink);
+        else
+            wcal<4, 2><<<grid, 256>>>(buf, nrec, len, spin, load, sink);
+        hipEventRecord(e1, 0);
+        if (hipEventSynchronize(e1) != hipSuccess)
+            return 1;
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        best = ms < best ? ms : best;
+    }
+    printf("mode %d load %d records %llu len %u spin %u: %.3f ms best, %.1f GB/s, bytes %llu\n", mode, load, nrec, len,
+           spin, best, nrec * len / best / 1e6, nrec * len);
+    return 0;
+}
