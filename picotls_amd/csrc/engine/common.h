@@ -209,6 +209,10 @@ __device__ __forceinline__ u32 lane_here()
 #ifndef G4_PAIR_STORES
 #define G4_PAIR_STORES 1
 #endif
+// ... and 8-lane groups whose steps straddle lines (cut runs' units) store each line in one step (segment.h)
+#ifndef G8_PAIR_STORES
+#define G8_PAIR_STORES 1
+#endif
 #define W8_H8_BASE (W8_SWAP ? 0u : (u32)LDS_AES_BYTES)   // the W8 kernels' 8-bit H^8 table
 #define W8_AES_BASE (W8_SWAP ? (u32)LDS_AES_BYTES : 0u)  // ... and their AES T-tables
 #define W8_RUN_UNITS 512  // units per run of a launch pair (both kernels: their runs must be the same)

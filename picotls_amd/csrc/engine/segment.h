@@ -244,6 +244,12 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             constexpr bool PAIR = G4_PAIR_STORES && G == 4;
             u32x4 held = {0, 0, 0, 0};
             bool have = false;
+            // G8_PAIR_STORES: a group whose steps straddle lines (a cut run's unit, counted from the stream's end) --
+            // the lanes past the line boundary (the same lanes every step) hold their blocks one step, so each line is
+            // stored by one step's instructions; uniform over the wave: no lane straddles in an aligned stream
+            const bool holder = G == 8 && ((u32)(uintptr_t)(dst + off) & 127u) < 16u * j;
+            // (unframed batches: the TLS-framed kernels measured slower with it, TLS 1.2 1200-byte seal -1.4 %)
+            const bool pair8 = G8_PAIR_STORES && G == 8 && W8 && FRAME == 0 && !aligned && __any(holder);
             for (int s = sa; s < sb; ++s) {
                 cur = nxt[0];
                 nxt[0] = *(const u32x4_u *)(src + off + 16 * G);
@@ -265,6 +271,14 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                         *(u32x4_u *)(dst + off) = o;
                         have = false;
                     }
+                } else if (pair8) {
+                    if (have)
+                        *(u32x4_u *)(dst + off - 16 * G) = held;
+                    have = holder && s + 1 < sb;
+                    if (have)
+                        held = o;
+                    else
+                        *(u32x4_u *)(dst + off) = o;
                 } else {
                     *(u32x4_u *)(dst + off) = o;
                 }
@@ -277,7 +291,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                 ctr += G;
                 off += 16 * G;
             }
-            s0 = (u32)sb;  // (PAIR: a first half in the range's last step was stored at once, nothing is held past it)
+            s0 = (u32)sb;  // (a block in the range's last step is stored at once: nothing is held past it)
         }
 #if W8_LEAN_STEP
         if constexpr (W8 && FRAME == 0) {
