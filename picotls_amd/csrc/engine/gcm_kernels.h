@@ -262,8 +262,11 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
     smax = wave_max(smax);
     // uniform run: every record is one unit (no partials), and a one-key batch may take a much longer run. A workgroup
     // with fewer records left than it has groups cuts them into units instead, so that a small batch (the per-record
-    // picotls path is a batch of one) spreads over the workgroup's waves.
-    const bool whole = smax <= smin + UNIFORM_SLACK && end - p >= WHOLE_MIN_RECS;
+    // picotls path is a batch of one) spreads over the workgroup's waves; so does a many-key run of fewer records than
+    // groups (round 5: the few records of a connection cut off at a workgroup's range edge were whole runs -- a few
+    // groups busy, the rest waiting -- and, when long, a W8 pair's EXT 3 run, for which that workgroup's EXT 3 kernel
+    // re-scanned all its runs: +2.7 ms per launch on 64K keys with uneven record counts)
+    const bool whole = smax <= smin + UNIFORM_SLACK && (args.multi_key ? (u64)n : end - p) >= WHOLE_MIN_RECS;
     if (whole && !args.multi_key)
         n = (u32)min(end - p, (u64)WHOLE_RUN_RECS);
     u32 units = n, nhuge = 0, log2 = args.unit_log2;

@@ -92,6 +92,7 @@ class Workload:
     key_order: str = "grouped"  # many keys: "grouped" by connection, or "random" (key_idx = splitmix(i) mod nkeys)
     sorted_lens: bool = False  # mixed lengths in ascending order over the batch (a batch built by record size)
     conn_classes: bool = False  # each connection (key) bulk (U[8 KiB, 16 KiB], one in four) or interactive (U[64, 1500])
+    scatter_mem: bool = False  # records keep their batch order but sit at random places in the arenas
 
     def scaled(self, nrecs: int) -> "Workload":
         return replace(self, nrecs=nrecs)
@@ -119,6 +120,20 @@ class Workload:
         i = np.arange(begin, end, dtype=np.uint64)
         if self.nkeys == 1:
             return np.zeros(end - begin, np.uint32), i
+        if self.key_order in ("sorted_random", "shuffled"):
+            # analysis orders: mixedrand's keys sorted (its uneven record counts per key, grouped in batch order), or
+            # mixed's exactly even counts in a random order
+            if self.key_order == "sorted_random":
+                allk = np.sort((splitmix_words_np(self.seed ^ 0x4B4958, 0, self.nrecs) % np.uint64(self.nkeys)).astype(np.uint32))
+            else:
+                even = (np.arange(self.nrecs, dtype=np.uint64) * np.uint64(self.nkeys) // np.uint64(self.nrecs)).astype(np.uint32)
+                allk = even[np.argsort(splitmix_words_np(self.seed ^ 0x534855, 0, self.nrecs), kind="stable")]
+            order = np.argsort(allk, kind="stable")
+            ks = allk[order]
+            starts = np.searchsorted(ks, ks, side="left")
+            seq = np.empty(self.nrecs, np.uint64)
+            seq[order] = (np.arange(self.nrecs) - starts).astype(np.uint64)
+            return allk[begin:end], seq[begin:end]
         if self.key_order == "random":
             # SURVEY §8(d) config 4 as written: key_idx = splitmix(i) mod nkeys over the whole batch, seq counting each
             # connection's records in batch order
@@ -135,7 +150,16 @@ class Workload:
 
     def descriptors(self, begin: int, end: int) -> RecordBatch:
         key, seq = self.key_and_seq(begin, end)
-        return RecordBatch.build(self.lens(begin, end), self.aad_len, seqs=seq, key_idx=key)
+        if not self.scatter_mem:
+            return RecordBatch.build(self.lens(begin, end), self.aad_len, seqs=seq, key_idx=key)
+        # the arenas laid out in a random order of the records, the descriptors in batch order: a run's records are as
+        # scattered over memory as the random key order scatters them, without the key grouping
+        perm = np.argsort(splitmix_words_np(self.seed ^ 0x534354, begin, end - begin), kind="stable")
+        b = RecordBatch.build(self.lens(begin, end)[perm], self.aad_len, seqs=seq[perm], key_idx=key[perm])
+        inv = np.empty(end - begin, np.int64)
+        inv[perm] = np.arange(end - begin)
+        b.seal, b.open = b.seal[inv], b.open[inv]
+        return b
 
     def keys(self) -> tuple[np.ndarray, np.ndarray]:
         kb = payload_np(self.seed ^ 0x4B4559, 0, self.nkeys * self.key_size).copy()
@@ -198,6 +222,12 @@ WORKLOADS = {
     "mixedconn": Workload("mixedconn", 4 << 20, None, 13, 32, nkeys=65536, conn_classes=True,
                           desc="4M records of 64K connections grouped, a quarter bulk (8-16 KiB records), the rest "
                                "interactive (64-1500 B), AES-256-GCM"),
+    "mixedscatter": Workload("mixedscatter", 4 << 20, None, 13, 32, nkeys=65536, scatter_mem=True,
+                             desc="mixed (keys grouped) with the records at random places in the arenas"),
+    "mixedpois": Workload("mixedpois", 4 << 20, None, 13, 32, nkeys=65536, key_order="sorted_random",
+                          desc="mixedrand's keys in sorted order (uneven record counts per key, grouped)"),
+    "mixedshuf": Workload("mixedshuf", 4 << 20, None, 13, 32, nkeys=65536, key_order="shuffled",
+                          desc="mixed's keys (64 records each) in a random order"),
     "tls16k256": Workload("tls16k256", 1 << 20, 16384, 5, 32, tls_header_aad=True,
                           desc="1M x 16384 B TLS records, AES-256-GCM, one key"),
     "u8k256": Workload("u8k256", 4 << 20, 8192, 13, 32, desc="4M x 8192 B records, AES-256-GCM, one key"),

@@ -33,7 +33,7 @@ def ref():
     return FusionRef()
 
 
-def _check(ref, rng, lens, aads, key_size, nkeys, tamper=8):
+def _check(ref, rng, lens, aads, key_size, nkeys, tamper=8, after_seal=None):
     n = len(lens)
     key_idx = np.sort(rng.integers(0, nkeys, n)) if nkeys > 1 else None
     b = RecordBatch.build(np.asarray(lens), np.asarray(aads), seqs=rng.integers(0, 2**62, n, dtype=np.uint64),
@@ -51,6 +51,8 @@ def _check(ref, rng, lens, aads, key_size, nkeys, tamper=8):
         want[int(b.seal[i]["out_off"]):int(b.seal[i]["out_off"]) + int(lens[i]) + 16])]
     assert bad_recs == [], f"{len(bad_recs)} records differ from fusion, first {bad_recs[:8]}"
     assert np.array_equal(sealed, want)
+    if after_seal is not None:
+        after_seal()
     # open fusion's records with tampering (ciphertext, tag, AAD bits); the plaintext is written either way, as fusion
     bad, badaad = want.copy(), aad.copy()
     victims = rng.choice(n, min(tamper, n), replace=False)
@@ -291,3 +293,24 @@ def test_w8_records_beyond_the_run_unit_cap_vs_fusion(ref):
     for k, ln in enumerate(big):
         lens[300 * k + 7] = ln
     _check(ref, rng, lens, rng.integers(0, 40, len(lens)), 32, 1, tamper=2)
+
+
+def test_w8_many_key_range_edges_stay_cut_vs_fusion(ref):
+    """A many-key batch with uneven record counts per key (sorted random keys, ~64 records each) is split among the
+    workgroups at tile edges that fall inside connections, so a workgroup's range can start or end with one or two
+    records of a key. Such a run is cut into units like any many-key run of fewer records than the workgroup has
+    groups (round 5: it was a whole run, and when long an EXT 3 run, for which that workgroup's EXT 3 kernel re-scanned
+    all its runs). 262,144 U[64, 16384] records over 4,096 AES-256 keys against fusion; the counters show no EXT 3
+    run in the seal or the open."""
+    rng = np.random.default_rng(8420)
+    n = 262144
+    seen = {}
+
+    def seal_done():
+        seen["seal"] = pa.debug_counters(reset=True)["runs"]
+
+    pa.debug_counters(reset=True)
+    _check(ref, rng, rng.integers(64, 16385, n), np.full(n, 13), 32, 4096, tamper=16, after_seal=seal_done)
+    opened = pa.debug_counters(reset=True)["runs"]
+    assert seen["seal"]["w8_tree"] == 0 and opened["w8_tree"] == 0, (seen, opened)
+    assert seen["seal"]["w8_serial"] >= 4096 and opened["w8_serial"] >= 4096, (seen, opened)
