@@ -105,6 +105,31 @@ def test_many_key_workload_orders():
     assert (np.diff(rand.astype(np.int64)) != 0).mean() > 0.9  # runs of one record: the device regroups these
 
 
+def test_mixed_analysis_workloads():
+    # (round 5) mixedpois: mixedrand's key counts grouped in batch order; mixedshuf: mixed's keys (equal
+    # counts) in random order; mixedscatter: mixed's records at random places in the arenas, descriptors in batch order
+    n = 20000
+    w = workloads.WORKLOADS
+    rand = w["mixedrand"].scaled(n).key_and_seq(0, n)[0]
+    pois = w["mixedpois"].scaled(n).key_and_seq(0, n)[0]
+    assert (pois == np.sort(rand)).all()
+    mixed = w["mixed"].scaled(n).key_and_seq(0, n)[0]
+    shuf, sseq = w["mixedshuf"].scaled(n).key_and_seq(0, n)
+    assert (np.sort(shuf) == mixed).all() and (np.diff(shuf.astype(np.int64)) != 0).mean() > 0.9
+    for k in np.unique(shuf)[:50]:
+        assert (sseq[shuf == k] == np.arange((shuf == k).sum())).all()
+    m = w["mixed"].scaled(n).descriptors(0, n)
+    sc = w["mixedscatter"].scaled(n).descriptors(0, n)
+    for f in ("len", "key_idx", "seq", "aad_len"):
+        assert (sc.seal[f] == m.seal[f]).all()
+    assert sc.pt_bytes == m.pt_bytes and sc.sealed_bytes == m.sealed_bytes
+    order = np.argsort(sc.seal["in_off"])
+    assert (np.diff(order) != 1).mean() > 0.9  # arena order is not batch order
+    ends = sc.seal["in_off"][order] + sc.seal["len"][order]
+    assert (ends[:-1] <= sc.seal["in_off"][order][1:]).all()  # still disjoint
+    assert (sc.open["in_off"] == sc.seal["out_off"]).all() and (sc.open["out_off"] == sc.seal["in_off"]).all()
+
+
 def test_lds_model_ceiling():
     import bench
 
