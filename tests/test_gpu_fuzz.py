@@ -76,3 +76,48 @@ def test_fuzz_batches_vs_fusion(ref, seed):
         o, ln = int(b.open[i]["out_off"]), int(lens[i])
         assert np.array_equal(plain[o:o + ln], pt[o:o + ln]), f"seed {seed} record {i}"
     ks.free()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_fuzz_w8_batches_odd_offsets_vs_fusion(ref, seed):
+    """Batches large enough for the W8 kernels (from 2048 records) with records at odd byte offsets (slot gaps of 1-47
+    bytes): the paired half-line and line stores of round 5 (4-lane groups, cut units) decide their pairs from the
+    output addresses, which then straddle lines by any amount. Seal bit-exact against fusion, open with tampering."""
+    rng = np.random.default_rng(9100 + seed)
+    n = int(rng.integers(2048, 12000))
+    nkeys = int(rng.choice([1, 3, 40, 500]))
+    key_size = int(rng.choice([16, 32]))
+    key_idx = np.sort(rng.integers(0, nkeys, n))
+    lens = _lengths(rng, n) if seed % 2 else rng.integers(900, 1400, n)  # (odd seeds: the mixed shapes; even: short)
+    aads = rng.integers(0, 40, n)
+    b = RecordBatch.build(lens, aads, seqs=rng.integers(0, 2**62, n, dtype=np.uint64), key_idx=key_idx,
+                          pt_gap=int(rng.integers(1, 48)), sealed_gap=int(rng.integers(1, 48)), aad_gap=int(rng.integers(0, 5)))
+    assert (b.seal["out_off"] % 16 != 0).any()
+    keys = np.frombuffer(rng.bytes(nkeys * key_size), np.uint8)
+    ivs = np.frombuffer(rng.bytes(nkeys * 12), np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(max(b.aad_bytes, 1)), np.uint8)
+    ks = pa.Keyset(keys, ivs, key_size)
+    sealed = gpu_seal(ks, b.seal, pt, aad, b.sealed_bytes)
+    expect = np.zeros(b.sealed_bytes, np.uint8)
+    ref.run_batch(True, keys, ivs, key_size, b.seal, pt, aad, expect, nthreads=8)
+    assert np.array_equal(sealed, expect), f"seed {seed}: n={n} nkeys={nkeys} key_size={key_size}"
+    victims = rng.choice(n, 5, replace=False)
+    bad = expect.copy()
+    for v in victims:
+        bad[int(b.seal[v]["out_off"]) + int(rng.integers(0, int(lens[v]) + 16))] ^= 0x04
+    plain, ok = gpu_open(ks, b.open, bad, aad, b.pt_bytes)
+    want_ok = np.ones(n, np.uint8)
+    want_ok[victims] = 0
+    assert np.array_equal(ok, want_ok), f"seed {seed}"
+    keep = np.ones(b.pt_bytes, bool)
+    for v in victims:
+        o = int(b.open[v]["out_off"])
+        keep[o:o + int(lens[v])] = False
+    mask = np.zeros(b.pt_bytes, bool)
+    for i in range(n):
+        o = int(b.open[i]["out_off"])
+        mask[o:o + int(lens[i])] = True
+    sel = mask & keep
+    assert np.array_equal(plain[sel], pt[sel]), f"seed {seed}"
+    ks.free()
