@@ -1272,7 +1272,7 @@ static u32 *w8_flags_locked(ptls_mi355x_keyset_t *ks, hipStream_t s)
     }
     if (v.size() < W8_FLAG_STREAMS) {
         u32 *f = nullptr;
-        if (hipMallocAsync((void **)&f, 4 * (size_t)ks->ds->ncu, s) != hipSuccess) {
+        if (hipMallocAsync((void **)&f, 4 * W8_FLAG_WORDS * (size_t)ks->ds->ncu, s) != hipSuccess) {
             (void)hipGetLastError();
             return nullptr;
         }

@@ -213,6 +213,11 @@ __device__ __forceinline__ u32 lane_here()
 #ifndef G8_PAIR_STORES
 #define G8_PAIR_STORES 1
 #endif
+// a W8 pair's flag block per workgroup (BatchArgs::w8_flags): [0] the runs EXT 4 left to EXT 3 (W8_SKIP_LIST + 1:
+// more than the list holds, or records past 2^32), then per listed run (walk order) its first record and the end of
+// the chunk that holds it
+#define W8_FLAG_WORDS 32
+#define W8_SKIP_LIST ((W8_FLAG_WORDS - 1) / 2)
 #define W8_H8_BASE (W8_SWAP ? 0u : (u32)LDS_AES_BYTES)   // the W8 kernels' 8-bit H^8 table
 #define W8_AES_BASE (W8_SWAP ? (u32)LDS_AES_BYTES : 0u)  // ... and their AES T-tables
 #define W8_RUN_UNITS 512  // units per run of a launch pair (both kernels: their runs must be the same)

@@ -778,15 +778,23 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     const u32 tsel_chunk = W8K ? (u32)W8_TAB_COMB : 0x10000u + 8u * GHASH_TABLE_BYTES;
 
     const u64 n = args.nrecs, C = args.bounds != nullptr ? 0 : args.chunk;
-    // the pair's second kernel (EXT 3): none of this workgroup's runs is its kind (the first kernel saw them all)
+    // the pair's second kernel (EXT 3): none of this workgroup's runs is its kind (the first kernel saw them all), or
+    // (round 5) the runs it left are listed, and this kernel visits just those (`slist`, `scnt`)
+    const u32 *slist = nullptr;
+    u32 scnt = 0;
     if constexpr (W8TREE) {
-        if (args.w8_split == 2 && args.w8_flags != nullptr && args.w8_flags[blockIdx.x] == 0)
-            return;
+        if (args.w8_split == 2 && args.w8_flags != nullptr) {
+            scnt = args.w8_flags[(u64)blockIdx.x * W8_FLAG_WORDS];
+            if (scnt == 0)
+                return;
+            if (scnt <= W8_SKIP_LIST)
+                slist = args.w8_flags + (u64)blockIdx.x * W8_FLAG_WORDS + 1;
+        }
     }
     unsigned long long *const kclock = blockIdx.x == 0 ? g_kclock_buf : nullptr;
     const u64 kc_t0 = kclock != nullptr ? __builtin_amdgcn_s_memtime() : 0ull;
     const u64 kc_r0 = kclock != nullptr ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    bool skipped_w8 = false;  // (the pair's first kernel: this workgroup left a run to the second one)
+    u32 skipped_w8 = 0;  // (the pair's first kernel: the runs this workgroup left to the second one)
     constexpr bool SPREAD = FRAME == 0 && EXT == 1;
     if constexpr (SPREAD) {  // a small one-key batch (spread_pieces): workgroup w < n takes record w unless it is long
         if (blockIdx.x >= n) {
@@ -796,9 +804,14 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     }
     // this workgroup's records: the chunk [beg, end) (cstart: its first record), then the chunk grid * C further on
     // (C != 0), or one contiguous range (C == 0): balanced by weight (args.bounds) or by count (spread: record w)
-    const u64 beg = SPREAD ? (u64)blockIdx.x : args.bounds != nullptr ? args.bounds[blockIdx.x] : C != 0 ? min(n, (u64)blockIdx.x * C) : n * blockIdx.x / gridDim.x;
+    u64 beg = SPREAD ? (u64)blockIdx.x : args.bounds != nullptr ? args.bounds[blockIdx.x] : C != 0 ? min(n, (u64)blockIdx.x * C) : n * blockIdx.x / gridDim.x;
     u64 end = SPREAD ? (u64)blockIdx.x + 1 : args.bounds != nullptr ? args.bounds[blockIdx.x + 1] : C != 0 ? min(n, beg + C) : n * (blockIdx.x + 1) / gridDim.x;
     u64 cstart = beg;
+    u32 sidx = 0;  // (EXT 3 with a run list) the listed run being processed
+    if constexpr (W8TREE) {
+        if (slist != nullptr)
+            beg = slist[0], end = slist[1];
+    }
     u32 loaded_key = 0xffffffffu, loaded_usrc = 0xffffffffu;
     u32 loaded_w8 = 0;  // the LDS holds the nine 4-bit tables (0) or the W8 map: serial segment ends (1), the tree (2)
     // the descriptors in batch order, or (an ungrouped many-key batch) the key-grouped copy built on the device; ok
@@ -891,6 +904,17 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             nxt = min(n, nxt_cstart);
             nxt_end = min(n, nxt_cstart + C);
         }
+        if constexpr (W8TREE) {
+            if (slist != nullptr) {  // the next listed run (none: the loop ends)
+                if (sidx + 1 < scnt) {
+                    nxt = slist[2 * sidx + 2];
+                    nxt_end = slist[2 * sidx + 3];
+                } else {
+                    nxt = nxt_end = 0;
+                }
+                ++sidx;
+            }
+        }
         PROF_STAMP(t1);
 
         // a W8 pair (w8_split 2): runs of long whole records (at least W8_MIN_STEPS steps) belong to the EXT 3 kernel,
@@ -899,7 +923,14 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             const bool tree = whole_run &&
                               __builtin_amdgcn_readfirstlane(gcm_steps<OPEN, FRAME>(recs[pos]) >= W8_MIN_STEPS ? 1u : 0u) != 0;
             if (tree != W8TREE) {
-                skipped_w8 = true;
+                if constexpr (!W8TREE) {  // (the pair's first kernel: the run's start into the list)
+                    const bool fits = end <= 0xffffffffull;
+                    if (args.w8_flags != nullptr && threadIdx.x == 0 && skipped_w8 < W8_SKIP_LIST && fits) {
+                        u32 *f = args.w8_flags + (u64)blockIdx.x * W8_FLAG_WORDS + 1 + 2 * skipped_w8;
+                        f[0] = (u32)pos, f[1] = (u32)end;
+                    }
+                    skipped_w8 = fits ? skipped_w8 + 1 : W8_SKIP_LIST + 1;
+                }
                 if (wave == 0 && nxt < nxt_end)
                     scan_run<OPEN, FRAME, false, EXT>(args, recs, nxt, nxt_end, rs_next);
                 __syncthreads();
@@ -1262,7 +1293,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         HP_PASS(hp_pos, hp_pos + hp_n, threadIdx.x, blockDim.x);
     if constexpr (W8K && !W8TREE) {  // the pair's first kernel, for the second (workgroup-uniform)
         if (args.w8_split == 2 && args.w8_flags != nullptr && threadIdx.x == 0)
-            args.w8_flags[blockIdx.x] = skipped_w8 ? 1u : 0u;
+            args.w8_flags[(u64)blockIdx.x * W8_FLAG_WORDS] = min(skipped_w8, (u32)W8_SKIP_LIST + 1);
     }
     if (kclock != nullptr && threadIdx.x == 0) {  // (vector stores and atomics only)
         const u64 t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();

@@ -100,9 +100,10 @@ struct BatchArgs {
     u32x4 *spread_part;
     u32 *spread_cnt;
     // chunked kernel, the W8 kernels (EXT 3, 4; launch_chunked): w8_split 1 = the EXT 4 kernel alone, 2 = a pair, in
-    // which EXT 4 takes every run but those of long whole records and EXT 3 (launched after it) those. w8_flags (grid
-    // words, optional): the pair's EXT 4 workgroup w sets word w to whether it left a run to EXT 3; the EXT 3
-    // workgroup w (same grid, same records) returns at once when it did not, instead of scanning every run again
+    // which EXT 4 takes every run but those of long whole records and EXT 3 (launched after it) those. w8_flags (grid x
+    // W8_FLAG_WORDS words, optional): the pair's EXT 4 workgroup w writes to its block how many runs it left to EXT 3
+    // and (round 5) where they start; the EXT 3 workgroup w (same grid, same records) returns at once when it left none,
+    // and visits just the listed runs when they fit the list, instead of scanning every run of its records again
     u32 w8_split;
     u32 *w8_flags;
     // the value each workgroup stores into done_flag[w] (the calling host thread's token for this call, never 0)

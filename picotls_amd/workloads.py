@@ -93,6 +93,7 @@ class Workload:
     sorted_lens: bool = False  # mixed lengths in ascending order over the batch (a batch built by record size)
     conn_classes: bool = False  # each connection (key) bulk (U[8 KiB, 16 KiB], one in four) or interactive (U[64, 1500])
     scatter_mem: bool = False  # records keep their batch order but sit at random places in the arenas
+    bulk_every: int = 0  # every bulk_every-th connection sends uniform 8200-byte records (whole runs of a W8 pair's EXT 3)
 
     def scaled(self, nrecs: int) -> "Workload":
         return replace(self, nrecs=nrecs)
@@ -112,7 +113,11 @@ class Workload:
             w = np.sort(splitmix_words_np(self.seed ^ 0x4C454E, 0, self.nrecs) % np.uint64(self.max_len - self.min_len + 1))
             return (np.uint64(self.min_len) + w[begin:end]).astype(np.uint64)
         w = splitmix_words_np(self.seed ^ 0x4C454E, begin, end - begin)
-        return (np.uint64(self.min_len) + w % np.uint64(self.max_len - self.min_len + 1)).astype(np.uint64)
+        lens = (np.uint64(self.min_len) + w % np.uint64(self.max_len - self.min_len + 1)).astype(np.uint64)
+        if self.bulk_every:
+            key, _ = self.key_and_seq(begin, end)
+            lens = np.where(key % self.bulk_every == 0, np.uint64(8200), lens).astype(np.uint64)
+        return lens
 
     def key_and_seq(self, begin: int, end: int) -> tuple[np.ndarray, np.ndarray]:
         """Single key: seq = record index. Many keys: records are grouped by connection (a server batches per
@@ -228,6 +233,9 @@ WORKLOADS = {
                           desc="mixedrand's keys in sorted order (uneven record counts per key, grouped)"),
     "mixedshuf": Workload("mixedshuf", 4 << 20, None, 13, 32, nkeys=65536, key_order="shuffled",
                           desc="mixed's keys (64 records each) in a random order"),
+    "mixedbulk": Workload("mixedbulk", 4 << 20, None, 13, 32, nkeys=16384, bulk_every=16,
+                          desc="4M records of 16K connections grouped (256 records each), every 16th a bulk transfer of "
+                               "uniform 8200-byte records, the rest U[64, 16384], AES-256-GCM"),
     "tls16k256": Workload("tls16k256", 1 << 20, 16384, 5, 32, tls_header_aad=True,
                           desc="1M x 16384 B TLS records, AES-256-GCM, one key"),
     "u8k256": Workload("u8k256", 4 << 20, 8192, 13, 32, desc="4M x 8192 B records, AES-256-GCM, one key"),

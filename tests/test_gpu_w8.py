@@ -314,3 +314,48 @@ def test_w8_many_key_range_edges_stay_cut_vs_fusion(ref):
     opened = pa.debug_counters(reset=True)["runs"]
     assert seen["seal"]["w8_tree"] == 0 and opened["w8_tree"] == 0, (seen, opened)
     assert seen["seal"]["w8_serial"] >= 4096 and opened["w8_serial"] >= 4096, (seen, opened)
+
+
+def test_w8_pair_run_list_vs_fusion(ref):
+    """A W8 pair's first kernel (EXT 4) lists where the runs it leaves to the second (EXT 3) start, and EXT 3 visits just
+    those (round 5; before, it re-scanned every run of its workgroup). 131,071 records (dealt chunks of 256, two per
+    workgroup, no weight balance) of 1,024 keys, 128 records each, alternating 8200-byte records (EXT 3's long whole
+    runs) and 1200-byte ones (EXT 4's whole runs in 4-lane groups): every workgroup leaves two runs to EXT 3. Against
+    fusion, sealed and opened with tampering; the counters show both kernels' runs."""
+    rng = np.random.default_rng(8430)
+    n = 131071
+    key = np.arange(n) // 128
+    lens = np.where(key % 2 == 0, 8200, 1200)
+    seen = {}
+
+    def seal_done():
+        seen["seal"] = pa.debug_counters(reset=True)
+
+    pa.debug_counters(reset=True)
+    b = RecordBatch.build(lens, np.full(n, 13), seqs=rng.integers(0, 2**62, n, dtype=np.uint64), key_idx=key)
+    nkeys = int(key.max()) + 1
+    keys = np.frombuffer(rng.bytes(nkeys * 16), np.uint8)
+    ivs = np.frombuffer(rng.bytes(nkeys * 12), np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(b.aad_bytes), np.uint8)
+    ks = pa.Keyset(keys, ivs, 16)
+    sealed = gpu_seal(ks, b.seal, pt, aad, b.sealed_bytes)
+    seal_done()
+    want = np.zeros(b.sealed_bytes, np.uint8)
+    ref.run_batch(True, keys, ivs, 16, b.seal, pt, aad, want, nthreads=8)
+    assert np.array_equal(sealed, want)
+    victims = rng.choice(n, 12, replace=False)
+    bad = want.copy()
+    for v in victims:
+        bad[int(b.open[v]["in_off"]) + int(rng.integers(0, int(lens[v]) + 16))] ^= 0x10
+    back, ok = gpu_open(ks, b.open, bad, aad, b.pt_bytes)
+    expect_ok = np.ones(n, np.uint8)
+    expect_ok[victims] = 0
+    assert np.array_equal(ok, expect_ok)
+    ref_back = np.zeros(b.pt_bytes, np.uint8)
+    ref.run_batch(False, keys, ivs, 16, b.open, bad, aad, ref_back, ok=np.zeros(n, np.uint8), nthreads=8)
+    assert np.array_equal(back, ref_back)
+    opened = pa.debug_counters(reset=True)
+    for c in (seen["seal"], opened):
+        assert c["launches"]["w8_tree"] == 1 and c["runs"]["w8_tree"] >= 500 and c["runs"]["w8_g4"] >= 500, c
+    ks.free()
