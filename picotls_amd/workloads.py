@@ -238,6 +238,8 @@ WORKLOADS = {
                                "uniform 8200-byte records, the rest U[64, 16384], AES-256-GCM"),
     "quic64k": Workload("quic64k", 4 << 20, 1200, 13, 16, nkeys=65536,
                         desc="4M x 1200 B QUIC packets of 64K connections (64 each, grouped), AES-128-GCM"),
+    "tls64k": Workload("tls64k", 1 << 20, 16384, 5, 16, tls_header_aad=True, nkeys=65536,
+                       desc="1M x 16384 B TLS records of 64K connections (16 each, grouped), AES-128-GCM"),
     "tls16k256": Workload("tls16k256", 1 << 20, 16384, 5, 32, tls_header_aad=True,
                           desc="1M x 16384 B TLS records, AES-256-GCM, one key"),
     "u8k256": Workload("u8k256", 4 << 20, 8192, 13, 32, desc="4M x 8192 B records, AES-256-GCM, one key"),
