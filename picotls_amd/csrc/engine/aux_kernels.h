@@ -7,8 +7,9 @@
 // A many-key batch whose records are not grouped by connection would give the chunked kernel one-record key runs, each
 // with its own table build and barrier (15 GiB/s on 4M records over 64K keys in random order against 724 grouped).
 // Small kernels group it on the device first: the number of key changes between neighbours (regroup when runs would
-// average under 8 records; a grouped batch stops here), key counts, their exclusive scan, and a scatter of record
-// indices into key order. The chunked kernel then walks the permutation; descriptors, outputs and ok bytes stay
+// average under 8 records, or (round 5) under 32 with at least two runs per key of the keyset: connections in bursts
+// of 9-10 records had run in 9-record runs at 510 GiB/s against 785 regrouped; a grouped batch stops here), key
+// counts, their exclusive scan, and a scatter of record indices into key order. The chunked kernel then walks the permutation; descriptors, outputs and ok bytes stay
 // at each record's own index, so the results are those of the batch order. ctl[0] = key changes, ctl[1] = regroup.
 #define KEY_GROUP_MAX_KEYS (1u << 20)
 
@@ -25,12 +26,18 @@ __global__ __launch_bounds__(256) void key_changes_kernel(const ptls_mi355x_reco
         atomicAdd(&ctl[0], changes);
 }
 
-__device__ __forceinline__ bool key_regroup(const u32 *ctl, u64 n) { return (u64)ctl[0] * 8 > n; }
+// (the key count bounds the distinct keys of the batch from above: more runs than twice that means keys recur, with
+// no per-key pass to find out; a batch over a few keys of a large keyset keeps its runs)
+__device__ __forceinline__ bool key_regroup(const u32 *ctl, u64 n, u32 nkeys)
+{
+    const u64 changes = ctl[0];
+    return changes * 8 > n || (changes >= 2 * (u64)nkeys && changes * 32 > n);
+}
 
 // key counts (only when regrouping): each thread counts a contiguous stretch of records and adds one count per key run
 __global__ __launch_bounds__(256) void key_hist_kernel(const ptls_mi355x_record_t *recs, u64 n, u32 nkeys, u32 *cnt, const u32 *ctl)
 {
-    if (!key_regroup(ctl, n))
+    if (!key_regroup(ctl, n, nkeys))
         return;
     const u64 nthr = (u64)gridDim.x * blockDim.x, t = (u64)blockIdx.x * blockDim.x + threadIdx.x;
     const u64 per = (n + nthr - 1) / nthr, i0 = min(n, t * per), i1 = min(n, i0 + per);
@@ -53,7 +60,7 @@ __global__ __launch_bounds__(256) void key_hist_kernel(const ptls_mi355x_record_
 __global__ __launch_bounds__(1024) void key_scan_kernel(u32 *cnt, u32 nb, u64 n, u32 *ctl)
 {
     __shared__ u32 wsum[16];
-    const bool regroup = key_regroup(ctl, n);
+    const bool regroup = key_regroup(ctl, n, nb - 1);
     if (threadIdx.x == 0)
         ctl[1] = regroup;
     if (!regroup)

@@ -125,6 +125,22 @@ class Workload:
         i = np.arange(begin, end, dtype=np.uint64)
         if self.nkeys == 1:
             return np.zeros(end - begin, np.uint32), i
+        if self.key_order.startswith("bursts"):
+            # analysis order: connections' records in bursts of B (key order "burstsB"): mixed's 64 records a key cut
+            # into bursts, the bursts in a random order over the batch
+            B = int(self.key_order[6:])
+            even = (np.arange(self.nrecs, dtype=np.uint64) * np.uint64(self.nkeys) // np.uint64(self.nrecs)).astype(np.uint32)
+            nb = (self.nrecs + B - 1) // B
+            border = np.argsort(splitmix_words_np(self.seed ^ 0x425253, 0, nb), kind="stable")
+            idx = (border[:, None] * B + np.arange(B)[None, :]).reshape(-1)
+            idx = idx[idx < self.nrecs]
+            allk = even[idx]
+            order = np.argsort(allk, kind="stable")
+            ks = allk[order]
+            starts = np.searchsorted(ks, ks, side="left")
+            seq = np.empty(self.nrecs, np.uint64)
+            seq[order] = (np.arange(self.nrecs) - starts).astype(np.uint64)
+            return allk[begin:end], seq[begin:end]
         if self.key_order in ("sorted_random", "shuffled"):
             # analysis orders: mixedrand's keys sorted (its uneven record counts per key, grouped in batch order), or
             # mixed's exactly even counts in a random order
@@ -240,6 +256,8 @@ WORKLOADS = {
                         desc="4M x 1200 B QUIC packets of 64K connections (64 each, grouped), AES-128-GCM"),
     "tls64k": Workload("tls64k", 1 << 20, 16384, 5, 16, tls_header_aad=True, nkeys=65536,
                        desc="1M x 16384 B TLS records of 64K connections (16 each, grouped), AES-128-GCM"),
+    "mixedburst": Workload("mixedburst", 4 << 20, None, 13, 32, nkeys=65536, key_order="bursts10",
+                           desc="mixed's 64 records a connection in bursts of 10, the bursts in random order"),
     "tls16k256": Workload("tls16k256", 1 << 20, 16384, 5, 32, tls_header_aad=True,
                           desc="1M x 16384 B TLS records, AES-256-GCM, one key"),
     "u8k256": Workload("u8k256", 4 << 20, 8192, 13, 32, desc="4M x 8192 B records, AES-256-GCM, one key"),

@@ -297,6 +297,56 @@ static void tls12_describe_diff(const char *what, const uint8_t *a, size_t alen,
     printf("# %s: streams of %zu and %zu bytes agree on their first %zu bytes (%zu records)\n", what, alen, blen, off, rec);
 }
 
+/* oracle/tls12_harness.c (libtls12_ref.so): picotls' TLS 1.2 receive over fusion's non-temporal AEADs */
+long ref_tls12_receive(size_t key_size, const uint8_t *master_secret, const uint8_t *hello_randoms, const uint8_t *input,
+                       size_t inlen, uint8_t *out, size_t outcap);
+extern int ptls_fusion_can_aesni256;
+
+/* when the two TLS 1.2 streams differ, which one is right: each stream through fusion's receive (its decryption is the
+ * 128-bit path whatever the CPU) and through ours, both streams sent again, and the CPU fusion ran on (its seal takes
+ * the 256-bit VAES path where cpuid offers it, ptls_fusion_can_aesni256) */
+static void tls12_arbitrate(ptls_aead_algorithm_t *ours, ptls_aead_algorithm_t *ref, ptls_hash_algorithm_t *hash, const uint8_t *ms,
+                            const uint8_t *randoms, const uint8_t *data, size_t len, const ptls_buffer_t *a, const ptls_buffer_t *b)
+{
+    static uint8_t plain[65536];
+    const size_t ks = ours->key_size;
+    const long fa = ref_tls12_receive(ks, ms, randoms, a->base, a->off, plain, sizeof(plain));
+    const int fa_ok = fa == (long)len && memcmp(plain, data, len) == 0;
+    const long fb = ref_tls12_receive(ks, ms, randoms, b->base, b->off, plain, sizeof(plain));
+    const int fb_ok = fb == (long)len && memcmp(plain, data, len) == 0;
+    ptls_buffer_t pa, a2, b2;
+    ptls_buffer_init(&pa, "", 0);
+    ptls_buffer_init(&a2, "", 0);
+    ptls_buffer_init(&b2, "", 0);
+    const int oa = tls12_receive(ours, hash, ms, randoms, a->base, a->off, &pa);
+    const int oa_ok = oa == 0 && pa.off == len && memcmp(pa.base, data, len) == 0;
+    tls12_send(ours, hash, ms, randoms, data, len, &a2);
+    tls12_send(ref, hash, ms, randoms, data, len, &b2);
+    const int a_same = a2.off == a->off && memcmp(a2.base, a->base, a->off) == 0;
+    const int b_same = b2.off == b->off && memcmp(b2.base, b->base, b->off) == 0;
+    const int again = a2.off == b2.off && memcmp(a2.base, b2.base, a2.off) == 0;
+    char model[128] = "?";
+    FILE *f = fopen("/proc/cpuinfo", "r");
+    if (f != NULL) {
+        char line[256];
+        while (fgets(line, sizeof(line), f) != NULL)
+            if (strncmp(line, "model name", 10) == 0) {
+                const char *c = strchr(line, ':');
+                snprintf(model, sizeof(model), "%s", c != NULL ? c + 2 : line);
+                model[strcspn(model, "\n")] = 0;
+                break;
+            }
+        fclose(f);
+    }
+    printf("# arbitration: fusion's receive of our stream %s, of its own %s; our receive of our stream %s\n",
+           fa_ok ? "ok" : "REJECTED", fb_ok ? "ok" : "REJECTED", oa_ok ? "ok" : "REJECTED");
+    printf("#   sent again: ours %s, fusion's %s, the two %s; fusion 256-bit seal %d on \"%s\"\n", a_same ? "unchanged" : "CHANGED",
+           b_same ? "unchanged" : "CHANGED", again ? "agree" : "differ", ptls_fusion_can_aesni256, model);
+    ptls_buffer_dispose(&pa);
+    ptls_buffer_dispose(&a2);
+    ptls_buffer_dispose(&b2);
+}
+
 static int tls12_test(ptls_aead_algorithm_t *ours, ptls_aead_algorithm_t *ref, ptls_hash_algorithm_t *hash, const char *what)
 {
     static uint8_t data[40000];
@@ -319,6 +369,7 @@ static int tls12_test(ptls_aead_algorithm_t *ours, ptls_aead_algorithm_t *ref, p
     if (!(a.off == b.off && memcmp(a.base, b.base, a.off) == 0)) {
         tls12_describe_diff(what, a.base, a.off, b.base, b.off);
         printf("# engine's last error: %s\n", ptls_mi355x_last_error());
+        tls12_arbitrate(ours, ref, hash, ms, randoms, data, sizeof(data), &a, &b);
     }
     int rret = tls12_receive(ours, hash, ms, randoms, b.base, b.off, &pa);
     OK(rret == 0 && pa.off == sizeof(data) && memcmp(pa.base, data, sizeof(data)) == 0, "tls12 receive (mi355x) of fusion's records");
