@@ -1380,7 +1380,7 @@ static int launch_batch(ptls_mi355x_keyset_t *ks, bool open, const ptls_mi355x_r
         u32 *ctl = ks->d_group, *cnt = ctl + 2, *perm = cnt + nb;
         HIP_TRY(hipMemsetAsync(ctl, 0, (2 + nb) * 4, s));
         const unsigned gh = (unsigned)min((nrecs + 255) / 256, (size_t)ks->ds->ncu * 8);
-        key_changes_kernel<<<gh, 256, 0, s>>>(recs, nrecs, ctl);
+        key_changes_kernel<<<(unsigned)min((nrecs + 255) / 256, (size_t)ks->ds->ncu * KEY_CHANGES_WG_PER_CU), 256, 0, s>>>(recs, nrecs, ctl);
         key_hist_kernel<<<gh, 256, 0, s>>>(recs, nrecs, (u32)ks->nkeys, cnt, ctl);
         key_scan_kernel<<<1, 1024, 0, s>>>(cnt, (u32)nb, nrecs, ctl);
         ptls_mi355x_record_t *grouped = (ptls_mi355x_record_t *)(ctl + ((2 + nb + nrecs + 1) & ~(size_t)1));

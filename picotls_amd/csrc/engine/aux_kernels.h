@@ -13,17 +13,29 @@
 // at each record's own index, so the results are those of the batch order. ctl[0] = key changes, ctl[1] = regroup.
 #define KEY_GROUP_MAX_KEYS (1u << 20)
 
-// ctl[0]: key changes between neighbouring records (a wave sum per atomic)
+// ctl[0]: key changes between neighbouring records, one atomic per workgroup. (Every wave adding its own sum put 8,192
+// device-scope atomics on one word: 112 us per 4M-record batch; 2 workgroups per CU with four loads in flight per lane
+// take 34 us, profiles/r5/aux_atomics_ab.txt.)
+#define KEY_CHANGES_WG_PER_CU 2
 __global__ __launch_bounds__(256) void key_changes_kernel(const ptls_mi355x_record_t *recs, u64 n, u32 *ctl)
 {
+    __shared__ u32 wsum[4];
     u32 changes = 0;
-    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x + 1; i < n; i += (u64)gridDim.x * blockDim.x)
+    const u64 stride = (u64)gridDim.x * blockDim.x;
+#pragma unroll 4
+    for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x + 1; i < n; i += stride)
         changes += recs[i - 1].key_idx != recs[i].key_idx;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1)
         changes += (u32)__shfl_xor((int)changes, off, 64);
-    if ((threadIdx.x & 63) == 0 && changes != 0)
-        atomicAdd(&ctl[0], changes);
+    if ((threadIdx.x & 63) == 0)
+        wsum[threadIdx.x >> 6] = changes;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const u32 total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        if (total != 0)
+            atomicAdd(&ctl[0], total);
+    }
 }
 
 // (the key count bounds the distinct keys of the batch from above: more runs than twice that means keys recur, with
@@ -150,7 +162,8 @@ __global__ __launch_bounds__(1024) void balance_bounds_kernel(const u32 *tiles, 
     const u32 t = threadIdx.x;
     const u64 per = (ntiles + blockDim.x - 1) / blockDim.x, t0 = min(ntiles, t * per), t1 = min(ntiles, t0 + per);
     u64 sum = 0;
-    for (u64 i = t0; i < t1; ++i)
+#pragma unroll 16
+    for (u64 i = t0; i < t1; ++i)  // (unrolled: 16 loads in flight per lane, not one latency per tile)
         sum += tiles[i];
     s_off[t] = sum;
     __syncthreads();

@@ -885,6 +885,47 @@ def test_ungrouped_many_key_batch_regrouped_on_device(ref, nkeys, frac_bad):
     assert np.array_equal(sealed2, sealed)
 
 
+def test_many_key_batch_in_bursts_regrouped_on_device(ref):
+    # (round 5) connections sending bursts of 6-20 records, the bursts in random order: runs average ~13 records, above
+    # the 8-record rule, but outnumber the 300 keys more than twice, so key_regroup groups the batch (aux_kernels.h);
+    # a W8-sized batch (>= 2048 records) with every key's bursts spread over it, against fusion, seal and open
+    rng = np.random.default_rng(655)
+    nkeys, bursts = 300, []
+    for k in range(nkeys):
+        left = 80
+        while left > 0:
+            m = min(left, int(rng.integers(6, 21)))
+            bursts.append((k, m))
+            left -= m
+    rng.shuffle(bursts)
+    key_idx = np.concatenate([np.full(m, k, np.int64) for k, m in bursts])
+    n = len(key_idx)
+    changes = int((key_idx[1:] != key_idx[:-1]).sum())
+    assert changes * 8 <= n and changes >= 2 * nkeys and changes * 32 > n  # only the burst rule regroups it
+    lens = rng.integers(0, 3000, n)
+    b = RecordBatch.build(lens, rng.integers(0, 30, n), seqs=rng.integers(0, 2**48, n, dtype=np.uint64), key_idx=key_idx)
+    keys = np.frombuffer(rng.bytes(nkeys * 16), np.uint8)
+    ivs = np.frombuffer(rng.bytes(nkeys * 12), np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aad = np.frombuffer(rng.bytes(max(b.aad_bytes, 1)), np.uint8)
+    ks = pa.Keyset(keys, ivs, 16)
+    sealed = gpu_seal(ks, b.seal, pt, aad, b.sealed_bytes)
+    expect = np.zeros(b.sealed_bytes, np.uint8)
+    ref.run_batch(True, keys, ivs, 16, b.seal, pt, aad, expect, nthreads=8)
+    assert np.array_equal(sealed, expect)
+    bad = expect.copy()
+    tamper = rng.choice(n, 7, replace=False)
+    for i in tamper:
+        bad[int(b.seal[i]["out_off"]) + int(b.seal[i]["len"])] ^= 0x40  # the tag's first byte
+    back, ok = gpu_open(ks, b.open, bad, aad, b.pt_bytes)
+    want_ok = np.ones(n, bool)
+    want_ok[tamper] = False
+    assert np.array_equal(ok.astype(bool), want_ok)
+    for i in range(n):
+        o, ln = int(b.open[i]["out_off"]), int(b.open[i]["len"])
+        assert np.array_equal(back[o:o + ln], pt[o:o + ln]), i
+
+
 # n = 1, 2, 33: one workgroup or a few; n = 256 * k: k records per workgroup on a 256-CU MI355X (one persistent
 # workgroup per CU once a batch has >= 32 records per CU)
 @pytest.mark.parametrize("n", [1, 2, 33, 300, 1000, 256 * 63, 256 * 64, 256 * 65, 256 * 129, 256 * 256])
