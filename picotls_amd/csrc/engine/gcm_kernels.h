@@ -183,6 +183,9 @@ __device__ unsigned long long g_ext_runs[EXT_RUN_ROWS][8];
 #ifndef EARLY_GHASH
 #define EARLY_GHASH 1
 #endif
+#ifndef MEAS_BUILD_ONCE
+#define MEAS_BUILD_ONCE 0
+#endif
 #define EARLY_GHASH_WAVE 11  // waves 11..15 (320 threads: one per table window of 9 tables) build a one-key launch's tables
 
 // Run-state control words (RUN_CTL_WORDS per buffer)
@@ -969,7 +972,10 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         // Horner with H^4)
         const bool g4run = W8K && !W8TREE && (whole ? W8_G4 : W8_G4_CUT);
         const u32 w8mode = !w8run ? 0u : W8TREE ? 2u : g4run ? 3u : 1u;
-        if (w8run && (key_idx != loaded_key || loaded_w8 != w8mode)) {
+        // (MEAS_BUILD_ONCE, measurement builds only: a workgroup's later runs keep its first run's tables -- wrong tags
+        // for other keys -- to price the per-run build, profiles/r5/table_build_cost.txt)
+        const bool key_new = key_idx != loaded_key && !(MEAS_BUILD_ONCE && loaded_key != 0xffffffffu);
+        if (w8run && (key_new || loaded_w8 != w8mode)) {
             // the 8-bit H^8 (H^4) table over slots 0..7, H in slot 8, and a cut run's combine power (or the tree's H^2)
             // at W8_TAB_COMB
             w8_build_tables(lds, (const lds_u8 *)key, whole ? 0xffffffffu : usrc, w8mode == 2, w8mode == 3 ? 3u : 7u);
