@@ -39,11 +39,14 @@ __global__ __launch_bounds__(256) void key_changes_kernel(const ptls_mi355x_reco
 }
 
 // (the key count bounds the distinct keys of the batch from above: more runs than twice that means keys recur, with
-// no per-key pass to find out; a batch over a few keys of a large keyset keeps its runs)
+// no per-key pass to find out; a batch over a few keys of a large keyset keeps its runs. The burst rule also wants
+// enough runs for the table builds it saves, ~2.4 us a run, to repay the grouping passes: KEY_REGROUP_MIN_RUNS, about
+// 32 runs per workgroup on 256 CUs)
+#define KEY_REGROUP_MIN_RUNS 8192
 __device__ __forceinline__ bool key_regroup(const u32 *ctl, u64 n, u32 nkeys)
 {
     const u64 changes = ctl[0];
-    return changes * 8 > n || (changes >= 2 * (u64)nkeys && changes * 32 > n);
+    return changes * 8 > n || (changes >= 2 * (u64)nkeys && changes * 32 > n && changes >= KEY_REGROUP_MIN_RUNS);
 }
 
 // key counts (only when regrouping): each thread counts a contiguous stretch of records and adds one count per key run

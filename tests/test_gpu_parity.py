@@ -887,12 +887,13 @@ def test_ungrouped_many_key_batch_regrouped_on_device(ref, nkeys, frac_bad):
 
 def test_many_key_batch_in_bursts_regrouped_on_device(ref):
     # (round 5) connections sending bursts of 6-20 records, the bursts in random order: runs average ~13 records, above
-    # the 8-record rule, but outnumber the 300 keys more than twice, so key_regroup groups the batch (aux_kernels.h);
-    # a W8-sized batch (>= 2048 records) with every key's bursts spread over it, against fusion, seal and open
+    # the 8-record rule, but outnumber the 1000 keys more than twice (and reach KEY_REGROUP_MIN_RUNS), so key_regroup
+    # groups the batch (aux_kernels.h); a W8-sized batch with every key's bursts spread over it, against fusion, seal
+    # and open
     rng = np.random.default_rng(655)
-    nkeys, bursts = 300, []
+    nkeys, bursts = 1000, []
     for k in range(nkeys):
-        left = 80
+        left = 120
         while left > 0:
             m = min(left, int(rng.integers(6, 21)))
             bursts.append((k, m))
@@ -901,8 +902,8 @@ def test_many_key_batch_in_bursts_regrouped_on_device(ref):
     key_idx = np.concatenate([np.full(m, k, np.int64) for k, m in bursts])
     n = len(key_idx)
     changes = int((key_idx[1:] != key_idx[:-1]).sum())
-    assert changes * 8 <= n and changes >= 2 * nkeys and changes * 32 > n  # only the burst rule regroups it
-    lens = rng.integers(0, 3000, n)
+    assert changes * 8 <= n and changes >= 2 * nkeys and changes * 32 > n and changes >= 8192  # only the burst rule
+    lens = rng.integers(0, 1500, n)
     b = RecordBatch.build(lens, rng.integers(0, 30, n), seqs=rng.integers(0, 2**48, n, dtype=np.uint64), key_idx=key_idx)
     keys = np.frombuffer(rng.bytes(nkeys * 16), np.uint8)
     ivs = np.frombuffer(rng.bytes(nkeys * 12), np.uint8)
