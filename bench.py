@@ -645,14 +645,17 @@ def per_rank(R, res) -> dict:
             "max_over_min": round(max(wall) / min(wall), 4) if min(wall) > 0 else None}
 
 
+W8_MIN_RECS = 256  # picotls_amd/csrc/engine/common.h: batches from this many records take the W8 kernels
+
+
 def lds_model(res, key_size: int, nrecs: int):
     """The bound the seal kernel actually meets: LDS table lookups. Per GHASH stream block an AES-128
     block costs 133 ds_read_b32 (AES-256: 197) and its GHASH fold 16 ds_read_b128 (the W8 kernels' Horner step on the
-    8-bit H^8 table, batches of at least W8_MIN_RECS = 2048 records) or 32 (4-bit windows); at the MI355X aggregate LDS
+    8-bit H^8 table, batches of at least W8_MIN_RECS records) or 32 (4-bit windows); at the MI355X aggregate LDS
     rates (MI355X_MICROARCH.md: ~75 TB/s ds_read_b32, ~150 TB/s ds_read_b128 with every CU at 2.4 GHz) that gives the
     chip's block rate ceiling; frac = achieved blocks/s over it (the clock under this load is lower)."""
     lookups = 133 if key_size == 16 else 197
-    ghash = 16 if nrecs >= 2048 else 32
+    ghash = 16 if nrecs >= W8_MIN_RECS else 32
     sec_per_block = lookups * 4 / 75e12 + ghash * 16 / 150e12
     peak = 1.0 / sec_per_block
     achieved = res["stream_blocks"] / (res["seal_ms"] / 1e3)
@@ -726,9 +729,9 @@ def main():
         "open_GiBps": round(res["payload_bytes"] / open_s / 2**30, 3),
         "roofline": {"bound": "hbm", "kernel": f"{'gcm_batch_kernel' if args.schedule == 'lockstep' else 'gcm_chunked_kernel'}"
                                                f"<{10 if wl.key_size == 16 else 14},seal>",
-                     # (one seal launch of W8_MIN_RECS = 2048 records or more is the W8 pair, EXT 4 + EXT 3:
+                     # (one seal launch of W8_MIN_RECS records or more is the W8 pair, EXT 4 + EXT 3:
                      # avg_launch_ms covers both, and profiles/pmc_<workload>.json sums their bytes)
-                     "launch": "w8 pair" if args.schedule != "lockstep" and res["records"] >= 2048 else "single",
+                     "launch": "w8 pair" if args.schedule != "lockstep" and res["records"] >= W8_MIN_RECS else "single",
                      "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic_from_profiles(wl.name, res["records"]),
                      "alg_bytes_per_launch": res["seal_alg_bytes"], "avg_launch_ms": round(res["seal_ms"], 4),

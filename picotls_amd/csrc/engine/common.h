@@ -167,9 +167,11 @@ __device__ __forceinline__ u32 lane_here()
 #define W8_TLS12 1
 #endif
 #ifndef W8_MIN_RECS
-// batches of fewer records keep the 4-bit kernel: the 8-bit table's build is not repaid (256 x 16 KiB -5 %, 1000 x 1200 B
-// -4 %, 1000 x 16 KiB even, 4096 x 16 KiB +7 %; profiles/r4/w8all_ab.txt)
-#define W8_MIN_RECS 2048
+// batches of fewer records keep the 4-bit kernel. Round 4 set 2048 (256 x 16 KiB -5 %, 1000 x 1200 B -4 %, 1000 x 16 KiB
+// even, profiles/r4/w8all_ab.txt); with round 5's W8 kernels the 8-bit path is ahead from 256 records (256 x 16 KiB
+// +1.8 %, 1000 x 16 KiB +3.2 %, 2000 x 16 KiB +2.3 %, 1000 x 1200 B +3.9 %) and even below (64 x 64 KiB, 100 x 16 KiB:
+// ±0.3 % with 64), profiles/r5/w8_min_recs_ab.txt
+#define W8_MIN_RECS 256
 #endif
 #ifndef W8_SWAP
 // (round 5) the W8 kernels' LDS map puts the 8-bit H^8 table at [0, 64K) and the AES T-tables at [64K, 128K): the

@@ -80,7 +80,7 @@ def test_fuzz_batches_vs_fusion(ref, seed):
 
 @pytest.mark.parametrize("seed", range(4))
 def test_fuzz_w8_batches_odd_offsets_vs_fusion(ref, seed):
-    """Batches large enough for the W8 kernels (from 2048 records) with records at odd byte offsets (slot gaps of 1-47
+    """Batches large enough for the W8 kernels (2048 records and more; W8_MIN_RECS is 256 since round 5) with records at odd byte offsets (slot gaps of 1-47
     bytes): the paired half-line and line stores of round 5 (4-lane groups, cut units) decide their pairs from the
     output addresses, which then straddle lines by any amount. Seal bit-exact against fusion, open with tampering."""
     rng = np.random.default_rng(9100 + seed)

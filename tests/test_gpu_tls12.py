@@ -386,7 +386,7 @@ def _tls12_expect(ref, keys, ivs, key_size, recs, arena, i):
 @pytest.mark.parametrize("key_size,nkeys,n,uniform", [(16, 3, 2600, 0), (32, 1, 2100, 0), (16, 1, 256 * 130, 16384),
                                                        (32, 2, 256 * 130, 1200), (16, 1, 256 * 130, 3001)])
 def test_tls12_w8_kernels_vs_fusion(ref, key_size, nkeys, n, uniform):
-    """TLS 1.2 framing in the W8 kernels (batches of at least W8_MIN_RECS = 2048 records): random lengths (EXT 4's cut
+    """TLS 1.2 framing in the W8 kernels (batches of at least W8_MIN_RECS records: 256 since round 5): random lengths (EXT 4's cut
     runs), 33,280 records of 16 KiB, 130 per workgroup (EXT 3's whole runs of long records), and 33,280 records of 1200
     or 3001 bytes (EXT 4's whole runs, in 4-lane groups since round 5). Every record (the uniform batches: 400 sampled
     and the ends) equals lib/fusion.c's seal with the record-layer nonce and AAD, nothing outside the wire records is

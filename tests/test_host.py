@@ -134,12 +134,12 @@ def test_lds_model_ceiling():
     import bench
 
     res = {"stream_blocks": 10**9, "seal_ms": 10.0}
-    m = bench.lds_model(res, 16, 1000)
-    # a batch below W8_MIN_RECS: 133 x 4 B at 75 TB/s + 32 x 16 B (4-bit GHASH windows) at 150 TB/s per block
+    m = bench.lds_model(res, 16, 100)
+    # a batch below W8_MIN_RECS (256): 133 x 4 B at 75 TB/s + 32 x 16 B (4-bit GHASH windows) at 150 TB/s per block
     assert abs(m["peak_at_2.4GHz"] - 1 / (532 / 75e12 + 512 / 150e12)) < 1e6
     assert abs(m["frac"] - 1e11 / m["peak_at_2.4GHz"]) < 1e-3
-    assert bench.lds_model(res, 32, 1000)["peak_at_2.4GHz"] < m["peak_at_2.4GHz"]
-    # the W8 kernels (2048 records and more): 16 x 16 B per block for the 8-bit Horner table
+    assert bench.lds_model(res, 32, 100)["peak_at_2.4GHz"] < m["peak_at_2.4GHz"]
+    # the W8 kernels (W8_MIN_RECS records and more): 16 x 16 B per block for the 8-bit Horner table
     w8 = bench.lds_model(res, 16, 1 << 20)
     assert abs(w8["peak_at_2.4GHz"] - 1 / (532 / 75e12 + 256 / 150e12)) < 1e6
     assert "16 ds_read_b128" in w8["per_block"]
