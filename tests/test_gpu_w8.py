@@ -196,6 +196,22 @@ def test_w8_pairs_on_many_streams_vs_fusion(ref):
     ks.free()
 
 
+@pytest.mark.parametrize("n,length,key_size,nkeys", [(256, 16384, 16, 1), (300, 1200, 32, 1), (1000, 0, 16, 1),
+                                                   (2047, 700, 16, 3), (255, 1200, 16, 1)])
+def test_w8_small_batches_vs_fusion(ref, n, length, key_size, nkeys):
+    """(round 5) Batches from W8_MIN_RECS = 256 records take the W8 serial kernel (EXT 4 alone: a workgroup's share is
+    too small for whole runs of long records, so no EXT 3), against fusion, sealed and opened with tampering; 255
+    records keep the 4-bit kernels."""
+    rng = np.random.default_rng(8700 + n + length)
+    pa.debug_counters(reset=True)
+    _check(ref, rng, np.full(n, length), np.full(n, 13), key_size, nkeys, tamper=3)
+    c = pa.debug_counters(reset=True)
+    if n >= 256:
+        assert c["launches"]["w8_serial"] >= 2 and c["launches"]["w8_tree"] == 0, c
+    else:
+        assert c["launches"]["w8_serial"] == 0 and c["launches"]["w8_tree"] == 0, c
+
+
 @pytest.mark.parametrize("length,aad,key_size,nkeys", [
     (1200, 13, 16, 1), (0, 13, 16, 1), (1, 0, 32, 1), (16, 16, 16, 2), (100, 17, 32, 3), (4095, 40, 16, 1),
     (7800, 5, 32, 1), (1223, 70, 16, 4)])
