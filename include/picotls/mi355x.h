@@ -319,6 +319,12 @@ int ptls_mi355x_encrypt_s(ptls_mi355x_keyset_t *ks, size_t key_idx, void *output
  * protection by the per-record vtable.
  */
 int ptls_mi355x_encrypt_block(ptls_mi355x_keyset_t *ks, size_t key_idx, void *out, const void *in);
+/**
+ * nblocks AES-ECB blocks on HOST buffers under key key_idx in one launch (ptls_fusion_aesecb_encrypt, lib/fusion.c:924,
+ * over many blocks). Backs the raw decrypt's counter blocks when the caller's counter does not start at 1
+ * (ptls_mi355x_aesgcm_decrypt, the semantics of ptls_fusion_aesgcm_decrypt at lib/fusion.c:679-682).
+ */
+int ptls_mi355x_encrypt_blocks(ptls_mi355x_keyset_t *ks, size_t key_idx, void *out, const void *in, size_t nblocks);
 
 /**
  * Returns a static string describing the last error on this thread (or "" if none).

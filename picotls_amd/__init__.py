@@ -61,6 +61,7 @@ ABI_FUNCTIONS = (
     "ptls_mi355x_encrypt_s",
     "ptls_mi355x_decrypt",
     "ptls_mi355x_encrypt_block",
+    "ptls_mi355x_encrypt_blocks",
     "ptls_mi355x_staging_bytes",
     "ptls_mi355x_release_staging",
     "ptls_mi355x_last_error",
@@ -133,6 +134,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.ptls_mi355x_decrypt.argtypes = [vp, sz, vp, vp, sz, u64, vp, sz]
     lib.ptls_mi355x_decrypt.restype = sz
     lib.ptls_mi355x_encrypt_block.argtypes = [vp, sz, vp, vp]
+    lib.ptls_mi355x_encrypt_blocks.argtypes = [vp, sz, vp, vp, sz]
     lib.ptls_mi355x_quiclb_batch.argtypes = [vp, vp, sz, vp, vp, vp]
     lib.ptls_mi355x_quiclb_transform.argtypes = [vp, sz, vp, vp, sz, ci]
     lib.ptls_mi355x_last_error.restype = ctypes.c_char_p
@@ -480,7 +482,8 @@ def debug_inject_error() -> int:
 
 
 def debug_clock_sample(dev_ptr: int, stream: int = 0) -> None:
-    """Writes (s_memtime, s_memrealtime, XCC id) of XCD 0 to 3 x u64 at dev_ptr, in stream order."""
+    """Writes (s_memtime, s_memrealtime, XCC id) of the XCD the probe wave ran on (the id is out[2]) to 3 x u64 at dev_ptr,
+    in stream order."""
     if load_library().ptls_mi355x_debug_clock_sample(dev_ptr, stream or None) != 0:
         raise _err("ptls_mi355x_debug_clock_sample")
 

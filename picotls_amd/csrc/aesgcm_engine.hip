@@ -80,7 +80,7 @@ static int fail(const char *fmt, const char *detail)
 // Test and measurement counters (include/picotls/mi355x_debug.h): chunked-kernel launches per EXT instantiation (0..4),
 // lockstep launches (5), span launches (6) -- host side, counted where the launch is made
 static std::atomic<uint64_t> g_launches[8];
-#define COUNT_LAUNCH(i) g_launches[(i)].fetch_add(1, std::memory_order_relaxed)
+#define COUNT_LAUNCH(i) (ENGINE_HOOKS ? g_launches[(i)].fetch_add(1, std::memory_order_relaxed) : 0)
 
 #define HIP_TRY(expr)                                                                                                         \
     do {                                                                                                                      \
@@ -854,23 +854,39 @@ int ptls_mi355x_debug_profile(unsigned long long *out, int reset)
 
 // ---- test and measurement hooks (include/picotls/mi355x_debug.h)
 
+// reads (and with reset, zeroes in the same atomic exchange) the per-workgroup run counters, so that a launch finishing
+// meanwhile is counted once, in this read or the next
+__global__ void ext_runs_take_kernel(unsigned long long *out, int reset)
+{
+    for (u32 i = threadIdx.x; i < EXT_RUN_ROWS * 8; i += blockDim.x) {
+        unsigned long long *c = &g_ext_runs[i / 8][i % 8];
+        out[i] = reset ? atomicExch(c, 0ull) : __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 int ptls_mi355x_debug_counters(uint64_t *out, int reset)
 {
     if (out == NULL)
         return fail("%s", "debug_counters: invalid arguments");
+    // (test-only) every launch made so far has finished, and counted its runs, before anything is read
+    HIP_TRY(hipDeviceSynchronize());
     for (int i = 0; i < 8; ++i)
         out[i] = reset ? g_launches[i].exchange(0) : g_launches[i].load();
-    HIP_TRY(hipDeviceSynchronize());  // (test-only: the device counters of every launch made so far)
-    static unsigned long long rows[EXT_RUN_ROWS][8];
-    HIP_TRY(hipMemcpyFromSymbol(rows, HIP_SYMBOL(g_ext_runs), sizeof(rows)));
+    std::vector<unsigned long long> rows((size_t)EXT_RUN_ROWS * 8);
+    unsigned long long *d = nullptr;
+    HIP_TRY(hipMalloc(&d, rows.size() * sizeof(rows[0])));
+    LAUNCH_CLEAR();
+    ext_runs_take_kernel<<<1, 256>>>(d, reset);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess)
+        e = hipMemcpy(rows.data(), d, rows.size() * sizeof(rows[0]), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess)
+        return fail("debug_counters: %s", hipGetErrorString(e));
     for (int i = 0; i < 8; ++i) {
         out[8 + i] = 0;
         for (int r = 0; r < EXT_RUN_ROWS; ++r)
-            out[8 + i] += rows[r][i];
-    }
-    if (reset) {
-        memset(rows, 0, sizeof(rows));
-        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_ext_runs), rows, sizeof(rows)));
+            out[8 + i] += rows[(size_t)r * 8 + i];
     }
     return 0;
 }
@@ -2075,24 +2091,34 @@ int ptls_mi355x_quiclb_transform(ptls_mi355x_keyset_t *ks, size_t key_idx, void 
     return 0;
 }
 
+int ptls_mi355x_encrypt_blocks(ptls_mi355x_keyset_t *ks, size_t key_idx, void *out, const void *in, size_t nblocks)
+{
+    if (ks == NULL || key_idx >= ks->nkeys || (nblocks != 0 && (out == NULL || in == NULL)) || nblocks > ((size_t)1 << 26))
+        return fail("%s", "encrypt_blocks: invalid arguments");
+    if (nblocks == 0)
+        return 0;
+    DeviceScope scope(ks->device);
+    StageCall call(ks->ds);
+    // staging: [0, n) blocks in | [n', n' + n) blocks out, n' = n rounded up to 32 bytes
+    const size_t n = nblocks * 16, up = (n + 31) & ~(size_t)31;
+    if (call.acquire(2 * up) != 0)
+        return -1;
+    memcpy(call.host(), in, n);
+    uint8_t *d = call.dev();
+    const hipStream_t s = call.stream();
+    if (wait_ready(ks, s) != 0 ||
+        call.roundtrip(up, [&] { return launch_ecb(ks->d_keys + key_idx, 1, ks->nr, ks->ds->ncu, NULL, d, d + up, nblocks, s); }) != 0)
+        return -1;
+    seen_ready(ks);
+    memcpy(out, call.host() + up, n);
+    return 0;
+}
+
 int ptls_mi355x_encrypt_block(ptls_mi355x_keyset_t *ks, size_t key_idx, void *out, const void *in)
 {
     if (ks == NULL || key_idx >= ks->nkeys || out == NULL || in == NULL)
         return fail("%s", "encrypt_block: invalid arguments");
-    DeviceScope scope(ks->device);
-    StageCall call(ks->ds);
-    // staging: [0, 16) block in | [32, 48) block out
-    if (call.acquire(64) != 0)
-        return -1;
-    memcpy(call.host(), in, 16);
-    uint8_t *d = call.dev();
-    const hipStream_t s = call.stream();
-    if (wait_ready(ks, s) != 0 ||
-        call.roundtrip(32, [&] { return launch_ecb(ks->d_keys + key_idx, 1, ks->nr, ks->ds->ncu, NULL, d, d + 32, 1, s); }) != 0)
-        return -1;
-    seen_ready(ks);
-    memcpy(out, call.host() + 32, 16);
-    return 0;
+    return ptls_mi355x_encrypt_blocks(ks, key_idx, out, in, 1);
 }
 
 }  // extern "C"

@@ -167,7 +167,11 @@ __device__ __forceinline__ unsigned long long stamp()
 
 // Runs processed per chunked instantiation (EXT 0..4), one row per workgroup (blockIdx.x mod EXT_RUN_ROWS), summed on the
 // host by ptls_mi355x_debug_counters: the evidence that a batch ran in the kernel a test means to exercise (one
-// uncontended atomic per run and workgroup)
+// uncontended atomic per workgroup and launch, at its end). ENGINE_HOOKS=0 compiles these and the kernel clock out (the
+// A/B of profiles/r6/hooks_ab.txt); the shipped build keeps them, as the GPU tests read them.
+#ifndef ENGINE_HOOKS
+#define ENGINE_HOOKS 1
+#endif
 #ifndef COMBINE_SCATTER
 #define COMBINE_SCATTER 1  // round 5: a record's unit combine as a scattered chain of group products (ghash.h)
 #endif
@@ -225,6 +229,13 @@ __device__ __forceinline__ u32 run_unit_log2(u32 total_steps, u32 smax, u32 cap)
     return fill > chain ? fill : chain;
 }
 
+// The only way a kernel instantiation (EXT) changes what scan_run returns: the spread kernel (EXT 1) scans its long
+// records as empty units. A W8 pair relies on its two kernels scanning identically -- EXT 4 lists (start, chunk end) of
+// the runs it leaves, and EXT 3 rebuilds exactly those runs from them -- so an EXT rule added here must keep EXT 3 and 4
+// equal (or the list must carry the run's length and EXT 3 check it).
+constexpr bool scan_rule_of_ext(int ext) { return ext == 1; }
+static_assert(scan_rule_of_ext(3) == scan_rule_of_ext(4), "a W8 pair's kernels must scan runs identically");
+
 template <bool OPEN, int FRAME, bool FIRST = false, int EXT = 0>
 __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355x_record_t *__restrict__ recs, u64 p, u64 end,
                                       lds_u32 *rs)
@@ -247,7 +258,7 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
         if (t < lim) {
             ptls_mi355x_record_t r = recs[p + t];
             other = args.multi_key && r.key_idx != key;
-            if (!record_ok<FRAME>(args, r) || (EXT == 1 && spread_long(args, r)))  // rejected or spread: one empty unit
+            if (!record_ok<FRAME>(args, r) || (scan_rule_of_ext(EXT) && spread_long(args, r)))  // rejected or spread: one empty unit
                 r.len = 0, r.aad_len = 0, r.flags = 0;
             steps[q] = gcm_steps<OPEN, FRAME>(r);
         }
@@ -794,10 +805,13 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 slist = args.w8_flags + (u64)blockIdx.x * W8_FLAG_WORDS + 1;
         }
     }
-    unsigned long long *const kclock = blockIdx.x == 0 ? g_kclock_buf : nullptr;
+    unsigned long long *const kclock = ENGINE_HOOKS && blockIdx.x == 0 ? g_kclock_buf : nullptr;
     const u64 kc_t0 = kclock != nullptr ? __builtin_amdgcn_s_memtime() : 0ull;
     const u64 kc_r0 = kclock != nullptr ? __builtin_amdgcn_s_memrealtime() : 0ull;
     u32 skipped_w8 = 0;  // (the pair's first kernel: the runs this workgroup left to the second one)
+    // (test hook, ptls_mi355x_debug_counters) the runs this workgroup processed, and those in 4-lane groups: counted in
+    // SGPRs, added to g_ext_runs once at the end (round 6: was one device-scope atomic per run)
+    u32 runs_here = 0, g4_here = 0;
     constexpr bool SPREAD = FRAME == 0 && EXT == 1;
     if constexpr (SPREAD) {  // a small one-key batch (spread_pieces): workgroup w < n takes record w unless it is long
         if (blockIdx.x >= n) {
@@ -962,8 +976,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             rb ^= 1;
             continue;
         }
-        if (threadIdx.x == 0)  // (this instantiation processes the run: ptls_mi355x_debug_counters)
-            atomicAdd(&g_ext_runs[blockIdx.x % EXT_RUN_ROWS][EXT], 1ull);
+        ++runs_here;  // (this instantiation processes the run: ptls_mi355x_debug_counters)
         typedef __attribute__((address_space(3))) const KeyEntry lds_key_t;
         lds_key_t *key = (lds_key_t *)(rs + RUN_KEY_OFF);  // staged by the scanner
         // the EXT 3 kernel's runs (all W8: the others were skipped above) take the 8-bit Horner table (ghash.h)
@@ -1050,8 +1063,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 // record ending 128 * k positions before its end), each taken in twice as many 4-lane steps, so the
                 // partials, their slots and the combine power are the 8-lane kernel's
                 constexpr u32 G4 = 4, RPW4 = 64 / G4;
-                if (threadIdx.x == 0)  // (ptls_mi355x_debug_counters: runs in 4-lane groups)
-                    atomicAdd(&g_ext_runs[blockIdx.x % EXT_RUN_ROWS][7], 1ull);
+                ++g4_here;  // (ptls_mi355x_debug_counters: runs in 4-lane groups)
                 for (;;) {
                     u32 ub = 0;
                     if (lane_here() == 0)
@@ -1300,6 +1312,12 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     if constexpr (W8K && !W8TREE) {  // the pair's first kernel, for the second (workgroup-uniform)
         if (args.w8_split == 2 && args.w8_flags != nullptr && threadIdx.x == 0)
             args.w8_flags[(u64)blockIdx.x * W8_FLAG_WORDS] = min(skipped_w8, (u32)W8_SKIP_LIST + 1);
+    }
+    if (ENGINE_HOOKS && threadIdx.x == 0) {
+        if (runs_here != 0)
+            atomicAdd(&g_ext_runs[blockIdx.x % EXT_RUN_ROWS][EXT], (unsigned long long)runs_here);
+        if (g4_here != 0)
+            atomicAdd(&g_ext_runs[blockIdx.x % EXT_RUN_ROWS][7], (unsigned long long)g4_here);
     }
     if (kclock != nullptr && threadIdx.x == 0) {  // (vector stores and atomics only)
         const u64 t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();

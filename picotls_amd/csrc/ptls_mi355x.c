@@ -377,18 +377,66 @@ void ptls_mi355x_aesgcm_encrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output,
     seal_one(ctx->ks, output, input, inlen, seq, aad, aadlen, supp);
 }
 
+/* fusion's decrypt with a counter whose low dword is not zero (lib/fusion.c:679-682, :741): the register's low 64 bits
+ * v = LE64(ctr[0..7]) advance by a 64-bit add, so E(K, J0) is taken at v + 1 and data block b at v + 2 + b, each block
+ * the register byte-reversed. The output is that keystream XOR the input (written whatever the tag says); the tag
+ * holds iff tag == GHASH(aad, input) ^ E(K, ctr_J0). The engine's open checks GHASH ^ E(K, nonce || 1) instead, so it is
+ * handed tag ^ E(K, ctr_J0) ^ E(K, nonce || 1): it accepts exactly when fusion's decrypt would. All AES blocks are one
+ * ECB launch (ptls_mi355x_encrypt_blocks); GHASH is the engine's open of the record. */
+static int raw_decrypt_offset_counter(ptls_mi355x_aesgcm_context_t *ctx, uint8_t *output, const uint8_t *input, size_t inlen,
+                                      const uint8_t *c, const void *aad, size_t aadlen, const uint8_t *tag)
+{
+    const size_t nb = (inlen + 15) / 16, nblk = nb + 2;
+    uint8_t *blk = malloc(nblk * 16), *ks = malloc(nblk * 16);
+    uint64_t seq, v = 0;
+    int ok = 0, done = 0;
+    if (blk == NULL || ks == NULL || raw_nonce(ctx, c, &seq) != 0)
+        goto Exit;
+    for (int i = 7; i >= 0; --i)
+        v = v << 8 | c[i];
+    for (size_t j = 0; j <= nb; ++j) { /* j = 0: J0 at v + 1; j = 1 + b: data block b at v + 2 + b */
+        uint8_t *p = blk + 16 * j;
+        const uint64_t x = v + 1 + j;
+        for (int i = 0; i < 8; ++i)
+            p[i] = c[15 - i], p[8 + i] = (uint8_t)(x >> (56 - 8 * i));
+    }
+    { /* the engine's J0 for (iv, seq): nonce || 0x00000001 */
+        uint8_t *p = blk + 16 * (nb + 1);
+        for (int i = 0; i < 12; ++i)
+            p[i] = c[15 - i];
+        p[12] = 0, p[13] = 0, p[14] = 0, p[15] = 1;
+    }
+    if (ptls_mi355x_encrypt_blocks(ctx->ks, 0, ks, blk, nblk) != 0)
+        goto Exit;
+    /* the input is staged first, so that output may alias it */
+    memcpy(ctx->bounce, input, inlen);
+    for (size_t i = 0; i < inlen; ++i)
+        output[i] = ctx->bounce[i] ^ ks[16 + i];
+    for (int i = 0; i < PTLS_AESGCM_TAG_SIZE; ++i)
+        ctx->bounce[inlen + i] = tag[i] ^ ks[i] ^ ks[16 * (nb + 1) + i];
+    ok = ptls_mi355x_decrypt(ctx->ks, 0, ctx->bounce, ctx->bounce, inlen + PTLS_AESGCM_TAG_SIZE, seq, aad, aadlen) == inlen;
+    done = 1;
+Exit:
+    if (!done) /* the engine could not run: nothing decrypted, fail closed */
+        memset(output, 0, inlen);
+    if (ks != NULL)
+        ptls_clear_memory(ks, nblk * 16);
+    ptls_clear_memory(ctx->bounce, inlen + PTLS_AESGCM_TAG_SIZE);
+    free(blk);
+    free(ks);
+    return ok;
+}
+
 int ptls_mi355x_aesgcm_decrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, const void *input, size_t inlen,
                                const void *ctr, const void *aad, size_t aadlen, const void *tag)
 {
     uint64_t seq;
     const uint8_t *c = ctr;
-    if ((c[0] | c[1] | c[2] | c[3]) != 0) {
-        /* fusion's decrypt counts from the low 32 bits (lib/fusion.c:680; its encrypt sets them to 1), so a record of
-         * either encrypt fails its tag; the engine's counter starts at 1, so nothing is decrypted here */
-        memset(output, 0, inlen);
+    if (inlen + aadlen > ctx->capacity)
         return 0;
-    }
-    if (inlen + aadlen > ctx->capacity || raw_nonce(ctx, ctr, &seq) != 0)
+    if ((c[0] | c[1] | c[2] | c[3]) != 0)
+        return raw_decrypt_offset_counter(ctx, output, input, inlen, c, aad, aadlen, tag);
+    if (raw_nonce(ctx, ctr, &seq) != 0)
         return 0;
     memcpy(ctx->bounce, input, inlen);
     memcpy(ctx->bounce + inlen, tag, PTLS_AESGCM_TAG_SIZE);
