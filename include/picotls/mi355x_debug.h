@@ -17,9 +17,10 @@ extern "C" {
  *              batch with long records), 2 seal with header-protection masks, 3 W8 butterfly end (long whole records
  *              of a W8 pair), 4 W8 serial end (every other run of a W8 pair)
  *   out[5]     launches of the lockstep kernel, out[6] of the span kernels (a lone long record), out[7] 0
- *   out[8..14] runs processed on the device by each chunked instantiation (same order; a run skipped because the
- *              pair's other kernel takes it is not counted), out[15] the EXT 4 runs among them processed in 4-lane
- *              groups (whole runs of short records)
+ *   out[8..12] runs processed on the device by each chunked instantiation (same order; a run skipped because the
+ *              pair's other kernel takes it is not counted), out[13] 0, out[14] the EXT 4 runs among them that were
+ *              multi-key runs (round 6: several connections' short records in one run), out[15] the EXT 4 runs
+ *              processed in 4-lane groups (whole runs of short records of one key)
  * Waits for the whole device (reading the device counters). reset != 0 zeroes them after reading. Returns 0 or -1.
  */
 int ptls_mi355x_debug_counters(uint64_t *out, int reset);

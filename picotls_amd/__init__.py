@@ -473,6 +473,7 @@ def debug_counters(reset: bool = False) -> dict:
         raise _err("ptls_mi355x_debug_counters")
     runs = dict(zip(COUNTER_NAMES[:5], out[8:13]))
     runs["w8_g4"] = out[15]  # (of the w8_serial runs: whole runs in 4-lane groups)
+    runs["w8_mk"] = out[14]  # (of the w8_serial runs: multi-key runs, round 6)
     return {"launches": dict(zip(COUNTER_NAMES[:7], out[:7])), "runs": runs}
 
 

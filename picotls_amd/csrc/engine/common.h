@@ -218,6 +218,22 @@ __device__ __forceinline__ u32 lane_here()
 // a W8 pair's flag block per workgroup (BatchArgs::w8_flags): [0] the runs EXT 4 left to EXT 3 (W8_SKIP_LIST + 1:
 // more than the list holds, or records past 2^32), then per listed run (walk order) its first record and the end of
 // the chunk that holds it
+// (round 6) multi-key runs (MK runs, EXT 4): a many-key batch's connections of short uniform records (under
+// W8_MIN_STEPS 8-lane steps, fewer than WHOLE_MIN_RECS records each: QUIC packets of many connections) share one
+// whole-record run of up to MK_SLOTS connections and CRUN_RECS records, in 4-lane groups, each connection's 4-bit H^4 and
+// H tables in a 16 KiB slot of [0, 64K) (ghash.h gmul4w). A connection's records are taken 16 at a time (a wave's
+// "claim": one connection per wave, so its round keys stay in SGPRs). Run state: ctl[RC_MK] = connections (0: not an
+// MK run), RC_UNITS = claims; the claims (first record | count << 8 | slot << 16) at RUN_UBASE_OFF, the key entries of
+// slots 1.. at RUN_DONE_OFF (slot 0's at RUN_KEY_OFF, as any run's)
+#ifndef MK_RUNS
+#define MK_RUNS 1
+#endif
+#define MK_SLOTS 4
+#define MK_NONE 0xffffffffu
+#define MK_SLOT_BYTES 16384
+__host__ __device__ constexpr u32 mk_kslot(u32 slot) { return (slot << 6) * 0x01010101u; }  // slot bits in each byte
+__host__ __device__ constexpr u32 mk_htab(u32 kslot) { return ((kslot & 0xc0u) << 8) + 8192u; }  // the slot's H table
+
 #define W8_FLAG_WORDS 32
 #define W8_SKIP_LIST ((W8_FLAG_WORDS - 1) / 2)
 #define W8_H8_BASE (W8_SWAP ? 0u : (u32)LDS_AES_BYTES)   // the W8 kernels' 8-bit H^8 table

@@ -202,6 +202,7 @@ __device__ unsigned long long g_ext_runs[EXT_RUN_ROWS][8];
 #define RC_CLAIM 6   // the first wave to find this run's queue empty scans the next run
 #define RC_LOG2 7    // the run's unit length: 2^RC_LOG2 steps (run_unit_log2)
 #define RC_HPNEXT 8  // seal_batch_hp: next header-protection mask of the previous run to hand out (hp_masks_pass)
+#define RC_MK 9      // (round 6) an MK run's connections (scan_mk), 0 for any other run
 
 // Scans the run that starts at record p into one run-state buffer, with ONE wave and no workgroup barrier, so that it
 // runs while the other waves are still busy with the previous run (the end-of-run tail where they would otherwise
@@ -229,10 +230,118 @@ __device__ __forceinline__ u32 run_unit_log2(u32 total_steps, u32 smax, u32 cap)
     return fill > chain ? fill : chain;
 }
 
+// (round 6) an MK run's key entry of table slot `slot` (common.h: slot 0 at RUN_KEY_OFF as in any run, slots 1.. over the
+// done / front words, which whole runs do not use)
+typedef __attribute__((address_space(3))) const KeyEntry lds_key_ct;
+__device__ __forceinline__ lds_key_ct *mk_key(lds_u32 *rs, u32 slot)
+{
+    return (lds_key_ct *)(slot == 0 ? rs + RUN_KEY_OFF : rs + RUN_DONE_OFF + (slot - 1) * (u32)(sizeof(KeyEntry) / 4));
+}
+static_assert(RUN_DONE_OFF + (MK_SLOTS - 1) * (int)(sizeof(KeyEntry) / 4) <= RUN_WORDS, "MK key entries in the run state");
+static_assert(MK_SLOTS * ((WHOLE_MIN_RECS + 15) / 16) <= CRUN_RECS + 16 && MK_SLOTS * MK_SLOT_BYTES <= 65536,
+              "MK claims in the ubase words, slots in [0, 64K)");
+
+// (round 6) scan_mk (EXT 4, many-key batches; called by scan_run once it has found that the run at p is the short
+// uniform records of one connection with fewer records than the workgroup has 8-lane groups, which it would otherwise
+// cut into units): joins that connection and the next ones into one multi-key whole run (common.h MK_RUNS) while each
+// is complete within the scan window (CRUN_RECS records; its last record followed by another key or the range end), has
+// fewer than WHOLE_MIN_RECS records, all of them accepted descriptors of a valid key, and all the run's records stay
+// within UNIFORM_SLACK steps of each other and under W8_MIN_STEPS steps -- so a W8 pair's EXT 3 kernel, which scans
+// without MK runs, takes none of these records and walks past them to the same run boundary. At least two
+// connections, else the run stays as scan_run makes it. One wave; writes the run state as scan_run does.
+template <bool OPEN, int FRAME>
+__device__ __forceinline__ bool scan_mk(const BatchArgs &args, u64 p, u64 end, lds_u32 *rs, const u32 (&kq)[CRUN_RECS / 64],
+                                        const u32 (&sq)[CRUN_RECS / 64])
+{
+    // (kq, sq: scan_run's descriptors of the window -- each record's key, and its steps if it may join, else ~0 -- so
+    // that this adds no memory round trip but the key entries')
+    constexpr u32 Q = CRUN_RECS / 64;
+    const u32 lane = lane_here();
+    const u32 lim = (u32)min(end - p, (u64)CRUN_RECS);
+    u64 chg[Q];
+#pragma unroll
+    for (u32 q = 0; q < Q; ++q) {
+        // the previous record's key: lane - 1, or lane 63 of the previous 64
+        u32 prev = (u32)__builtin_amdgcn_ds_bpermute((int)((lane - 1) & 63) * 4, (int)kq[q]);
+        if (lane == 0)
+            prev = q == 0 ? kq[0] : (u32)__builtin_amdgcn_readlane((int)kq[q == 0 ? 0 : q - 1], 63);
+        const u32 t = q * 64 + lane;
+        chg[q] = __ballot(t < lim && t > 0 && kq[q] != prev);
+    }
+    u32 b[MK_SLOTS + 1];
+    b[0] = 0;
+    u32 k = 0, lo = 0xffffffffu, hi = 0;
+#pragma unroll  // (b[] in registers: its indices constant)
+    for (u32 s = 0; s < MK_SLOTS; ++s) {
+        // the next connection's first record after b[s] (lim: none in the window)
+        u32 nb = lim;
+#pragma unroll
+        for (int q = Q - 1; q >= 0; --q) {
+            const u32 sh = b[s] + 1 > (u32)q * 64 ? b[s] + 1 - (u32)q * 64 : 0u;
+            const u64 m = sh >= 64 ? 0ull : chg[q] & (~0ull << sh);
+            if (m != 0)
+                nb = (u32)q * 64 + (u32)__builtin_ctzll(m);
+        }
+        if (!(nb < lim || p + lim == end) || nb - b[s] >= (u32)WHOLE_MIN_RECS)
+            break;
+        u32 mn = 0xffffffffu, mx = 0;
+#pragma unroll
+        for (u32 q = 0; q < Q; ++q) {
+            const u32 t = q * 64 + lane;
+            if (t >= b[s] && t < nb)
+                mn = min(mn, sq[q]), mx = max(mx, sq[q]);
+        }
+        mn = wave_min(mn), mx = wave_max(mx);
+        const u32 nlo = min(lo, mn), nhi = max(hi, mx);
+        if (mx >= (u32)W8_MIN_STEPS || nhi > nlo + UNIFORM_SLACK)  // (an ineligible record: mx = ~0)
+            break;
+        lo = nlo, hi = nhi, b[s + 1] = nb, k = s + 1;
+        if (nb >= lim)
+            break;
+    }
+    if (k < 2)
+        return false;
+    // claims: a connection's records 16 at a time; slot s = the connection's table slot
+    u32 nclaims = 0;
+#pragma unroll
+    for (u32 s = 0; s < MK_SLOTS; ++s) {
+        if (s >= k)
+            break;
+        const u32 cnt = b[s + 1] - b[s], ncl = (cnt + 15) / 16;
+        if (lane >= nclaims && lane < nclaims + ncl) {
+            const u32 i = lane - nclaims;
+            rs[RUN_UBASE_OFF + lane] = (b[s] + 16 * i) | min(16u, cnt - 16 * i) << 8 | s << 16;
+        }
+        nclaims += ncl;
+        if (s > 0) {  // the connection's key entry beside the first connection's (staged by scan_run)
+            const u32 qs = b[s] >> 6, kw = qs == 0 ? kq[0] : qs == 1 ? kq[1] : qs == 2 ? kq[2] : kq[3];
+            static_assert(Q == 4, "the selects above");
+            const u32 key = (u32)__builtin_amdgcn_readlane((int)kw, (int)(b[s] & 63));
+            lds_u32 *dst = rs + RUN_DONE_OFF + (s - 1) * (u32)(sizeof(KeyEntry) / 4);
+            dst[lane] = ((const u32 *)(args.keys + key))[lane];
+            dst[lane + 64] = ((const u32 *)(args.keys + key))[lane + 64];
+        }
+    }
+    if (lane == 0) {
+        rs[RC_KEY] = kq[0];
+        rs[RC_NEXT] = 0;
+        rs[RC_N] = b[k];
+        rs[RC_WHOLE] = 1;
+        rs[RC_UNITS] = nclaims;
+        rs[RC_HUGE] = 0;
+        rs[RC_CLAIM] = 0;
+        rs[RC_LOG2] = 0;
+        rs[RC_HPNEXT] = 0;
+        rs[RC_MK] = k;
+    }
+    return true;
+}
+
 // The only way a kernel instantiation (EXT) changes what scan_run returns: the spread kernel (EXT 1) scans its long
 // records as empty units. A W8 pair relies on its two kernels scanning identically -- EXT 4 lists (start, chunk end) of
 // the runs it leaves, and EXT 3 rebuilds exactly those runs from them -- so an EXT rule added here must keep EXT 3 and 4
-// equal (or the list must carry the run's length and EXT 3 check it).
+// equal (or the list must carry the run's length and EXT 3 check it). (Round 6: EXT 4 alone joins connections of short
+// records into MK runs, scan_mk; those hold no record of EXT 3's and end where EXT 3's own runs of them end.)
 constexpr bool scan_rule_of_ext(int ext) { return ext == 1; }
 static_assert(scan_rule_of_ext(3) == scan_rule_of_ext(4), "a W8 pair's kernels must scan runs identically");
 
@@ -249,15 +358,24 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
         ((lds_u32 *)(rs + RUN_KEY_OFF))[lane] = ((const u32 *)(args.keys + key))[lane],
         ((lds_u32 *)(rs + RUN_KEY_OFF))[lane + 64] = ((const u32 *)(args.keys + key))[lane + 64];
     u32 steps[Q], nc[Q], bkt[Q];
+    constexpr bool MKS = MK_RUNS && EXT == 4;
+    u32 mkk[MKS ? Q : 1], mks[MKS ? Q : 1];  // (MK: each record's key, and its steps if scan_mk may take it, else ~0)
     u32 n = lim;  // ends at the first record of another key
 #pragma unroll
     for (u32 q = 0; q < Q; ++q) {
         const u32 t = q * 64 + lane;
         steps[q] = nc[q] = bkt[q] = 0;
+        if constexpr (MKS)
+            mkk[q] = mks[q] = 0xffffffffu;
         bool other = false;
         if (t < lim) {
             ptls_mi355x_record_t r = recs[p + t];
             other = args.multi_key && r.key_idx != key;
+            if constexpr (MKS) {
+                mkk[q] = r.key_idx;
+                if (record_ok<FRAME>(args, r) && r.key_idx < args.nkeys)
+                    mks[q] = gcm_steps<OPEN, FRAME>(r);
+            }
             if (!record_ok<FRAME>(args, r) || (scan_rule_of_ext(EXT) && spread_long(args, r)))  // rejected or spread: one empty unit
                 r.len = 0, r.aad_len = 0, r.flags = 0;
             steps[q] = gcm_steps<OPEN, FRAME>(r);
@@ -274,6 +392,13 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
             smin = min(smin, steps[q]), smax = max(smax, steps[q]);
     smin = wave_min(smin);
     smax = wave_max(smax);
+    if constexpr (MK_RUNS && EXT == 4) {
+        // (round 6) a connection of short uniform records, fewer than the workgroup's groups: join the next
+        // connections into one multi-key whole run (scan_mk) instead of cutting it into units
+        if (args.multi_key && key < args.nkeys && n < (u32)WHOLE_MIN_RECS && smax < (u32)W8_MIN_STEPS &&
+            smax <= smin + UNIFORM_SLACK && scan_mk<OPEN, FRAME>(args, p, end, rs, mkk, mks))
+            return;
+    }
     // uniform run: every record is one unit (no partials), and a one-key batch may take a much longer run. A workgroup
     // with fewer records left than it has groups cuts them into units instead, so that a small batch (the per-record
     // picotls path is a batch of one) spreads over the workgroup's waves; so does a many-key run of fewer records than
@@ -389,6 +514,8 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
         rs[RC_CLAIM] = 0;
         rs[RC_LOG2] = log2;
         rs[RC_HPNEXT] = 0;
+        if constexpr (MK_RUNS && EXT == 4)  // (only EXT 4 reads it)
+            rs[RC_MK] = 0;
     }
 }
 
@@ -811,7 +938,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     u32 skipped_w8 = 0;  // (the pair's first kernel: the runs this workgroup left to the second one)
     // (test hook, ptls_mi355x_debug_counters) the runs this workgroup processed, and those in 4-lane groups: counted in
     // SGPRs, added to g_ext_runs once at the end (round 6: was one device-scope atomic per run)
-    u32 runs_here = 0, g4_here = 0;
+    u32 runs_here = 0, g4_here = 0, mk_here = 0;
     constexpr bool SPREAD = FRAME == 0 && EXT == 1;
     if constexpr (SPREAD) {  // a small one-key batch (spread_pieces): workgroup w < n takes record w unless it is long
         if (blockIdx.x >= n) {
@@ -908,6 +1035,8 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         const bool whole_run = __builtin_amdgcn_readfirstlane(rs[RC_WHOLE]);
         const u32 total_units = __builtin_amdgcn_readfirstlane(rs[RC_UNITS]);
         const u32 nhuge = __builtin_amdgcn_readfirstlane(rs[RC_HUGE]);
+        // (round 6) a multi-key run (EXT 4, scan_mk): its connections, 0 for any other run
+        const u32 mk_n = MK_RUNS && W8K && !W8TREE ? __builtin_amdgcn_readfirstlane(rs[RC_MK]) : 0u;
         // the run's unit length in steps (a power of two <= CHUNK_STEPS) and the key element of its combine power
         // H^(G * ustep): [7] = H^8, [9..12] = H^16..H^128, [8] = H^CHUNK_BLOCKS
         const u32 ulog2 = __builtin_amdgcn_readfirstlane(rs[RC_LOG2]), ustep = 1u << ulog2;
@@ -988,7 +1117,22 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         // (MEAS_BUILD_ONCE, measurement builds only: a workgroup's later runs keep its first run's tables -- wrong tags
         // for other keys -- to price the per-run build, profiles/r5/table_build_cost.txt)
         const bool key_new = key_idx != loaded_key && !(MEAS_BUILD_ONCE && loaded_key != 0xffffffffu);
-        if (w8run && (key_new || loaded_w8 != w8mode)) {
+        if (mk_n != 0) {
+            // (round 6) an MK run: each connection's H^4 and H as 4-bit window-major tables in its slot (ghash.h),
+            // 128 threads a table; the next other run rebuilds its own tables (loaded_key none)
+            static_assert(ENGINE_WG >= 2 * MK_SLOTS * 128, "a table per 128 threads");
+            const u32 t = threadIdx.x >> 7, slot = t >> 1;
+            if (slot < mk_n) {
+                lds_key_t *kp = mk_key(rs, slot);
+                const u32 el = (t & 1) ? 0u : 3u;  // H, H^4
+                build_elem_table_w4(lds, slot * MK_SLOT_BYTES + (t & 1) * GHASH_TABLE_BYTES,
+                                    u32x4{kp->h[el][0], kp->h[el][1], kp->h[el][2], kp->h[el][3]}, 128u * t);
+            }
+            __syncthreads();
+            loaded_key = 0xffffffffu;
+            loaded_usrc = 0xffffffffu;
+            loaded_w8 = 4;
+        } else if (w8run && (key_new || loaded_w8 != w8mode)) {
             // the 8-bit H^8 (H^4) table over slots 0..7, H in slot 8, and a cut run's combine power (or the tree's H^2)
             // at W8_TAB_COMB
             w8_build_tables(lds, (const lds_u8 *)key, whole ? 0xffffffffu : usrc, w8mode == 2, w8mode == 3 ? 3u : 7u);
@@ -1014,6 +1158,55 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             if (threadIdx.x == 0)
                 PROF_ADD(7, 1);
         }
+        if (MK_RUNS && W8K && !W8TREE && mk_n != 0) {
+            ++mk_here;  // (ptls_mi355x_debug_counters: MK runs)
+            {
+                // (round 6) an MK run: each wave claims one of the run's claims (up to 16 records of one connection,
+                // scan_mk) and runs them as a whole run's 4-lane groups do, with the connection's round keys and IV in
+                // SGPRs and its tables' slot (gmul4w, w8_lane_end4 on the slot's H)
+                constexpr u32 G4 = 4;
+                for (;;) {
+                    u32 cb = 0;
+                    if (lane_here() == 0)
+                        cb = atomicAdd((u32 *)&rs[RC_NEXT], 1u);
+                    cb = __builtin_amdgcn_readfirstlane(cb);
+                    if (cb >= total_units)
+                        break;
+                    const u32 e = __builtin_amdgcn_readfirstlane(rs[RUN_UBASE_OFF + cb]);
+                    const u32 mk_first = e & 0xffu, mk_cnt = (e >> 8) & 0xffu, slot = e >> 16;
+                    lds_key_t *kp = mk_key(rs, slot);
+                    u32 rkm[NR + 1][4];
+#pragma unroll
+                    for (int r = 0; r <= NR; ++r)
+#pragma unroll
+                        for (int c = 0; c < 4; ++c)
+                            rkm[r][c] = __builtin_amdgcn_readfirstlane(kp->rk[r][c]);
+                    const u32 mv0 = __builtin_amdgcn_readfirstlane(kp->iv[0]), mv1 = __builtin_amdgcn_readfirstlane(kp->iv[1]),
+                              mv2 = __builtin_amdgcn_readfirstlane(kp->iv[2]);
+                    u32x4 acc;
+                    u32 okw;
+                    {
+                        const u32 lane = lane_here(), j = lane % G4, qd = lane / G4;
+                        const u32 laneoff = (lane & 31) * 4 | W8_AES_BASE;
+                        const bool valid = qd < mk_cnt;
+                        ptls_mi355x_record_t r = {};
+                        if (valid)
+                            r = recs[pos + mk_first + qd];
+                        const bool live = valid && record_ok<FRAME>(args, r);  // (scan_mk took accepted ones only)
+                        if (!live)
+                            r.len = 0, r.aad_len = 0, r.flags = 0;
+                        const u32 ekslot = CLDS_PART + 16u * (threadIdx.x / G4);
+                        gcm_segment<NR, OPEN, 1, FRAME, CT, true, (int)G4, true>(
+                            args, lds, rkm, mv0, mv1, mv2, r, live, 0u, live ? 2u * gcm_steps<OPEN, FRAME>(r) : 0u, j, laneoff, 0u, acc,
+                            true, okw, true, ekslot, false, mk_kslot(slot));
+                    }
+                    asm volatile("" ::: "memory");
+                    const u32 qd = lane_here() / G4;
+                    if (OPEN && okw <= 1 && qd < mk_cnt)  // the tag check (its length lane)
+                        args.ok[ok_at(pos + mk_first + qd)] = (uint8_t)okw;
+                }
+            }
+        } else {
         PROF_STAMP(t2);
         u32 rk[NR + 1][4];
 #pragma unroll
@@ -1279,6 +1472,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                 PROF_ADD(11, stamp() - tc0), PROF_ADD(12, 1);
 #endif
         }
+        }  // (not an MK run)
         // the run's units are all handed out: the first wave to get here scans the next run into the other buffer
         // while the rest finish theirs
         u32 claim = 0;
@@ -1318,6 +1512,8 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             atomicAdd(&g_ext_runs[blockIdx.x % EXT_RUN_ROWS][EXT], (unsigned long long)runs_here);
         if (g4_here != 0)
             atomicAdd(&g_ext_runs[blockIdx.x % EXT_RUN_ROWS][7], (unsigned long long)g4_here);
+        if (MK_RUNS && EXT == 4 && mk_here != 0)
+            atomicAdd(&g_ext_runs[blockIdx.x % EXT_RUN_ROWS][6], (unsigned long long)mk_here);
     }
     if (kclock != nullptr && threadIdx.x == 0) {  // (vector stores and atomics only)
         const u64 t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();

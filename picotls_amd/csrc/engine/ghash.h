@@ -197,6 +197,83 @@ __device__ __forceinline__ u32x4 gmul8(const lds_u8 *, u32x4 t, u32 lane, W8Lane
     return acc;
 }
 
+// ------------------------------------------------------------------------------------------------ GHASH (multi-key runs)
+//
+// (round 6) Multi-key whole runs (MK runs, gcm_chunked_kernel EXT 4): the short records of up to MK_SLOTS connections
+// share one run, each connection's tables in a 16 KiB slot of the W8 map's [0, 64K): H^4 (the 4-lane Horner power) and H
+// (the segment end, w8_lane_end4), both 4-bit window-major (entry (w, n) at T + (w >> 4) * 4096 + n * 256 + (w & 15) *
+// 16, T = slot << 14). gmul4w is gmul8's scheme on that 4-bit table: lane l = lane & 15 takes window i ^ l at its i-th
+// lookup (i < 32), so the 16 lanes of a ds_read_b128 phase read 16 distinct bank groups (w & 15) for any data and any
+// slots (the slot is address bits 14-15): 32 conflict-free lookups per multiply instead of 16, in exchange for a table a
+// quarter of the 8-bit one's size. The operand is spread once per multiply into eight "nibble bytes" registers R[c]
+// (byte b of R[c] = nibble of window (4c + b) ^ l, with the slot's address bits above it), so a lookup's address is one
+// v_perm of R[c] and the window bytes L (gmul8's W8_SWAP form), as in gmul8.
+struct MK4Lane {
+    u32 s0, s1;  // v_perm selectors of R[2k], R[2k + 1] from (hi_k, lo_k) for this lane's bits 0-2
+};
+__device__ __forceinline__ MK4Lane mk4_lane(u32 lane)
+{
+    // byte b of R[2k + r] = (e even ? hi : lo) byte 2 (r ^ l2) + (e >> 1), e = b ^ (l & 3); perm(hi, lo, sel): hi is
+    // bytes 4-7, lo bytes 0-3
+    const u32 lb = lane & 3, l2 = (lane >> 2) & 1;
+    u32 s[2];
+#pragma unroll
+    for (u32 r = 0; r < 2; ++r) {
+        u32 sel = 0;
+#pragma unroll
+        for (u32 b = 0; b < 4; ++b) {
+            const u32 e = b ^ lb, byte = 2u * (r ^ l2) + (e >> 1);
+            sel |= ((e & 1u) ? byte : 4u + byte) << (8 * b);
+        }
+        s[r] = sel;
+    }
+    return MK4Lane{s[0], s[1]};
+}
+// t * (the 4-bit window-major table of slot `slot`) for this lane (W8Lane w: the window bytes L_0, W8_SWAP)
+__device__ __forceinline__ u32x4 gmul4w(const lds_u8 *, u32x4 t, W8Lane w, MK4Lane m, u32 kslot)
+{
+    static_assert(W8_SWAP, "the window bytes of gmul8's W8_SWAP form");
+    asm volatile("" : "+v"(w.base), "+v"(m.s0), "+v"(m.s1));
+    u32 L[4];
+#pragma unroll
+    for (u32 c = 0; c < 4; ++c)
+        L[c] = w.base ^ (c * 0x40404040u);
+    // dwords k <- k ^ (bit 3 of the lane), by the constant lane mask of lanes 8-15 of every 16 (gmul8)
+    u32 a0, a1, a2, a3;
+    asm("s_mov_b32 vcc_lo, 0xff00ff00\n\t"
+        "s_mov_b32 vcc_hi, 0xff00ff00\n\t"
+        "v_cndmask_b32 %0, %4, %5, vcc\n\t"
+        "v_cndmask_b32 %1, %5, %4, vcc\n\t"
+        "v_cndmask_b32 %2, %6, %7, vcc\n\t"
+        "v_cndmask_b32 %3, %7, %6, vcc"
+        : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3)
+        : "v"(t[0]), "v"(t[1]), "v"(t[2]), "v"(t[3])
+        : "vcc");
+    const u32 a[4] = {a0, a1, a2, a3};
+    u32 R[8];
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) {
+        const u32 lo = (a[k] & 0x0f0f0f0fu) | kslot, hi = ((a[k] >> 4) & 0x0f0f0f0fu) | kslot;
+        R[2 * k] = __builtin_amdgcn_perm(hi, lo, m.s0);
+        R[2 * k + 1] = __builtin_amdgcn_perm(hi, lo, m.s1);
+    }
+    if (CT_PROBE_CONST)
+#pragma unroll
+        for (u32 c = 0; c < 8; ++c)
+            R[c] = kslot * 0x01010101u;
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (u32 i = 0; i < 32; i += 2) {
+        const u32 c = i >> 2, b = i & 3, off = c >= 4 ? 4096u : 0u;
+        const u32x4 e0 = lds_load128(__builtin_amdgcn_perm(R[c], L[c & 3], 0x0c0c0000u | ((4u + b) << 8) | b) + off);
+        const u32x4 e1 = lds_load128(__builtin_amdgcn_perm(R[c], L[c & 3], 0x0c0c0000u | ((5u + b) << 8) | (b + 1)) + off);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            acc[k] = xor3(acc[k], e0[k], e1[k]);
+    }
+    return acc;
+}
+
 // A group's product by the unit combine power (table 8) or another combine element: with SEG_COOP gmul_group_w
 // (window-major, conflict-free by construction) in both modes; without it, the constant-time mode gmul_tab (every lane
 // the whole product from the same rows of a nibble-major table) and the default mode gmul_group
@@ -495,10 +572,10 @@ __device__ __forceinline__ u32x4 group4_allreduce(u32x4 t)
 }
 // The W8 segment end of a 4-lane group: sum_j a_j H^(4 - rank_j) = ((v_0 H + v_1) H + v_2) H + v_3) H over the ranks, a
 // scattered chain of four group products with the window-major H table (32 lookups per product, 8 per lane)
-__device__ __forceinline__ u32x4 w8_lane_end4(const lds_u8 *, u32x4 v, u32 lane, u32 rank)
+__device__ __forceinline__ u32x4 w8_lane_end4(const lds_u8 *, u32x4 v, u32 lane, u32 rank, u32 htab = W8_TAB_H)
 {
     const u32x4 z = {0, 0, 0, 0};
-    const Group4Ws k = group4_ws(W8_TAB_H, lane);
+    const Group4Ws k = group4_ws(htab, lane);
     u32 g = group4_scatter(rank == 0 ? v : z, lane);
 #pragma unroll
     for (u32 r = 1; r < 4; ++r)

@@ -198,4 +198,37 @@ __device__ __forceinline__ void build_elem_table(lds_u8 *lds, u32 base, u32x4 h,
         store_window<false>(lds + base + p * 256, v, ec, c);
 }
 
+// (round 6, MK runs) the same window-major table by 128 threads [tid0, tid0 + 128): four per window, each deriving the
+// window's elements and storing 4 of its 16 entries (entries n with n >> 2 == the thread's quarter), so that the eight
+// tables of a multi-key run take the whole workgroup at once
+__device__ __forceinline__ void build_elem_table_w4(lds_u8 *lds, u32 base, u32x4 h, u32 tid0)
+{
+    const u32 i = threadIdx.x - tid0, p = i >> 2, qt = i & 3;
+    if (i >= 128)
+        return;
+    u32 b0 = bswap32(h[0]), b1 = bswap32(h[1]), b2 = bswap32(h[2]), b3 = bswap32(h[3]);
+    for (u32 k = 0; k < (p >> 3); ++k)
+        gf_mulxs_be(b0, b1, b2, b3, 32);
+    if (p & 7)
+        gf_mulxs_be(b0, b1, b2, b3, 4 * (p & 7));
+    u32x4 v[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        v[m] = u32x4{bswap32(b0), bswap32(b1), bswap32(b2), bswap32(b3)};
+        if (m < 3)
+            gf_mulxs_be(b0, b1, b2, b3, 1);
+    }
+    lds_u8 *row = lds + base + (p >> 4) * 4096 + (p & 15) * 16;
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) {
+        const u32 n = 4 * qt + k;
+        u32x4 e = {0, 0, 0, 0};
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            if ((n >> (3 - m)) & 1u)
+                e ^= v[m];
+        *(lds_u32x4 *)(row + n * 256) = e;
+    }
+}
+
 #endif  // PTLS_MI355X_ENGINE_LDS_TABLES_H

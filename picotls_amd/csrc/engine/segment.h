@@ -33,11 +33,12 @@
 // (ekslot) until the tree is done, and is added on the length lane only (lane jl: the lane the tag or the unit partial
 // is taken from). The round-2 form (CT_TREE 0) ran four multiplies, H^8, H^4, H^2, H^1 kept on the bits of e, in every
 // step in which some lane of the wave was at its last position (two or more steps per segment).
-template <int NR, bool OPEN, int NB, int FRAME = 0, bool CT = false, bool W8 = false, int GG = ENGINE_G>
+template <int NR, bool OPEN, int NB, int FRAME = 0, bool CT = false, bool W8 = false, int GG = ENGINE_G, bool MK4 = false>
 __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 *lds, const u32 (&rk)[NR + 1][4], u32 iv0,
                                             u32 iv1, u32 iv2, const ptls_mi355x_record_t &r, bool valid, u32 m_lo,
                                             u32 m_hi, u32 j, u32 laneoff, u32 tsel_horner, u32x4 &acc, bool finish,
-                                            u32 &okw, bool aligned, u32 ekslot = 0, bool w8tree = false)
+                                            u32 &okw, bool aligned, u32 ekslot = 0, bool w8tree = false,
+                                            u32 mk_kslot = MK_NONE)
 {
     // G lanes per record: ENGINE_G, or 4 in the W8 serial kernel's whole runs (ghash.h, 4-lane groups), whose aligned
     // streams then put text blocks on 64-byte boundaries (a group stores 64 bytes a step)
@@ -51,6 +52,18 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     W8Lane w8 = {};
     if constexpr (W8)
         w8 = w8_lane(lane_here());
+    // (round 6) MK4: a multi-key run's record (4-lane groups of the W8 serial kernel): the Horner on its connection's
+    // 4-bit H^4 table (gmul4w) and the segment end on its H table, in the table slot mk_kslot names (ghash.h)
+    static_assert(!MK4 || (W8 && G == 4), "MK runs are 4-lane W8 runs");
+    MK4Lane mk4 = {};
+    if constexpr (MK4)
+        mk4 = mk4_lane(lane_here());
+    auto horner = [&](u32x4 t) -> u32x4 {
+        if constexpr (MK4)
+            return gmul4w(lds, t, w8, mk4, mk_kslot);
+        else
+            return gmul8(lds, t, GMUL8_LANE(), w8);
+    };
     constexpr bool SEAL_FRAME = FRAME == 1 && !OPEN, OPEN_FRAME = FRAME == 1 && OPEN, TLS12 = FRAME == 2;
     const u32 L = gcm_text_len<OPEN, FRAME>(r), A = gcm_aad_len<OPEN, FRAME>(r);
     // bytes of text readable at src (a framed seal reads len payload bytes; its last text byte is the content type)
@@ -284,7 +297,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 if constexpr (W8)
-                    acc = gmul8(lds, acc ^ (OPEN ? cur : o), GMUL8_LANE(), w8);
+                    acc = horner(acc ^ (OPEN ? cur : o));
                 else
                     acc = gmul_tab(lds, acc ^ (OPEN ? cur : o), tsel_horner);
                 __builtin_amdgcn_sched_barrier(0);
@@ -358,7 +371,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             const u32x4 t = acc ^ X;
             u32x4 prod = t;
             if (s0 + 1 < Smax) {
-                prod = gmul8(lds, t, GMUL8_LANE(), w8);
+                prod = horner(t);
                 if ((int)m0 == m_last)
                     prod = t;
             }
@@ -417,7 +430,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             prod = t;
             if (s0 + 1 < Smax) {
                 if constexpr (W8)
-                    prod = gmul8(lds, t, GMUL8_LANE(), w8);
+                    prod = horner(t);
                 else
                     prod = gmul_tab(lds, t, tsel_horner);
                 if (last_here)
@@ -444,7 +457,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         // (w8tree, the EXT 3 kernel's long whole records: the butterfly over the ranks with H and H^2 nibble-major)
         const u32 rank = valid ? (u32)G - e_last : j;
         if constexpr (G == 4)
-            acc = w8_lane_end4(lds, acc, lane_here(), rank);
+            acc = w8_lane_end4(lds, acc, lane_here(), rank, MK4 ? mk_htab(mk_kslot) : (u32)W8_TAB_H);
         else if (w8tree)
             acc = w8_tree_end(lds, acc, lane_here(), rank);
         else

@@ -375,3 +375,50 @@ def test_w8_pair_run_list_vs_fusion(ref):
     for c in (seen["seal"], opened):
         assert c["launches"]["w8_tree"] == 1 and c["runs"]["w8_tree"] >= 500 and c["runs"]["w8_g4"] >= 500, c
     ks.free()
+
+
+@pytest.mark.parametrize("length,aad,key_size,per_key,n", [
+    (1200, 13, 16, 64, 256 * 256), (1200, 13, 32, 64, 40000), (37, 0, 16, 48, 30000), (600, 21, 16, 17, 30000),
+    (3000, 13, 32, 100, 40000), (1, 5, 16, 5, 20000)])
+def test_w8_multi_key_runs_vs_fusion(ref, length, aad, key_size, per_key, n):
+    """(round 6) Multi-key runs (MK runs, gcm_kernels.h scan_mk): a many-key batch's connections of short uniform
+    records with fewer records than the workgroup has groups (QUIC packets of many connections) are joined, up to four
+    connections and 256 records, into one whole run in 4-lane groups, each connection's tables in its own LDS slot
+    (ghash.h gmul4w). Connections of 5 to 100 records (claims of 16 records, partial claims), 1 to 3000-byte records,
+    AES-128 and AES-256, against fusion, sealed and opened with tampering; the counters show MK runs in both."""
+    rng = np.random.default_rng(8800 + length + per_key)
+    nkeys = (n + per_key - 1) // per_key
+    key = np.arange(n) // per_key
+    b = RecordBatch.build(np.full(n, length), np.full(n, aad), seqs=rng.integers(0, 2**62, n, dtype=np.uint64),
+                          key_idx=key)
+    keys = np.frombuffer(rng.bytes(nkeys * key_size), np.uint8)
+    ivs = np.frombuffer(rng.bytes(nkeys * 12), np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aadb = np.frombuffer(rng.bytes(max(b.aad_bytes, 1)), np.uint8)
+    ks = pa.Keyset(keys, ivs, key_size)
+    pa.debug_counters(reset=True)
+    sealed = gpu_seal(ks, b.seal, pt, aadb, b.sealed_bytes)
+    c_seal = pa.debug_counters(reset=True)
+    want = np.zeros(b.sealed_bytes, np.uint8)
+    ref.run_batch(True, keys, ivs, key_size, b.seal, pt, aadb, want, nthreads=8)
+    bad_recs = [i for i in range(n) if not np.array_equal(
+        sealed[int(b.seal[i]["out_off"]):int(b.seal[i]["out_off"]) + length + 16],
+        want[int(b.seal[i]["out_off"]):int(b.seal[i]["out_off"]) + length + 16])]
+    assert bad_recs == [], f"{len(bad_recs)} records differ from fusion, first {bad_recs[:8]}"
+    assert np.array_equal(sealed, want)
+    victims = rng.choice(n, 16, replace=False)
+    bad = want.copy()
+    for t, v in enumerate(victims):
+        bad[int(b.open[v]["in_off"]) + int(rng.integers(0, length + 16))] ^= 1 << (t % 8)
+    back, ok = gpu_open(ks, b.open, bad, aadb, b.pt_bytes)
+    c_open = pa.debug_counters(reset=True)
+    expect_ok = np.ones(n, np.uint8)
+    expect_ok[victims] = 0
+    assert np.array_equal(ok, expect_ok)
+    ref_back = np.zeros(b.pt_bytes, np.uint8)
+    ref.run_batch(False, keys, ivs, key_size, b.open, bad, aadb, ref_back, ok=np.zeros(n, np.uint8), nthreads=8)
+    assert np.array_equal(back, ref_back)
+    # most connections run in MK runs (a workgroup's range edges leave a few cut ones)
+    for c in (c_seal, c_open):
+        assert c["runs"]["w8_mk"] >= 0.5 * nkeys / 4, (c, nkeys)
+    ks.free()
