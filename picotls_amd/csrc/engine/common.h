@@ -228,6 +228,9 @@ __device__ __forceinline__ u32 lane_here()
 #ifndef MK_RUNS
 #define MK_RUNS 1
 #endif
+#ifndef MK_EARLY_SCAN
+#define MK_EARLY_SCAN 1
+#endif
 #define MK_SLOTS 4
 #define MK_NONE 0xffffffffu
 #define MK_SLOT_BYTES 16384

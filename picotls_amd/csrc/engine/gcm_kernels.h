@@ -251,7 +251,7 @@ static_assert(MK_SLOTS * ((WHOLE_MIN_RECS + 15) / 16) <= CRUN_RECS + 16 && MK_SL
 // connections, else the run stays as scan_run makes it. One wave; writes the run state as scan_run does.
 template <bool OPEN, int FRAME>
 __device__ __forceinline__ bool scan_mk(const BatchArgs &args, u64 p, u64 end, lds_u32 *rs, const u32 (&kq)[CRUN_RECS / 64],
-                                        const u32 (&sq)[CRUN_RECS / 64])
+                                        const u32 (&sq)[CRUN_RECS / 64], u32 key_after)
 {
     // (kq, sq: scan_run's descriptors of the window -- each record's key, and its steps if it may join, else ~0 -- so
     // that this adds no memory round trip but the key entries')
@@ -282,7 +282,11 @@ __device__ __forceinline__ bool scan_mk(const BatchArgs &args, u64 p, u64 end, l
             if (m != 0)
                 nb = (u32)q * 64 + (u32)__builtin_ctzll(m);
         }
-        if (!(nb < lim || p + lim == end) || nb - b[s] >= (u32)WHOLE_MIN_RECS)
+        // complete: another key follows within the window, or the range ends there, or (a connection ending exactly at
+        // a full window) the record after the window has another key
+        const bool complete = nb < lim || p + lim == end ||
+                              key_after != (u32)__builtin_amdgcn_readlane((int)kq[Q - 1], 63);
+        if (!complete || nb - b[s] >= (u32)WHOLE_MIN_RECS)
             break;
         u32 mn = 0xffffffffu, mx = 0;
 #pragma unroll
@@ -360,7 +364,22 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
     u32 steps[Q], nc[Q], bkt[Q];
     constexpr bool MKS = MK_RUNS && EXT == 4;
     u32 mkk[MKS ? Q : 1], mks[MKS ? Q : 1];  // (MK: each record's key, and its steps if scan_mk may take it, else ~0)
+    // (MK: the key of the record after a full window, so that a connection ending exactly there counts as complete)
+    const u32 mk_after = MKS && args.multi_key && lim == (u32)CRUN_RECS && p + lim < end ? recs[p + lim].key_idx : 0xffffffffu;
     u32 n = lim;  // ends at the first record of another key
+    // (round 6) the fields the scan reads -- len, key_idx, aad_len | flags << 16: 12 bytes at offset 28 -- loaded for all
+    // Q record slots before any is used (a lane past the run's end re-reads the run's last record), so the window costs
+    // one memory round trip; loaded whole and under the t < lim branch, the compiler issued the slots one trip each
+    static_assert(offsetof(ptls_mi355x_record_t, len) == 28 && offsetof(ptls_mi355x_record_t, key_idx) == 32 &&
+                      offsetof(ptls_mi355x_record_t, aad_len) == 36 && offsetof(ptls_mi355x_record_t, flags) == 38,
+                  "descriptor layout");
+    u32 dl[Q], dk[Q], da[Q];
+#pragma unroll
+    for (u32 q = 0; q < Q; ++q) {
+        const u32 t = q * 64 + lane, tt = t < lim ? t : lim - 1;
+        const u32 *w = (const u32 *)(recs + p + tt) + 7;
+        dl[q] = w[0], dk[q] = w[1], da[q] = w[2];
+    }
 #pragma unroll
     for (u32 q = 0; q < Q; ++q) {
         const u32 t = q * 64 + lane;
@@ -369,7 +388,8 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
             mkk[q] = mks[q] = 0xffffffffu;
         bool other = false;
         if (t < lim) {
-            ptls_mi355x_record_t r = recs[p + t];
+            ptls_mi355x_record_t r = {};
+            r.len = dl[q], r.key_idx = dk[q], r.aad_len = (uint16_t)da[q], r.flags = (uint16_t)(da[q] >> 16);
             other = args.multi_key && r.key_idx != key;
             if constexpr (MKS) {
                 mkk[q] = r.key_idx;
@@ -396,7 +416,7 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
         // (round 6) a connection of short uniform records, fewer than the workgroup's groups: join the next
         // connections into one multi-key whole run (scan_mk) instead of cutting it into units
         if (args.multi_key && key < args.nkeys && n < (u32)WHOLE_MIN_RECS && smax < (u32)W8_MIN_STEPS &&
-            smax <= smin + UNIFORM_SLACK && scan_mk<OPEN, FRAME>(args, p, end, rs, mkk, mks))
+            smax <= smin + UNIFORM_SLACK && scan_mk<OPEN, FRAME>(args, p, end, rs, mkk, mks, mk_after))
             return;
     }
     // uniform run: every record is one unit (no partials), and a one-key batch may take a much longer run. A workgroup
@@ -1158,8 +1178,27 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
             if (threadIdx.x == 0)
                 PROF_ADD(7, 1);
         }
+#if ENGINE_PROFILE
+        unsigned long long t2 = stamp();
+#endif
         if (MK_RUNS && W8K && !W8TREE && mk_n != 0) {
             ++mk_here;  // (ptls_mi355x_debug_counters: MK runs)
+#if MK_EARLY_SCAN
+            // the workgroup's last wave scans the next run before it claims: the scan's memory round trips then wait
+            // while the other waves work, instead of after the claims, when all of them would wait for it
+            if (wave == ENGINE_WG / 64 - 1) {
+                u32 claim = 0;
+                if (lane_here() == 0)
+                    claim = atomicAdd((u32 *)&rs[RC_CLAIM], 1u) == 0;
+                PROF_STAMP(ts0);
+                if (__builtin_amdgcn_readfirstlane(claim) && nxt < nxt_end)
+                    scan_run<OPEN, FRAME, false, EXT>(args, recs, nxt, nxt_end, rs_next);
+#if ENGINE_PROFILE
+                if (lane_here() == 0)  // [15] the early scans' cycles
+                    PROF_ADD(15, stamp() - ts0);
+#endif
+            }
+#endif
             {
                 // (round 6) an MK run: each wave claims one of the run's claims (up to 16 records of one connection,
                 // scan_mk) and runs them as a whole run's 4-lane groups do, with the connection's round keys and IV in
@@ -1172,6 +1211,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                     cb = __builtin_amdgcn_readfirstlane(cb);
                     if (cb >= total_units)
                         break;
+                    PROF_STAMP(tc0);
                     const u32 e = __builtin_amdgcn_readfirstlane(rs[RUN_UBASE_OFF + cb]);
                     const u32 mk_first = e & 0xffu, mk_cnt = (e >> 8) & 0xffu, slot = e >> 16;
                     lds_key_t *kp = mk_key(rs, slot);
@@ -1204,10 +1244,16 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
                     const u32 qd = lane_here() / G4;
                     if (OPEN && okw <= 1 && qd < mk_cnt)  // the tag check (its length lane)
                         args.ok[ok_at(pos + mk_first + qd)] = (uint8_t)okw;
+#if ENGINE_PROFILE
+                    if (lane_here() == 0)  // [13] MK claims' cycles, [14] MK claims
+                        PROF_ADD(13, stamp() - tc0), PROF_ADD(14, 1);
+#endif
                 }
             }
         } else {
-        PROF_STAMP(t2);
+#if ENGINE_PROFILE
+        t2 = stamp();
+#endif
         u32 rk[NR + 1][4];
 #pragma unroll
         for (int r = 0; r <= NR; ++r)

@@ -203,7 +203,8 @@ __device__ __forceinline__ void build_elem_table(lds_u8 *lds, u32 base, u32x4 h,
 // tables of a multi-key run take the whole workgroup at once
 __device__ __forceinline__ void build_elem_table_w4(lds_u8 *lds, u32 base, u32x4 h, u32 tid0)
 {
-    const u32 i = threadIdx.x - tid0, p = i >> 2, qt = i & 3;
+    // (window p = i mod 32, quarter i / 32: the 16 lanes of a store phase write 16 windows, i.e. 16 distinct bank groups)
+    const u32 i = threadIdx.x - tid0, p = i & 31, qt = i >> 5;
     if (i >= 128)
         return;
     u32 b0 = bswap32(h[0]), b1 = bswap32(h[1]), b2 = bswap32(h[2]), b3 = bswap32(h[3]);

@@ -62,6 +62,9 @@ def main():
     if p[12]:
         print(f"  unit tails (partial store, record combine, tag): {p[11] / p[12]:.0f} cycles per wave-round, "
               f"{100 * p[11] / 16 / max(p[2], 1):.1f} % of the unit loop")
+    if p[14]:
+        print(f"  MK claims: {p[13] / p[14]:.0f} cycles per claim ({p[14] / runs:.1f} a run); early scans "
+              f"{p[15] / runs:.0f} cycles per run")
     waves = 16
     print(f"  wave idle at unit-loop barrier: {p[4] / runs / waves:.0f} cycles/run/wave "
           f"({100 * p[4] / waves / max(p[2], 1):.1f} % of the unit loop)")
