@@ -197,6 +197,15 @@ static int set_kernel_attrs(void)
     CHUNKED_ATTR_X(14, true, 0, 1);
     CHUNKED_ATTR_X(10, false, 0, 2);
     CHUNKED_ATTR_X(14, false, 0, 2);
+#if MK_RUNS  // (round 6) the serial W8 kernel of many-key batches, with multi-key runs (EXT 5)
+#define CHUNKED_ATTR_MK(frame)                                                                                         \
+    CHUNKED_ATTR_X(10, false, frame, 5);                                                                               \
+    CHUNKED_ATTR_X(10, true, frame, 5);                                                                                \
+    CHUNKED_ATTR_X(14, false, frame, 5);                                                                               \
+    CHUNKED_ATTR_X(14, true, frame, 5)
+#else
+#define CHUNKED_ATTR_MK(frame) (void)0
+#endif
 #define CHUNKED_ATTR_W8(frame)                                                                                         \
     CHUNKED_ATTR_X(10, false, frame, 3);                                                                               \
     CHUNKED_ATTR_X(10, true, frame, 3);                                                                                \
@@ -205,7 +214,8 @@ static int set_kernel_attrs(void)
     CHUNKED_ATTR_X(10, false, frame, 4);                                                                               \
     CHUNKED_ATTR_X(10, true, frame, 4);                                                                                \
     CHUNKED_ATTR_X(14, false, frame, 4);                                                                               \
-    CHUNKED_ATTR_X(14, true, frame, 4)
+    CHUNKED_ATTR_X(14, true, frame, 4);                                                                                \
+    CHUNKED_ATTR_MK(frame)
 #if W8_HORNER
     CHUNKED_ATTR_W8(0);
     CHUNKED_ATTR_W8(1);
@@ -1023,7 +1033,7 @@ static bool use_chunked(int schedule) { return schedule != PTLS_MI355X_SCHEDULE_
 template <int NR, bool OPEN, int FRAME, int EXT = 0>
 static void launch_chunked_x(bool ct, unsigned grid, hipStream_t s, const BatchArgs &a)
 {
-    COUNT_LAUNCH(EXT);
+    COUNT_LAUNCH(EXT == 5 ? 4 : EXT);  // (the MK form of the serial W8 kernel counts as it)
 #if SEG_COOP
     (void)ct;
     gcm_chunked_kernel<NR, OPEN, FRAME, true, EXT><<<grid, ENGINE_WG, CLDS_ALLOC, s>>>(a);
@@ -1067,7 +1077,12 @@ static void launch_chunked(bool ct, unsigned grid, hipStream_t s, const BatchArg
             b.w8_split = whole_possible ? 2u : 1u;
             if (!whole_possible)
                 b.w8_flags = nullptr;
-            launch_chunked_x<NR, OPEN, FRAME, 4>(ct, grid, s, b);
+            // (round 6) many-key batches take EXT 5: EXT 4 plus multi-key runs (gcm_kernels.h scan_mk); one-key batches
+            // keep EXT 4, whose code the MK path would grow (small launches slowed by 5-14 % with it compiled in)
+            if (MK_RUNS && a.multi_key)
+                launch_chunked_x<NR, OPEN, FRAME, 5>(ct, grid, s, b);
+            else
+                launch_chunked_x<NR, OPEN, FRAME, 4>(ct, grid, s, b);
             if (whole_possible)
                 launch_chunked_x<NR, OPEN, FRAME, 3>(ct, grid, s, b);
             return;

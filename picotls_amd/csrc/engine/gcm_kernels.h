@@ -344,10 +344,12 @@ __device__ __forceinline__ bool scan_mk(const BatchArgs &args, u64 p, u64 end, l
 // The only way a kernel instantiation (EXT) changes what scan_run returns: the spread kernel (EXT 1) scans its long
 // records as empty units. A W8 pair relies on its two kernels scanning identically -- EXT 4 lists (start, chunk end) of
 // the runs it leaves, and EXT 3 rebuilds exactly those runs from them -- so an EXT rule added here must keep EXT 3 and 4
-// equal (or the list must carry the run's length and EXT 3 check it). (Round 6: EXT 4 alone joins connections of short
-// records into MK runs, scan_mk; those hold no record of EXT 3's and end where EXT 3's own runs of them end.)
+// equal (or the list must carry the run's length and EXT 3 check it). (Round 6: EXT 5, the serial kernel of many-key
+// batches, also joins connections of short records into MK runs, scan_mk; those hold no record of EXT 3's and end where
+// EXT 3's own runs of them end.)
 constexpr bool scan_rule_of_ext(int ext) { return ext == 1; }
-static_assert(scan_rule_of_ext(3) == scan_rule_of_ext(4), "a W8 pair's kernels must scan runs identically");
+static_assert(scan_rule_of_ext(3) == scan_rule_of_ext(4) && scan_rule_of_ext(3) == scan_rule_of_ext(5),
+              "a W8 pair's kernels must scan runs identically");
 
 template <bool OPEN, int FRAME, bool FIRST = false, int EXT = 0>
 __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355x_record_t *__restrict__ recs, u64 p, u64 end,
@@ -362,7 +364,7 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
         ((lds_u32 *)(rs + RUN_KEY_OFF))[lane] = ((const u32 *)(args.keys + key))[lane],
         ((lds_u32 *)(rs + RUN_KEY_OFF))[lane + 64] = ((const u32 *)(args.keys + key))[lane + 64];
     u32 steps[Q], nc[Q], bkt[Q];
-    constexpr bool MKS = MK_RUNS && EXT == 4;
+    constexpr bool MKS = MK_RUNS && EXT == 5;
     u32 mkk[MKS ? Q : 1], mks[MKS ? Q : 1];  // (MK: each record's key, and its steps if scan_mk may take it, else ~0)
     // (MK: the key of the record after a full window, so that a connection ending exactly there counts as complete)
     const u32 mk_after = MKS && args.multi_key && lim == (u32)CRUN_RECS && p + lim < end ? recs[p + lim].key_idx : 0xffffffffu;
@@ -412,7 +414,7 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
             smin = min(smin, steps[q]), smax = max(smax, steps[q]);
     smin = wave_min(smin);
     smax = wave_max(smax);
-    if constexpr (MK_RUNS && EXT == 4) {
+    if constexpr (MK_RUNS && EXT == 5) {
         // (round 6) a connection of short uniform records, fewer than the workgroup's groups: join the next
         // connections into one multi-key whole run (scan_mk) instead of cutting it into units
         if (args.multi_key && key < args.nkeys && n < (u32)WHOLE_MIN_RECS && smax < (u32)W8_MIN_STEPS &&
@@ -534,7 +536,7 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
         rs[RC_CLAIM] = 0;
         rs[RC_LOG2] = log2;
         rs[RC_HPNEXT] = 0;
-        if constexpr (MK_RUNS && EXT == 4)  // (only EXT 4 reads it)
+        if constexpr (MK_RUNS && EXT == 5)  // (only the MK kernel reads it)
             rs[RC_MK] = 0;
     }
 }
@@ -933,7 +935,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     // (the lane index and what derives from it are computed in the unit loop, lane_here())
     const u32 wave = threadIdx.x >> 6;
     const u32 tsel_horner = 0x10000u + (u32)(G - 1) * GHASH_TABLE_BYTES;
-    constexpr bool W8K = W8_HORNER && (EXT == 3 || EXT == 4);  // a W8 kernel (launch_chunked)
+    constexpr bool W8K = W8_HORNER && (EXT == 3 || EXT == 4 || EXT == 5);  // a W8 kernel (launch_chunked)
     constexpr bool W8TREE = W8_HORNER && EXT == 3;                  // ... with the butterfly segment end
     // the unit combine table: slot 8, or in the W8 kernel's map W8_TAB_COMB
     const u32 tsel_chunk = W8K ? (u32)W8_TAB_COMB : 0x10000u + 8u * GHASH_TABLE_BYTES;
@@ -1056,7 +1058,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         const u32 total_units = __builtin_amdgcn_readfirstlane(rs[RC_UNITS]);
         const u32 nhuge = __builtin_amdgcn_readfirstlane(rs[RC_HUGE]);
         // (round 6) a multi-key run (EXT 4, scan_mk): its connections, 0 for any other run
-        const u32 mk_n = MK_RUNS && W8K && !W8TREE ? __builtin_amdgcn_readfirstlane(rs[RC_MK]) : 0u;
+        const u32 mk_n = MK_RUNS && EXT == 5 ? __builtin_amdgcn_readfirstlane(rs[RC_MK]) : 0u;
         // the run's unit length in steps (a power of two <= CHUNK_STEPS) and the key element of its combine power
         // H^(G * ustep): [7] = H^8, [9..12] = H^16..H^128, [8] = H^CHUNK_BLOCKS
         const u32 ulog2 = __builtin_amdgcn_readfirstlane(rs[RC_LOG2]), ustep = 1u << ulog2;
@@ -1181,7 +1183,7 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
 #if ENGINE_PROFILE
         unsigned long long t2 = stamp();
 #endif
-        if (MK_RUNS && W8K && !W8TREE && mk_n != 0) {
+        if (MK_RUNS && EXT == 5 && mk_n != 0) {
             ++mk_here;  // (ptls_mi355x_debug_counters: MK runs)
 #if MK_EARLY_SCAN
             // the workgroup's last wave scans the next run before it claims: the scan's memory round trips then wait
@@ -1555,10 +1557,10 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     }
     if (ENGINE_HOOKS && threadIdx.x == 0) {
         if (runs_here != 0)
-            atomicAdd(&g_ext_runs[blockIdx.x % EXT_RUN_ROWS][EXT], (unsigned long long)runs_here);
+            atomicAdd(&g_ext_runs[blockIdx.x % EXT_RUN_ROWS][EXT == 5 ? 4 : EXT], (unsigned long long)runs_here);
         if (g4_here != 0)
             atomicAdd(&g_ext_runs[blockIdx.x % EXT_RUN_ROWS][7], (unsigned long long)g4_here);
-        if (MK_RUNS && EXT == 4 && mk_here != 0)
+        if (MK_RUNS && EXT == 5 && mk_here != 0)
             atomicAdd(&g_ext_runs[blockIdx.x % EXT_RUN_ROWS][6], (unsigned long long)mk_here);
     }
     if (kclock != nullptr && threadIdx.x == 0) {  // (vector stores and atomics only)
