@@ -7,9 +7,12 @@
 //   mode 3: mode 2 with non-temporal loads and stores
 //   mode 4: mode 2 with a line's two halves accessed together: a store held one step and issued beside the next
 //           one, both halves of a line loaded in its first step
+//   mode 5: mode 2 with record r's quad steps shifted by 16 (r mod 4) bytes (round 6: the 1200-byte open reads its
+//           1216-byte ciphertext records in steps aligned to the 1200-byte plaintext, i.e. 16-byte-shifted 64-byte
+//           pieces that straddle half lines)
 // with SPIN dependent VALU operations between steps (the AES work between a group's stores in the real kernel).
 //   hipcc --offload-arch=gfx950 -O3 tools/mb/wcal.hip -o tools/mb/wcal.bin
-//   wcal <mode 0..4> <load 0|1> <records> <len> <spin> <reps>
+//   wcal <mode 0..5> <load 0|1> <records> <len> <spin> <reps>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -17,7 +20,7 @@
 typedef unsigned int u32;
 typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 
-template <int GL, int V = 0>  // lanes per record (0: wave-wide stream); V 1 non-temporal, 2 paired halves
+template <int GL, int V = 0>  // lanes per record (0: wave-wide stream); V 1 non-temporal, 2 paired halves, 3 shifted
 __global__ __launch_bounds__(256) void wcal(unsigned char *buf, unsigned long long nrec, u32 len, u32 spin, int load,
                                             u32 *sink)
 {
@@ -40,12 +43,12 @@ __global__ __launch_bounds__(256) void wcal(unsigned char *buf, unsigned long lo
         const u32 j = lane % GL;
         const unsigned long long groups = (unsigned long long)gridDim.x * (256 / GL);
         for (unsigned long long r = (blockIdx.x * 256ull + threadIdx.x) / GL; r < nrec; r += groups) {
-            const unsigned long long s = r * len, e = s + len;
-            const unsigned long long c0 = s / (16 * GL), c1 = (e + 16 * GL - 1) / (16 * GL);
+            const unsigned long long s = r * len, e = s + len, sh = V == 3 ? 16 * (r & 3) : 0;
+            const unsigned long long c0 = (s - sh) / (16 * GL), c1 = (e - sh + 16 * GL - 1) / (16 * GL);
             u32x4 held = {0, 0, 0, 0};
             bool have = false;
             for (unsigned long long c = c0; c < c1; ++c) {
-                const unsigned long long a = c * 16 * GL + 16 * j;
+                const unsigned long long a = c * 16 * GL + 16 * j + sh;
                 const bool in = a >= s && a < e;
                 u32x4 *p = (u32x4 *)(buf + a);
                 if (V == 2) {
@@ -97,13 +100,13 @@ __global__ __launch_bounds__(256) void wcal(unsigned char *buf, unsigned long lo
 int main(int argc, char **argv)
 {
     if (argc < 7) {
-        fprintf(stderr, "usage: wcal <mode 0..4> <load 0|1> <records> <len> <spin> <reps>\n");
+        fprintf(stderr, "usage: wcal <mode 0..5> <load 0|1> <records> <len> <spin> <reps>\n");
         return 2;
     }
     const int mode = atoi(argv[1]), load = atoi(argv[2]), reps = atoi(argv[6]);
     const unsigned long long nrec = strtoull(argv[3], 0, 10);
     const u32 len = (u32)atoi(argv[4]), spin = (u32)atoi(argv[5]);
-    if (len % 16 != 0 || mode < 0 || mode > 4 || nrec == 0 || nrec * len > (16ull << 30)) {
+    if (len % 16 != 0 || mode < 0 || mode > 5 || nrec == 0 || nrec * len > (16ull << 30)) {
         fprintf(stderr, "bad arguments\n");
         return 2;
     }
@@ -127,8 +130,10 @@ int main(int argc, char **argv)
             wcal<4><<<grid, 256>>>(buf, nrec, len, spin, load, sink);
         else if (mode == 3)
             wcal<4, 1><<<grid, 256>>>(buf, nrec, len, spin, load, sink);
-        else
+        else if (mode == 4)
             wcal<4, 2><<<grid, 256>>>(buf, nrec, len, spin, load, sink);
+        else
+            wcal<4, 3><<<grid, 256>>>(buf, nrec, len, spin, load, sink);
         hipEventRecord(e1, 0);
         if (hipEventSynchronize(e1) != hipSuccess)
             return 1;
