@@ -2,7 +2,7 @@
 """AES-GCM seal+open throughput of the MI355X record engine (BASELINE.json metric), device-resident.
 
     python bench.py [--gpus N --steps K --warmup W] [--workload tls16k]
-                    [--extra quic1200,mixed,mixedrand,shard1200,ptlsbench] [--no-cpu-baseline] [--no-e2e]
+                    [--extra quic1200,mixed,mixedrand,shard1200,ptlsbench,quic64k,tls64k] [--no-cpu-baseline] [--no-e2e]
 
 One step = seal the whole batch, then open the sealed batch again (one launch each), inputs already in HBM.
 value = (sum L sealed + sum L opened) over all ranks / max-over-ranks wall time of the K timed steps, in GiB/s
@@ -25,7 +25,9 @@ Also reported:
                 own rate (both directions busy); never `value`
   extra         the other BASELINE configs at full size: quic1200 (configs[2]), mixed / mixedrand (configs[3], keys
                 grouped by connection / in random order as SURVEY §8(d) writes it), ptlsbench (configs[0]: 1000-record
-                batches under t/ptlsbench.c's conventions, on the GPU; fusion beside it in cpu_baseline)
+                batches under t/ptlsbench.c's conventions, on the GPU; fusion beside it in cpu_baseline), and two
+                many-connection shapes: quic64k (4M x 1200 B over 64K connections, the
+                multi-key runs of round 6) and tls64k (1M x 16 KiB over 64K connections)
 """
 from __future__ import annotations
 
@@ -50,7 +52,7 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", default="tls16k")
-    p.add_argument("--extra", default="quic1200,mixed,mixedrand,shard1200,ptlsbench",
+    p.add_argument("--extra", default="quic1200,mixed,mixedrand,shard1200,ptlsbench,quic64k,tls64k",
                    help="comma list of extra workloads to report ('' for none)")
     p.add_argument("--records", type=int, default=0, help="override record count (smaller runs)")
     p.add_argument("--no-cpu-baseline", action="store_true")

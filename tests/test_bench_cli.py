@@ -13,7 +13,7 @@ def test_default_legs_cover_every_baseline_config(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py"])
     a = bench.parse()
     assert a.gpus == 1 and a.workload == "tls16k"
-    assert set(a.extra.split(",")) == {"quic1200", "mixed", "mixedrand", "shard1200", "ptlsbench"}
+    assert set(a.extra.split(",")) == {"quic1200", "mixed", "mixedrand", "shard1200", "ptlsbench", "quic64k", "tls64k"}
     assert a.e2e is None  # on for N = 1 at full size (main), off with --no-e2e
     monkeypatch.setattr(sys, "argv", ["bench.py", "--no-e2e"])
     assert bench.parse().e2e is False
