@@ -36,7 +36,7 @@ ptls_mi355x_keyset_t *ptls_mi355x_aead_get_keyset(ptls_aead_context_t *ctx);
  * boundary: fusion's `__m128i ctr` is passed as its 16 bytes in memory (what _mm_storeu_si128(p, ctr) writes), so a
  * caller switches with one store. The GCM nonce is the counter's upper 12 bytes, byte-reversed (the layout
  * calc_counter builds, lib/fusion.c:1126-1133); as in fusion's encrypt, the low 32 bits are ignored there (fusion sets
- * them to 1 for E(K, J0), lib/fusion.c:489), and decrypt takes them zero (below). One engine keyset per context; a call is a per-record launch, so use the
+ * them to 1 for E(K, J0), lib/fusion.c:489), and decrypt counts from them as fusion's does (below). One engine keyset per context; a call is a per-record launch, so use the
  * batch API of picotls/mi355x.h for throughput. The contexts are not thread-safe (fusion's are not either).
  */
 typedef struct ptls_mi355x_aesgcm_context ptls_mi355x_aesgcm_context_t;
@@ -56,8 +56,10 @@ void ptls_mi355x_aesgcm_free(ptls_mi355x_aesgcm_context_t *ctx);
 void ptls_mi355x_aesgcm_encrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, const void *input, size_t inlen,
                                 const void *ctr, const void *aad, size_t aadlen, ptls_aead_supplementary_encryption_t *supp);
 /* ptls_fusion_aesgcm_decrypt: 1 if the tag verifies (plaintext in output), else 0 (the plaintext is written either way,
- * as fusion's). The counter's low 32 bits must be zero, as calc_counter leaves them: fusion's decrypt counts from them
- * (lib/fusion.c:680) while its encrypt ignores them, so with other values no record verifies; here output is zeroed */
+ * as fusion's). fusion's decrypt counts from the counter's low 32 bits (lib/fusion.c:679-682: a 64-bit add on the
+ * register's low half, E(K, J0) at low + 1, data block b at low + 2 + b) while its encrypt ignores them; calc_counter
+ * leaves them zero. This decrypt does the same for any value (round 6): with non-zero low bits the output is that
+ * keystream XOR the input and the tag holds iff it equals GHASH ^ E(K, counter + 1), bit for bit fusion's result */
 int ptls_mi355x_aesgcm_decrypt(ptls_mi355x_aesgcm_context_t *ctx, void *output, const void *input, size_t inlen,
                                const void *ctr, const void *aad, size_t aadlen, const void *tag);
 
