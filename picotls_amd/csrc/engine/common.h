@@ -211,6 +211,16 @@ __device__ __forceinline__ u32 lane_here()
 #ifndef G4_PAIR_STORES
 #define G4_PAIR_STORES 1
 #endif
+// (round 6) a 4-lane group's open aligns its steps to the record's text, not to its output (segment.h): text block 0
+// starts a step, so the AAD step needs no keystream, as in the seal (1200-byte open: 19 AES steps instead of 20)
+#ifndef G4_OPEN_TEXT_STEPS
+#define G4_OPEN_TEXT_STEPS 1
+#endif
+// ... and its steady steps, no longer aligned to the output's lines, still store every 128-byte line in one step: a lane
+// holds up to two blocks (the line's halves) until the step that produces the line's last block (segment.h)
+#ifndef G4_LINE_HOLD
+#define G4_LINE_HOLD 1
+#endif
 // ... and 8-lane groups whose steps straddle lines (cut runs' units) store each line in one step (segment.h)
 #ifndef G8_PAIR_STORES
 #define G8_PAIR_STORES 1

@@ -77,6 +77,11 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     if (aligned) {  // text block b at position P + na + b, and (dst / 16 + b) mod G == that position mod G
         const u32 K0 = (total + G - 1) / G;
         P = (int)(((u32)((uintptr_t)dst >> 4) - na) & (G - 1));
+        // (round 6) a 4-lane open puts text block 0 at a step's start instead: the steps before it need no keystream
+        // (the seal's aligned output gives it the same padding), and the steady steps hold their blocks until a line is
+        // whole (G4_LINE_HOLD)
+        if constexpr (G4_OPEN_TEXT_STEPS && OPEN && G == 4)
+            P = (int)((0u - na) & (G - 1));
         // ... unless that costs a record shorter than ALIGN_MIN_STEPS steps one more step (its wave would take it too:
         // -6 % on 1200-byte records), which keeps the padding of a multiple of G positions
         if ((u32)P + total > K0 * G && K0 < ALIGN_MIN_STEPS)
@@ -254,9 +259,22 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             u32 off = 16u * (u32)b0;                               // its byte offset in the text
             u32 ctr = (u32)b0 + 2;
             // G4_PAIR_STORES: the block held from the previous step (the first half of its line), stored with this one
-            constexpr bool PAIR = G4_PAIR_STORES && G == 4;
+            constexpr bool LINE = G4_LINE_HOLD && G4_OPEN_TEXT_STEPS && OPEN && G == 4;
+            constexpr bool PAIR = G4_PAIR_STORES && G == 4 && !LINE;
             u32x4 held = {0, 0, 0, 0};
             bool have = false;
+            // G4_LINE_HOLD (a 4-lane open, its steps aligned to the text, not to the output): held = the lane's block
+            // in a line's first half, held2 its block in the second half (the next step's). The line is whole at the
+            // second half's step, or one step later for a lane past its first half's line offset ("late": j >
+            // (dst + off) / 16 mod 4, the line's last block falls in the next step); then the lane stores both. Late
+            // lanes store from dst - 64, so both kinds store at p - 64 and p
+            u32x4 held2 = {0, 0, 0, 0};
+            bool late = false;
+            uint8_t *dst_l = dst;
+            if constexpr (LINE) {
+                late = j > (((u32)(uintptr_t)(dst + off) >> 4) & 3u);
+                dst_l = dst - (late ? 64 : 0);
+            }
             // G8_PAIR_STORES: a group whose steps straddle lines (a cut run's unit, counted from the stream's end) --
             // the lanes past the line boundary (the same lanes every step) hold their blocks one step, so each line is
             // stored by one step's instructions; uniform over the wave: no lane straddles in an aligned stream
@@ -274,7 +292,20 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                 aes_ctr_cached1<NR>(lds, laneoff, rk, cc1, st);
                 __builtin_amdgcn_sched_barrier(0);
                 const u32x4 o = cur ^ u32x4{st[0][0], st[0][1], st[0][2], st[0][3]};
-                if constexpr (PAIR) {
+                if constexpr (LINE) {
+                    const bool first = (((u32)(uintptr_t)(dst + off)) & 64u) == 0;
+                    if (!first)
+                        held2 = o;
+                    if (first == late) {  // the held line is whole at this step (held from inside the range only)
+                        uint8_t *p = dst_l + off;
+                        if (s >= sa + 1 + (int)late)
+                            *(u32x4_u *)(p - 64) = held;
+                        if (!late || s > sa)
+                            *(u32x4_u *)p = held2;
+                    }
+                    if (first)
+                        held = o;
+                } else if constexpr (PAIR) {
                     if ((((uintptr_t)(dst + off)) & 64u) == 0 && s + 1 < sb) {
                         held = o;
                         have = true;
@@ -303,6 +334,16 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                 __builtin_amdgcn_sched_barrier(0);
                 ctr += G;
                 off += 16 * G;
+            }
+            if constexpr (LINE) {  // the blocks still held after the range's last step
+                uint8_t *p = dst + off - 16 * G;
+                if ((((u32)(uintptr_t)p) & 64u) == 0) {
+                    *(u32x4_u *)p = held;
+                } else if (late) {
+                    *(u32x4_u *)p = held2;
+                    if (sb - 1 > sa)
+                        *(u32x4_u *)(p - 64) = held;
+                }
             }
             s0 = (u32)sb;  // (a block in the range's last step is stored at once: nothing is held past it)
         }

@@ -422,3 +422,54 @@ def test_w8_multi_key_runs_vs_fusion(ref, length, aad, key_size, per_key, n):
     for c in (c_seal, c_open):
         assert c["runs"]["w8_mk"] >= 0.5 * nkeys / 4, (c, nkeys)
     ks.free()
+
+
+@pytest.mark.parametrize("length,aad,key_size,per_key,shift", [
+    (1200, 13, 16, 0, "16"), (1200, 13, 16, 0, "byte"), (1000, 0, 32, 0, "16"), (200, 40, 16, 0, "16"),
+    (100, 17, 16, 0, "byte"), (4095, 13, 16, 0, "16"), (63, 5, 32, 0, "16"), (1200, 13, 16, 64, "16"),
+    (700, 21, 32, 40, "byte")])
+def test_w8_g4_open_into_shifted_outputs_vs_fusion(ref, length, aad, key_size, per_key, shift):
+    """(round 6) A 4-lane group's open aligns its steps to the record's text (G4_OPEN_TEXT_STEPS), so its output is no
+    longer aligned to the steps, and its steady steps hold blocks until a 128-byte line is whole (G4_LINE_HOLD: early
+    and late lanes, the range's first and last steps). The plaintexts go to outputs shifted by 16 x (i mod 8) bytes or
+    by any byte count, for one key (short whole runs) and for connections of 40-64 records (MK runs), with AADs of
+    0-3 blocks (text block 0 at every position of a step); every byte of the output buffer, tags and ok bytes against
+    fusion, with tampering."""
+    rng = np.random.default_rng(8900 + length + aad + per_key + (1 if shift == "byte" else 0))
+    n = 256 * 130
+    nkeys = 1 if per_key == 0 else (n + per_key - 1) // per_key
+    key = None if per_key == 0 else np.arange(n) // per_key
+    b = RecordBatch.build(np.full(n, length), np.full(n, aad), seqs=rng.integers(0, 2**62, n, dtype=np.uint64),
+                          key_idx=key)
+    keys = np.frombuffer(rng.bytes(nkeys * key_size), np.uint8)
+    ivs = np.frombuffer(rng.bytes(nkeys * 12), np.uint8)
+    pt = np.frombuffer(rng.bytes(b.pt_bytes), np.uint8)
+    aadb = np.frombuffer(rng.bytes(max(b.aad_bytes, 1)), np.uint8)
+    sealed = np.zeros(b.sealed_bytes, np.uint8)
+    ref.run_batch(True, keys, ivs, key_size, b.seal, pt, aadb, sealed, nthreads=8)
+    victims = rng.choice(n, 16, replace=False)
+    for t, v in enumerate(victims):
+        sealed[int(b.open[v]["in_off"]) + int(rng.integers(0, length + 16))] ^= 1 << (t % 8)
+    recs = b.open.copy()
+    stride = (length + 127) // 128 * 128 + 128
+    sh = 16 * (np.arange(n) % 8) if shift == "16" else (np.arange(n) * 37) % 128
+    recs["out_off"] = (np.arange(n) * stride + sh).astype(np.uint64)
+    out_bytes = n * stride + 128
+    ks = pa.Keyset(keys, ivs, key_size)
+    pa.debug_counters(reset=True)
+    back, ok = gpu_open(ks, recs, sealed, aadb, out_bytes, out_fill=0x5A)
+    c = pa.debug_counters(reset=True)
+    expect_ok = np.ones(n, np.uint8)
+    expect_ok[victims] = 0
+    assert np.array_equal(ok, expect_ok)
+    ref_back = np.full(out_bytes, 0x5A, np.uint8)
+    ref.run_batch(False, keys, ivs, key_size, recs, sealed, aadb, ref_back, ok=np.zeros(n, np.uint8), nthreads=8)
+    bad_recs = [i for i in range(n) if not np.array_equal(back[i * stride:(i + 1) * stride],
+                                                          ref_back[i * stride:(i + 1) * stride])]
+    assert bad_recs == [], f"{len(bad_recs)} record slots differ from fusion, first {bad_recs[:8]}"
+    assert np.array_equal(back, ref_back)
+    if per_key == 0:
+        assert c["runs"]["w8_g4"] >= 200, c
+    else:
+        assert c["runs"]["w8_mk"] >= 0.5 * nkeys / 4, (c, nkeys)
+    ks.free()
