@@ -221,6 +221,13 @@ __device__ __forceinline__ u32 lane_here()
 #ifndef G4_LINE_HOLD
 #define G4_LINE_HOLD 1
 #endif
+// (round 6) the serial W8 kernels' waves issue by the steps left in their segment (s_setprio 3..0 in bands of this many
+// steps, segment.h): the waves of a SIMD then end equal claims together instead of in the order of their age, which
+// left a run's last wave alone on its SIMD. tls64k +4.3 %, quic64k +5.0 %, mixed +0.7 %, quic1200 +0.4 %; the tree
+// kernel keeps its issue order (tls16k -2.3 % with it) (profiles/r6/progress_prio_ab.txt); 0: off
+#ifndef PROGRESS_PRIO
+#define PROGRESS_PRIO 4
+#endif
 // ... and 8-lane groups whose steps straddle lines (cut runs' units) store each line in one step (segment.h)
 #ifndef G8_PAIR_STORES
 #define G8_PAIR_STORES 1

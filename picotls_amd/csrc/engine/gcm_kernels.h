@@ -1526,6 +1526,9 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
         u32 claim = 0;
         if (lane_here() == 0)
             claim = atomicAdd((u32 *)&rs[RC_CLAIM], 1u) == 0;
+#if ENGINE_PROFILE
+        PROF_STAMP(tsc);
+#endif
         if (__builtin_amdgcn_readfirstlane(claim) && nxt < nxt_end)
             scan_run<OPEN, FRAME, false, EXT>(args, recs, nxt, nxt_end, rs_next);
         PROF_STAMP(tw);
@@ -1536,6 +1539,9 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
 #if ENGINE_PROFILE
         if (lane_here() == 0)
             PROF_ADD(4, t3 - tw);
+        // (not an MK run) [13] the tail scan's cycles, [14] the scanning wave's wait at the barrier after it
+        if (lane_here() == 0 && mk_n == 0 && __builtin_amdgcn_readfirstlane(claim) && nxt < nxt_end)
+            PROF_ADD(13, tw - tsc), PROF_ADD(14, t3 - tw);
         if (threadIdx.x == 0) {
             PROF_ADD(0, t1 - t0);
             PROF_ADD(1, t2 - t1);

@@ -253,7 +253,25 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     sa = wave_smax_perg<G>(sa);
     sb = wave_smin_perg<G>(sb);
 
+    // (round 6, PROGRESS_PRIO) the waves of a SIMD issue by the work they have left in the segment: the one furthest
+    // behind first, so that equal claims end together instead of in the issue order's age skew (a run's last wave
+    // otherwise finishes alone on its SIMD)
+    auto progress_prio = [&](u32 left) {
+        if constexpr (PROGRESS_PRIO && W8) {
+            if (w8tree)  // (the tree kernel's long whole runs: measured -2.3 % on tls16k with it)
+                return;
+            if (left > 3u * PROGRESS_PRIO)
+                __builtin_amdgcn_s_setprio(3);
+            else if (left > 2u * PROGRESS_PRIO)
+                __builtin_amdgcn_s_setprio(2);
+            else if (left > 1u * PROGRESS_PRIO)
+                __builtin_amdgcn_s_setprio(1);
+            else
+                __builtin_amdgcn_s_setprio(0);
+        }
+    };
     for (u32 s0 = 0; s0 < Smax; ++s0) {
+        progress_prio(Smax - s0);
         if ((int)s0 == sa && sb > sa) {
             const int b0 = (int)(j + G * (m_lo + (u32)sa)) - D0;  // this lane's text block at step sa
             u32 off = 16u * (u32)b0;                               // its byte offset in the text
@@ -282,6 +300,8 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             // (unframed batches: the TLS-framed kernels measured slower with it, TLS 1.2 1200-byte seal -1.4 %)
             const bool pair8 = G8_PAIR_STORES && G == 8 && W8 && FRAME == 0 && !aligned && __any(holder);
             for (int s = sa; s < sb; ++s) {
+                if ((s & 3) == 0)
+                    progress_prio(Smax - (u32)s);
                 cur = nxt[0];
                 nxt[0] = *(const u32x4_u *)(src + off + 16 * G);
                 u32 st[1][4] = {{n0, n1, n2, bswap32(ctr) ^ rk[0][3]}};
@@ -484,6 +504,9 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             acc = prod ^ ek0;
         __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (PROGRESS_PRIO && W8)
+        if (!w8tree)
+            __builtin_amdgcn_s_setprio(0);
 
     static_assert(G == 8 || W8, "dpp_xor8 reduces groups of 8 lanes");
     // (round 5) an open's received tag is loaded before the segment end, whose lookups hide its latency (loaded after

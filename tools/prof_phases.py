@@ -62,7 +62,10 @@ def main():
     if p[12]:
         print(f"  unit tails (partial store, record combine, tag): {p[11] / p[12]:.0f} cycles per wave-round, "
               f"{100 * p[11] / 16 / max(p[2], 1):.1f} % of the unit loop")
-    if p[14]:
+    if p[14] and p[12]:  # (not MK: the tail scans, ENGINE_PROFILE slots 13-14)
+        print(f"  tail scans: {p[13] / runs:.0f} cycles per run; the scanning wave then waits {p[14] / runs:.0f} cycles "
+              f"at the barrier")
+    elif p[14]:
         print(f"  MK claims: {p[13] / p[14]:.0f} cycles per claim ({p[14] / runs:.1f} a run); early scans "
               f"{p[15] / runs:.0f} cycles per run")
     waves = 16
