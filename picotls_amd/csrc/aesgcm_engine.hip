@@ -847,9 +847,9 @@ void ptls_mi355x_keyset_free(ptls_mi355x_keyset_t *ks)
 int ptls_mi355x_debug_profile(unsigned long long *out, int reset)
 {
     HIP_TRY(hipDeviceSynchronize());
-    static unsigned long long rows[PROF_ROWS][16];
+    static unsigned long long rows[PROF_ROWS][PROF_SLOTS];
     HIP_TRY(hipMemcpyFromSymbol(rows, HIP_SYMBOL(g_prof), sizeof(g_prof)));
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < PROF_SLOTS; ++i) {
         out[i] = 0;
         for (int r = 0; r < PROF_ROWS; ++r)
             out[i] += rows[r][i];

@@ -430,4 +430,31 @@ __device__ __forceinline__ void publish_done(u32 *flags, u32 token)
         __hip_atomic_store(flags + blockIdx.x, token, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Diagnostic build only (-DENGINE_PROFILE=1): s_memtime stamps of the chunked kernel's phases, summed over runs and
+// workgroups: [0] run setup, [1] GHASH table build, [2] unit loop, [3] kernel prologue (AES tables, first scan), [4] wave idle at the unit-loop barrier,
+// [5] units, [6] runs, [7] table builds.
+#ifndef ENGINE_PROFILE
+#define ENGINE_PROFILE 0
+#endif
+#if ENGINE_PROFILE
+// one row of counters per workgroup (blockIdx.x mod PROF_ROWS): the rows are summed on the host, so the counter
+// atomics of 256 workgroups do not queue on one address inside the phases they measure
+#define PROF_ROWS 1024
+#define PROF_SLOTS 24
+__device__ unsigned long long g_prof[PROF_ROWS][PROF_SLOTS];
+__device__ __forceinline__ unsigned long long stamp()
+{
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define PROF_STAMP(v) const unsigned long long v = stamp()
+#define PROF_ADD(i, v) atomicAdd(&g_prof[blockIdx.x % PROF_ROWS][i], (unsigned long long)(v))
+#else
+#define PROF_STAMP(v)
+#define PROF_ADD(i, x)
+#endif
+
 #endif  // PTLS_MI355X_ENGINE_COMMON_H

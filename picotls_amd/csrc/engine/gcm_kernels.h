@@ -139,31 +139,6 @@ __global__ __launch_bounds__(ENGINE_WG) __attribute__((amdgpu_waves_per_eu(ENGIN
     }
 }
 
-// Diagnostic build only (-DENGINE_PROFILE=1): s_memtime stamps of the chunked kernel's phases, summed over runs and
-// workgroups: [0] run setup, [1] GHASH table build, [2] unit loop, [3] kernel prologue (AES tables, first scan), [4] wave idle at the unit-loop barrier,
-// [5] units, [6] runs, [7] table builds.
-#ifndef ENGINE_PROFILE
-#define ENGINE_PROFILE 0
-#endif
-#if ENGINE_PROFILE
-// one row of counters per workgroup (blockIdx.x mod PROF_ROWS): the rows are summed on the host, so the counter
-// atomics of 256 workgroups do not queue on one address inside the phases they measure
-#define PROF_ROWS 1024
-__device__ unsigned long long g_prof[PROF_ROWS][16];
-__device__ __forceinline__ unsigned long long stamp()
-{
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-#define PROF_STAMP(v) const unsigned long long v = stamp()
-#define PROF_ADD(i, v) atomicAdd(&g_prof[blockIdx.x % PROF_ROWS][i], (unsigned long long)(v))
-#else
-#define PROF_STAMP(v)
-#define PROF_ADD(i, x)
-#endif
 
 // Runs processed per chunked instantiation (EXT 0..4), one row per workgroup (blockIdx.x mod EXT_RUN_ROWS), summed on the
 // host by ptls_mi355x_debug_counters: the evidence that a batch ran in the kernel a test means to exercise (one

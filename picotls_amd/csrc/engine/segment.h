@@ -44,6 +44,9 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     // streams then put text blocks on 64-byte boundaries (a group stores 64 bytes a step)
     constexpr int G = GG;
     static_assert(G == 8 || (G == 4 && W8), "8-lane groups, or 4-lane groups in the W8 kernels");
+#if ENGINE_PROFILE
+    const unsigned long long tsg0 = stamp();
+#endif
     constexpr int GS = G == 8 ? 3 : 2;  // log2 G
     // W8 (a W8 run of the pair's EXT 3 kernel, gcm_chunked_kernel): Horner on the 8-bit H^8 table (gmul8), the lanes'
     // last powers by a serial Horner over the group's ranks with the window-major H table (W8_TAB_H, w8_lane_end)
@@ -270,6 +273,9 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                 __builtin_amdgcn_s_setprio(0);
         }
     };
+#if ENGINE_PROFILE
+    const unsigned long long tsg1 = stamp();
+#endif
     for (u32 s0 = 0; s0 < Smax; ++s0) {
         progress_prio(Smax - s0);
         if ((int)s0 == sa && sb > sa) {
@@ -507,6 +513,9 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     if constexpr (PROGRESS_PRIO && W8)
         if (!w8tree)
             __builtin_amdgcn_s_setprio(0);
+#if ENGINE_PROFILE
+    const unsigned long long tsg2 = stamp();
+#endif
 
     static_assert(G == 8 || W8, "dpp_xor8 reduces groups of 8 lanes");
     // (round 5) an open's received tag is loaded before the segment end, whose lookups hide its latency (loaded after
@@ -579,6 +588,12 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
             *(u32x4_u *)(dst + L) = tag;
         }
     }
+#if ENGINE_PROFILE
+    if (W8 && !w8tree && lane_here() == 0) {  // [16] setup, [17] steps, [18] end of the serial W8 kernels' segments, [19] segments
+        const unsigned long long tsg3 = stamp();
+        PROF_ADD(16, tsg1 - tsg0), PROF_ADD(17, tsg2 - tsg1), PROF_ADD(18, tsg3 - tsg2), PROF_ADD(19, 1);
+    }
+#endif
 }
 
 #endif  // PTLS_MI355X_ENGINE_SEGMENT_H

@@ -25,7 +25,7 @@ def main():
     calls = 300
     for _ in range(20):
         enc.encrypt(pt, 7, aad)
-    prof = (ctypes.c_ulonglong * 16)()
+    prof = (ctypes.c_ulonglong * 24)()  # PROF_SLOTS
     dbg = getattr(lib, "ptls_mi355x_debug_profile", None)  # exported by -DENGINE_PROFILE=1 builds only
     if dbg is not None:
         dbg.argtypes = [ctypes.c_void_p, ctypes.c_int]

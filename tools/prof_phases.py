@@ -37,7 +37,7 @@ def main():
     ks = ctypes.c_void_p(lib.ptls_mi355x_keyset_new(keys.ctypes.data, ivs.ctypes.data, wl.nkeys, wl.key_size))
     lib.ptls_mi355x_keyset_set_schedule(ks, a.schedule)
     s = torch.cuda.current_stream().cuda_stream
-    prof = (ctypes.c_ulonglong * 16)()
+    prof = (ctypes.c_ulonglong * 24)()  # PROF_SLOTS
     lib.ptls_mi355x_seal_batch(ks, d_seal.data_ptr(), b.n, d_pt.data_ptr(), d_aad.data_ptr(), sealed.data_ptr(), s)
     torch.cuda.synchronize()
     lib.ptls_mi355x_debug_profile(prof, 1)
@@ -62,12 +62,17 @@ def main():
     if p[12]:
         print(f"  unit tails (partial store, record combine, tag): {p[11] / p[12]:.0f} cycles per wave-round, "
               f"{100 * p[11] / 16 / max(p[2], 1):.1f} % of the unit loop")
-    if p[14] and p[12]:  # (not MK: the tail scans, ENGINE_PROFILE slots 13-14)
+    if p[14] and not p[15]:  # (no MK run: the tail scans, ENGINE_PROFILE slots 13-14)
         print(f"  tail scans: {p[13] / runs:.0f} cycles per run; the scanning wave then waits {p[14] / runs:.0f} cycles "
               f"at the barrier")
     elif p[14]:
         print(f"  MK claims: {p[13] / p[14]:.0f} cycles per claim ({p[14] / runs:.1f} a run); early scans "
               f"{p[15] / runs:.0f} cycles per run")
+    if p[19]:
+        seg = p[16] + p[17] + p[18]
+        print(f"  segments (serial W8 kernels, per wave): {p[19] / a.reps:.0f} a launch; setup {p[16] / p[19]:.0f}, steps "
+              f"{p[17] / p[19]:.0f}, end {p[18] / p[19]:.0f} cycles each ({100 * p[16] / seg:.1f} / {100 * p[17] / seg:.1f} / "
+              f"{100 * p[18] / seg:.1f} %)")
     waves = 16
     print(f"  wave idle at unit-loop barrier: {p[4] / runs / waves:.0f} cycles/run/wave "
           f"({100 * p[4] / waves / max(p[2], 1):.1f} % of the unit loop)")
