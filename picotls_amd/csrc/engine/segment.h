@@ -592,6 +592,8 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     if (W8 && !w8tree && lane_here() == 0) {  // [16] setup, [17] steps, [18] end of the serial W8 kernels' segments, [19] segments
         const unsigned long long tsg3 = stamp();
         PROF_ADD(16, tsg1 - tsg0), PROF_ADD(17, tsg2 - tsg1), PROF_ADD(18, tsg3 - tsg2), PROF_ADD(19, 1);
+        // [20] the wave's steps, [21] of them in the steady form
+        PROF_ADD(20, Smax), PROF_ADD(21, sb > sa ? (u32)(sb - sa) : 0u);
     }
 #endif
 }
