@@ -48,10 +48,35 @@ __device__ __forceinline__ u32x4 load_partial_raw(const uint8_t *p, u32 n)
     return v;
 }
 
+// stores bytes 0..n-1 of v (n < 16): (round 6, STORE_PARTIAL_BITS) an 8-, 4-, 2- and 1-byte store by the bits of n,
+// each from the low end of the bytes left, instead of n byte stores (a wave looped max n times over its lanes)
+typedef unsigned long long __attribute__((aligned(1))) u64_u;
+typedef unsigned short __attribute__((aligned(1))) u16_u;
+#ifndef STORE_PARTIAL_BITS
+#define STORE_PARTIAL_BITS 1
+#endif
 __device__ __forceinline__ void store_partial(uint8_t *p, u32x4 v, u32 n)
 {
-    for (u32 i = 0; i < n; ++i)
-        p[i] = (uint8_t)(v[i >> 2] >> (8 * (i & 3)));
+    if constexpr (STORE_PARTIAL_BITS) {
+        u32 a = v[0], b = v[1];
+        if (n & 8) {
+            *(u64_u *)p = (unsigned long long)b << 32 | a;
+            p += 8, a = v[2], b = v[3];
+        }
+        if (n & 4) {
+            *(u32_u *)p = a;
+            p += 4, a = b;
+        }
+        if (n & 2) {
+            *(u16_u *)p = (unsigned short)a;
+            p += 2, a >>= 16;
+        }
+        if (n & 1)
+            *p = (uint8_t)a;
+    } else {
+        for (u32 i = 0; i < n; ++i)
+            p[i] = (uint8_t)(v[i >> 2] >> (8 * (i & 3)));
+    }
 }
 
 // ------------------------------------------------------------------------------------------------ main kernel

@@ -275,10 +275,14 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     };
 #if ENGINE_PROFILE
     const unsigned long long tsg1 = stamp();
+    unsigned long long tsteady = 0;
 #endif
     for (u32 s0 = 0; s0 < Smax; ++s0) {
         progress_prio(Smax - s0);
         if ((int)s0 == sa && sb > sa) {
+#if ENGINE_PROFILE
+            const unsigned long long tst0 = stamp();
+#endif
             const int b0 = (int)(j + G * (m_lo + (u32)sa)) - D0;  // this lane's text block at step sa
             u32 off = 16u * (u32)b0;                               // its byte offset in the text
             u32 ctr = (u32)b0 + 2;
@@ -372,6 +376,9 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
                 }
             }
             s0 = (u32)sb;  // (a block in the range's last step is stored at once: nothing is held past it)
+#if ENGINE_PROFILE
+            tsteady += stamp() - tst0;
+#endif
         }
 #if W8_LEAN_STEP
         if constexpr (W8 && FRAME == 0) {
@@ -593,7 +600,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         const unsigned long long tsg3 = stamp();
         PROF_ADD(16, tsg1 - tsg0), PROF_ADD(17, tsg2 - tsg1), PROF_ADD(18, tsg3 - tsg2), PROF_ADD(19, 1);
         // [20] the wave's steps, [21] of them in the steady form
-        PROF_ADD(20, Smax), PROF_ADD(21, sb > sa ? (u32)(sb - sa) : 0u);
+        PROF_ADD(20, Smax), PROF_ADD(21, sb > sa ? (u32)(sb - sa) : 0u), PROF_ADD(22, tsteady);
     }
 #endif
 }

@@ -74,6 +74,9 @@ def main():
               f"{p[17] / p[19]:.0f}, end {p[18] / p[19]:.0f} cycles each ({100 * p[16] / seg:.1f} / {100 * p[17] / seg:.1f} / "
               f"{100 * p[18] / seg:.1f} %)")
         print(f"  steps per segment {p[20] / p[19]:.2f}, of them steady {p[21] / p[19]:.2f} ({100 * p[21] / max(p[20], 1):.1f} %)")
+        if p[22] and p[21] and p[20] > p[21]:
+            print(f"  cycles per steady step {p[22] / p[21]:.0f}, per other step {(p[17] - p[22]) / (p[20] - p[21]):.0f}; "
+                  f"the other steps take {100 * (p[17] - p[22]) / p[17]:.1f} % of the steps' time")
     waves = 16
     print(f"  wave idle at unit-loop barrier: {p[4] / runs / waves:.0f} cycles/run/wave "
           f"({100 * p[4] / waves / max(p[2], 1):.1f} % of the unit loop)")
