@@ -473,3 +473,44 @@ def test_w8_g4_open_into_shifted_outputs_vs_fusion(ref, length, aad, key_size, p
     else:
         assert c["runs"]["w8_mk"] >= 0.5 * nkeys / 4, (c, nkeys)
     ks.free()
+
+
+@pytest.mark.parametrize("length,aad,shift", [(1200, 13, 16), (1000, 0, 1), (333, 40, 7)])
+def test_w8_g4_open_in_place_shifted_vs_fusion(ref, length, aad, shift):
+    """(round 6) The 4-lane open with line holding stores each block up to two steps after it was read: opened in place
+    (plaintext over its ciphertext) at offsets shifted by 16 x (i mod 8) or by odd byte counts, every record's plaintext
+    and ok byte equal fusion's, and the bytes between records untouched."""
+    rng = np.random.default_rng(8950 + length + shift)
+    n = 256 * 130
+    stride = (length + 16 + 127) // 128 * 128 + 128
+    recs = np.zeros(n, dtype=pa.RECORD_DTYPE)
+    recs["in_off"] = recs["out_off"] = (np.arange(n) * stride + (np.arange(n) * shift) % 128).astype(np.uint64)
+    recs["len"] = length
+    recs["aad_off"] = (np.arange(n) * max(aad, 1)).astype(np.uint32)
+    recs["aad_len"] = aad
+    recs["seq"] = rng.integers(0, 2**62, n, dtype=np.uint64)
+    key, iv = np.frombuffer(rng.bytes(16), np.uint8), np.frombuffer(rng.bytes(12), np.uint8)
+    arena = np.frombuffer(rng.bytes(n * stride + 128), np.uint8).copy()
+    aadb = np.frombuffer(rng.bytes(n * max(aad, 1) + 1), np.uint8)
+    sealed = arena.copy()
+    ref.run_batch(True, key, iv, 16, recs, arena, aadb, sealed, nthreads=8)  # in place: ciphertext and tag at in_off
+    victims = rng.choice(n, 12, replace=False)
+    for t, v in enumerate(victims):
+        sealed[int(recs[v]["in_off"]) + int(rng.integers(0, length + 16))] ^= 1 << (t % 8)
+    want = sealed.copy()
+    ref.run_batch(False, key, iv, 16, recs, sealed, aadb, want, ok=np.zeros(n, np.uint8), nthreads=8)
+    ks = pa.Keyset(key, iv, 16)
+    d_arena, d_recs, d_aad = dev(sealed), dev(recs), dev(aadb)
+    d_ok = empty(n, 0x55)
+    pa.debug_counters(reset=True)
+    pa.open_batch(ks, d_recs.data_ptr(), n, d_arena.data_ptr(), d_aad.data_ptr(), d_arena.data_ptr(), d_ok.data_ptr())
+    torch.cuda.synchronize()
+    c = pa.debug_counters(reset=True)
+    expect_ok = np.ones(n, np.uint8)
+    expect_ok[victims] = 0
+    assert np.array_equal(d_ok.cpu().numpy(), expect_ok)
+    got = d_arena.cpu().numpy()
+    bad = [i for i in range(n) if not np.array_equal(got[i * stride:(i + 1) * stride], want[i * stride:(i + 1) * stride])]
+    assert bad == [], f"{len(bad)} record slots differ from fusion, first {bad[:8]}"
+    assert c["runs"]["w8_g4"] >= 200, c
+    ks.free()
