@@ -242,6 +242,12 @@ __device__ __forceinline__ u32 lane_here()
 // "claim": one connection per wave, so its round keys stay in SGPRs). Run state: ctl[RC_MK] = connections (0: not an
 // MK run), RC_UNITS = claims; the claims (first record | count << 8 | slot << 16) at RUN_UBASE_OFF, the key entries of
 // slots 1.. at RUN_DONE_OFF (slot 0's at RUN_KEY_OFF, as any run's)
+// (round 6) the scan tries an MK run only from a connection of MK_MIN_FIRST records: connections of one or two records
+// stay cut into units, which spread over every wave where an MK run of such connections is one claim on one wave
+// (64K connections of 2 packets +3.7 %, 100,000 mixed records over 64K keys +3.1 %, profiles/r6/mk_min_first_ab.txt)
+#ifndef MK_MIN_FIRST
+#define MK_MIN_FIRST 3
+#endif
 #ifndef MK_RUNS
 #define MK_RUNS 1
 #endif

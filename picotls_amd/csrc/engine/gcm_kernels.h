@@ -392,7 +392,7 @@ __device__ __forceinline__ void scan_run(const BatchArgs &args, const ptls_mi355
     if constexpr (MK_RUNS && EXT == 5) {
         // (round 6) a connection of short uniform records, fewer than the workgroup's groups: join the next
         // connections into one multi-key whole run (scan_mk) instead of cutting it into units
-        if (args.multi_key && key < args.nkeys && n < (u32)WHOLE_MIN_RECS && smax < (u32)W8_MIN_STEPS &&
+        if (args.multi_key && key < args.nkeys && n >= (u32)MK_MIN_FIRST && n < (u32)WHOLE_MIN_RECS && smax < (u32)W8_MIN_STEPS &&
             smax <= smin + UNIFORM_SLACK && scan_mk<OPEN, FRAME>(args, p, end, rs, mkk, mks, mk_after))
             return;
     }
