@@ -260,8 +260,23 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
     // behind first, so that equal claims end together instead of in the issue order's age skew (a run's last wave
     // otherwise finishes alone on its SIMD)
     auto progress_prio = [&](u32 left) {
+        if constexpr (TREE_PRIO_BAND && W8) {
+            if (w8tree) {
+                const u32 q = left / TREE_PRIO_BAND;
+                const u32 lvl = TREE_PRIO_INV ? (q >= 3 ? 0u : 3u - q) : (q >= 3 ? 3u : q);
+                if (lvl == 3)
+                    __builtin_amdgcn_s_setprio(3);
+                else if (lvl == 2)
+                    __builtin_amdgcn_s_setprio(2);
+                else if (lvl == 1)
+                    __builtin_amdgcn_s_setprio(1);
+                else
+                    __builtin_amdgcn_s_setprio(0);
+                return;
+            }
+        }
         if constexpr (PROGRESS_PRIO && W8) {
-            if (w8tree)  // (the tree kernel's long whole runs: measured -2.3 % on tls16k with it)
+            if (w8tree)  // (the tree kernel's long whole runs take TREE_PRIO_BAND above: bands of 4 measured -2.3 %)
                 return;
             if (left > 3u * PROGRESS_PRIO)
                 __builtin_amdgcn_s_setprio(3);
@@ -518,7 +533,7 @@ __device__ __forceinline__ void gcm_segment(const BatchArgs &args, const lds_u8 
         __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (PROGRESS_PRIO && W8)
-        if (!w8tree)
+        if (!w8tree || TREE_PRIO_BAND)
             __builtin_amdgcn_s_setprio(0);
 #if ENGINE_PROFILE
     const unsigned long long tsg2 = stamp();
