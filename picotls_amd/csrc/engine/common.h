@@ -224,7 +224,7 @@ __device__ __forceinline__ u32 lane_here()
 // (round 6) the serial W8 kernels' waves issue by the steps left in their segment (s_setprio 3..0 in bands of this many
 // steps, segment.h): the waves of a SIMD then end equal claims together instead of in the order of their age, which
 // left a run's last wave alone on its SIMD. tls64k +4.3 %, quic64k +5.0 %, mixed +0.7 %, quic1200 +0.4 %; the tree
-// kernel keeps its issue order (tls16k -2.3 % with it) (profiles/r6/progress_prio_ab.txt); 0: off
+// kernel takes its own, wider bands (TREE_PRIO_BAND: with these, tls16k -2.3 %) (profiles/r6/progress_prio_ab.txt); 0: off
 #ifndef PROGRESS_PRIO
 #define PROGRESS_PRIO 4
 #endif
