@@ -228,11 +228,12 @@ __device__ __forceinline__ u32 lane_here()
 #ifndef PROGRESS_PRIO
 #define PROGRESS_PRIO 4
 #endif
-// ... and the tree kernel's (EXT 3, long whole records) in bands of TREE_PRIO_BAND steps: tls16k +0.4 / +0.7 %, AES-256
-// 16 KiB +0.6 %, 256K x 16 KiB +2.2 % on two boxes (bands of 4 measured -2.3 %; the waves nearest their segment's
-// end first, TREE_PRIO_INV, -1 to -2 %) (profiles/r6/tree_prio_ab.txt); 0: the tree kernel keeps its issue order
+// ... and the tree kernel's (EXT 3, long whole records) in bands of TREE_PRIO_BAND steps: 32 gave tls16k +0.4 / +0.7 %,
+// AES-256 16 KiB +0.6 %, 256K x 16 KiB +2.2 % on two boxes, 16 a further +0.25 to +0.8 % on tls16k (bands of 4
+// measured -2.3 %, of 64 -2 to -3 %; the waves nearest their segment's end first, TREE_PRIO_INV, -1 to -2 %)
+// (profiles/r6/tree_prio_ab.txt, tree_prio_band_ab.txt); 0: the tree kernel keeps its issue order
 #ifndef TREE_PRIO_BAND
-#define TREE_PRIO_BAND 32
+#define TREE_PRIO_BAND 16
 #endif
 #ifndef TREE_PRIO_INV
 #define TREE_PRIO_INV 0
